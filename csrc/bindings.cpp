@@ -1,0 +1,71 @@
+// pybind11 bindings for the gfx950 kernel library.
+// The ABI is raw device pointers (as Python ints from tensor.data_ptr()) plus
+// the hipStream_t of the caller's current stream, so the module links only
+// against the HIP runtime (torch's own libamdhip64, already loaded by
+// `import torch`), never against torch's C++ ABI. Every entry returns the HIP
+// error code of the launch; the Python wrappers raise on non-zero.
+#include <pybind11/pybind11.h>
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "kernels/api.h"
+
+namespace py = pybind11;
+#define P(x) reinterpret_cast<void*>(static_cast<uintptr_t>(x))
+#define CP(x) reinterpret_cast<const void*>(static_cast<uintptr_t>(x))
+#define FP(x) reinterpret_cast<float*>(static_cast<uintptr_t>(x))
+#define CFP(x) reinterpret_cast<const float*>(static_cast<uintptr_t>(x))
+#define IP(x) reinterpret_cast<int*>(static_cast<uintptr_t>(x))
+#define CIP(x) reinterpret_cast<const int*>(static_cast<uintptr_t>(x))
+#define ST(x) reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(x))
+typedef uint64_t u64;
+
+PYBIND11_MODULE(_dnn_hip, m) {
+  m.doc() = "distributed_neural_networks_amd HIP/CDNA4 kernels (gfx950)";
+  m.attr("arch") = "gfx950";
+
+  m.def("gemm_bf16", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N,
+                        int K, int act, int out_f32, u64 st) {
+    return dnn_gemm_bf16(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, out_f32, ST(st));
+  });
+  m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {
+    return dnn_silu_mul_packed(CP(gu), ld_in, P(out), ld_out, M, F, ST(st));
+  });
+  m.def("cifar_stage0", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
+    return dnn_cifar_stage0(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
+  });
+  m.def("cifar_head_tail", [](u64 hid, u64 w2p, u64 b2, u64 probs, u64 pred, int B, u64 st) {
+    return dnn_cifar_head_tail(CP(hid), CP(w2p), CFP(b2), FP(probs), IP(pred), B, ST(st));
+  });
+#ifdef DNN_HAVE_TRANSFORMER
+  m.def("layernorm", [](u64 x, int ldx, u64 w, u64 b, u64 y, int ldy, int M, int N, float eps, int rms, u64 st) {
+    return dnn_layernorm(CP(x), ldx, CFP(w), CFP(b), P(y), ldy, M, N, eps, rms, ST(st));
+  });
+  m.def("embed_gpt2", [](u64 idx, u64 wte, u64 wpe, u64 out, int B, int T, int d, u64 pos, u64 st) {
+    return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), ST(st));
+  });
+  m.def("qkv_split", [](u64 qkv, u64 q, u64 kc, u64 vc, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
+                        u64 cos, u64 sin, int rope, u64 st) {
+    return dnn_qkv_split(CP(qkv), P(q), P(kc), P(vc), B, T, H, Hkv, hd, S, CIP(pos), CFP(cos), CFP(sin), rope,
+                         ST(st));
+  });
+  m.def("flash_attn", [](u64 q, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
+                         float scale, u64 st) {
+    return dnn_flash_attn(CP(q), CP(kc), CP(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));
+  });
+  m.def("attn_decode", [](u64 q, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S, u64 lens,
+                          float scale, int splits, u64 ws, u64 st) {
+    return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st));
+  });
+  m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st) {
+    return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st));
+  });
+  m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, u64 st) {
+    return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, ST(st));
+  });
+  m.def("gemm_fp8", [](u64 A, u64 sa, u64 W, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N, int K,
+                       int act, u64 st) {
+    return dnn_gemm_fp8(CP(A), CFP(sa), CP(W), CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, ST(st));
+  });
+#endif
+}

@@ -1,0 +1,28 @@
+// C ABI of the kernel library (every function enqueues on `st` and returns the
+// hipError_t of the launch; 0 = success, negative = rejected shape).
+#pragma once
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias, const void* R,
+                  int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st);
+int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
+int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
+                     int B, int grid, hipStream_t st);
+int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
+                        hipStream_t st);
+int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N, float eps,
+                  int rms, hipStream_t st);
+int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d, const int* pos,
+                   hipStream_t st);
+int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
+                  const int* pos, const float* cos, const float* sin, int rope, hipStream_t st);
+int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv, int hd, int S,
+                   const int* pos, float scale, hipStream_t st);
+int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd, int S,
+                    const int* lens, float scale, int splits, float* ws, hipStream_t st);
+int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st);
+int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, hipStream_t st);
+int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,
+                 const void* R, int ldr, int M, int N, int K, int act, hipStream_t st);
+}

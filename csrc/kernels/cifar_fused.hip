@@ -1,0 +1,248 @@
+// CIFAR-10 ConvNet stage kernels for gfx950.
+//
+// Stage 0 (reference ModelPart0_2Node, cifar_model_parts.py:37-42):
+//   conv1(3->32,3x3,p1)+bias+ReLU+maxpool2 -> conv2(32->64,3x3,p1)+bias+ReLU+maxpool2
+//   -> flatten in NCHW order (c*64 + h*8 + w), ONE kernel, bf16 output (B,4096).
+// Both convolutions are implicit GEMMs on v_mfma_f32_32x32x16_bf16; the 32-row
+// M tile is a 4x8 pixel block so that the 2x2 max-pool is done inside each
+// lane's accumulator registers (C/D row = (g&3) + 8*(g>>2) + 4*(lane>>5)).
+// The per-image working set lives in LDS: padded input [3][34][34] bf16, the
+// pooled conv1 map as padded HWC [18][18][32] bf16 with a 16-B chunk XOR
+// swizzle (chunk ^ (Y&3)) that makes conv2's ds_read_b128 A-fragment reads
+// conflict-free, and an 8 KiB output staging buffer for coalesced stores.
+// conv2's B operand (64x288 weights) stays resident in VGPRs for the whole
+// persistent loop (one 32-channel N-tile per wave = 72 VGPRs); the next image
+// is prefetched into registers while conv2 runs.
+//
+// Stage 1 tail (reference ModelPart1_2Node, cifar_model_parts.py:53-58, plus the
+// host-side argmax of node.py:61/190, done per row here): after fc1+bias+ReLU
+// (gemm_bf16 with ACT_RELU), fc2(512->10)+bias+softmax+argmax on MFMA, 16 rows
+// per wave-iteration.
+#include "common.h"
+
+namespace dnn {
+
+constexpr int XIN_W = 34, XIN_PLANE = 34 * 34;              // padded input plane (elements)
+constexpr int XIN_BYTES = 3 * XIN_PLANE * 2;                 // 6936
+constexpr int XIN_OFF = 0;
+constexpr int ACT1_OFF = 6944;                               // 16-B aligned
+constexpr int ACT1_BYTES = 18 * 18 * 32 * 2;                 // 20736
+constexpr int OBUF_OFF = ACT1_OFF + ACT1_BYTES;              // 27680
+constexpr int S0_LDS = OBUF_OFF + 4096 * 2;                  // 35872
+
+__device__ __forceinline__ int act1_byte(int Y, int X, int c) {
+  return ACT1_OFF + (((Y * 18 + X) * 32) + ((((c >> 3) ^ (Y & 3))) << 3) + (c & 7)) * 2;
+}
+
+// conv1 A-operand offset (elements, relative to the pixel's top-left padded
+// position) of im2col column k = c*9 + ky*3 + kx (PyTorch weight flatten order).
+__device__ __forceinline__ constexpr int c1_off(int k) {
+  return (k / 9) * XIN_PLANE + ((k % 9) / 3) * XIN_W + (k % 3);
+}
+
+__global__ __launch_bounds__(256, 2) void cifar_stage0_kernel(
+    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
+    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B) {
+  __shared__ __attribute__((aligned(16))) char smem[S0_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  bf16_t* xin = reinterpret_cast<bf16_t*>(smem + XIN_OFF);
+
+  // Zero the halos once (interiors are rewritten per image; halos never are).
+  for (int i = tid; i < (ACT1_OFF) / 4; i += 256) reinterpret_cast<uint32_t*>(smem)[i] = 0u;
+  for (int i = tid; i < ACT1_BYTES / 4; i += 256) reinterpret_cast<uint32_t*>(smem + ACT1_OFF)[i] = 0u;
+
+  // Resident weights. conv1: B[k][oc] = w1p[oc][k], k in [0,32) (27 real).
+  bf16x8 w1f[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 32 + s * 16 + h * 8);
+  const float bias1 = b1[r32];
+  // conv2: this wave's N-tile (32 output channels), all 18 k-steps of 16.
+  const int nt = wave & 1;
+  const int oc2 = nt * 32 + r32;
+  bf16x8 w2f[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
+  const float bias2 = b2[oc2];
+
+  // Prefetch registers for one input image: 3072 fp32 = 768 float4, 3 per thread.
+  float4 pf[3];
+  int img = blockIdx.x;
+  if (img < B) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) pf[u] = reinterpret_cast<const float4*>(x + (size_t)img * 3072)[tid + u * 256];
+  }
+  __syncthreads();
+
+  for (; img < B; img += gridDim.x) {
+    // ---- input -> LDS (bf16, padded) ----
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = (tid + u * 256) * 4;      // flat fp32 index into [3][32][32]
+      const int c = e >> 10, y = (e >> 5) & 31, xx = e & 31;
+      bf16_t* d = xin + c * XIN_PLANE + (y + 1) * XIN_W + xx + 1;
+      d[0] = f2bf(pf[u].x); d[1] = f2bf(pf[u].y); d[2] = f2bf(pf[u].z); d[3] = f2bf(pf[u].w);
+    }
+    __syncthreads();
+
+    // ---- conv1 + bias + ReLU + pool -> act1 (HWC, padded, swizzled) ----
+    for (int t = wave; t < 32; t += 4) {
+      const int ty = t >> 2, tx = t & 3;
+      const int py = 4 * ty + (r32 >> 3), px = 8 * tx + (r32 & 7);   // output pixel of this lane's A row
+      const bf16_t* base = xin + py * XIN_W + px;                      // top-left of its 3x3x3 window
+      bf16x8 a0, a1;
+      // k-step 0 covers k in [0,16), k-step 1 k in [16,32) (real up to 26);
+      // lane half h takes k = 16*s + 8*h + j. All offsets are compile-time.
+      if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a0[j] = (short)base[c1_off(j)]; a1[j] = (short)base[c1_off(16 + j)]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a0[j] = (short)base[c1_off(8 + j)];
+          a1[j] = j < 3 ? (short)base[c1_off(24 + (j < 3 ? j : 0))] : (short)0;
+        }
+      }
+      f32x16 acc = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w1f[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w1f[1], acc, 0, 0, 0);
+      // lane holds channel r32; reg g -> pixel (y=g>>2, x=(g&3)+4h) of the 4x8 block
+#pragma unroll
+      for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+        for (int qx = 0; qx < 2; ++qx) {
+          const int g0 = (2 * qy) * 4 + 2 * qx;
+          float v = fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5]));
+          v = fmaxf(v + bias1, 0.f);
+          const int Y = 2 * ty + qy + 1, X = 4 * tx + 2 * h + qx + 1;
+          *reinterpret_cast<bf16_t*>(smem + act1_byte(Y, X, r32)) = f2bf(v);
+        }
+    }
+    __syncthreads();
+
+    // prefetch the next image while conv2 runs
+    const int nimg = img + gridDim.x;
+    if (nimg < B) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) pf[u] = reinterpret_cast<const float4*>(x + (size_t)nimg * 3072)[tid + u * 256];
+    }
+
+    // ---- conv2 + bias + ReLU + pool -> obuf (NCHW flatten order) ----
+    {
+      f32x16 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
+      const int mt0 = (wave >> 1) * 4;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        const int kk = s >> 1, ky = kk / 3, kx = kk % 3;
+        const int chunk = (s & 1) * 2 + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+          const int Y = 4 * ty2 + (r32 >> 3) + ky, X = 8 * tx2 + (r32 & 7) + kx;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + ACT1_OFF + ((Y * 18 + X) * 32 + ((chunk ^ (Y & 3)) << 3)) * 2);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2f[s], acc[i], 0, 0, 0);
+        }
+      }
+      bf16_t* obuf = reinterpret_cast<bf16_t*>(smem + OBUF_OFF);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+#pragma unroll
+        for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+          for (int qx = 0; qx < 2; ++qx) {
+            const int g0 = (2 * qy) * 4 + 2 * qx;
+            float v = fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5]));
+            v = fmaxf(v + bias2, 0.f);
+            const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h + qx;
+            obuf[oc2 * 64 + PY * 8 + PX] = f2bf(v);
+          }
+      }
+    }
+    __syncthreads();
+    // ---- coalesced store of the 8 KiB output row ----
+    {
+      const int4* src = reinterpret_cast<const int4*>(smem + OBUF_OFF);
+      int4* dst = reinterpret_cast<int4*>(out + (size_t)img * 4096);
+      dst[tid] = src[tid];
+      dst[tid + 256] = src[tid + 256];
+    }
+    // next iteration's input write touches only xin (not read after conv1)
+  }
+}
+
+// fc2 (512->10) + bias + softmax + argmax. hid: (B,512) bf16 (fc1+ReLU output).
+// One wave handles 16 rows per iteration with mfma_f32_16x16x32_bf16:
+// A = hid rows (lane: row l&15, k 8*(l>>4)+j), B = W2 padded to 16 classes held
+// in VGPRs. Softmax across each 16-lane row group with xor-shuffles.
+__global__ __launch_bounds__(256) void cifar_head_tail_kernel(const bf16_t* __restrict__ hid, const bf16_t* __restrict__ w2p,
+                                                              const float* __restrict__ b2, float* __restrict__ probs,
+                                                              int* __restrict__ pred, int B) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int col = lane & 15, kq = (lane >> 4) * 8;
+  bf16x8 wf[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wf[s] = *reinterpret_cast<const bf16x8*>(w2p + col * 512 + s * 32 + kq);
+  const float bias = col < 10 ? b2[col] : 0.f;
+  for (int r0 = gw * 16; r0 < B; r0 += nw * 16) {
+    const int row = r0 + (lane & 15);
+    const int rc = row < B ? row : B - 1;
+    const bf16_t* ap = hid + (size_t)rc * 512 + kq;
+    bf16x8 a[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a[s] = *reinterpret_cast<const bf16x8*>(ap + s * 32);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], wf[s], acc, 0, 0, 0);
+    // acc[r] = logit(row = r0 + (lane>>4)*4 + r, class = col)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = col < 10 ? acc[r] + bias : -INFINITY;
+      float mx = z;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float e = col < 10 ? __expf(z - mx) : 0.f;
+      float sum = e;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+      // argmax: smallest class index attaining the max (numpy semantics)
+      int cand = (z == mx) ? col : 16;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+      const int m = r0 + (lane >> 4) * 4 + r;
+      if (m < B) {
+        if (col < 10) probs[(size_t)m * 10 + col] = e / sum;
+        if (col == 0) pred[m] = cand;
+      }
+    }
+  }
+}
+
+}  // namespace dnn
+
+using namespace dnn;
+
+extern "C" int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                                const float* b2, int B, int grid, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (grid <= 0) grid = 512;
+  if (grid > B) grid = B;
+  hipLaunchKernelGGL(cifar_stage0_kernel, dim3(grid), dim3(256), 0, st, x, (bf16_t*)out, (const bf16_t*)w1p, b1,
+                     (const bf16_t*)w2p, b2, B);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
+                                   hipStream_t st) {
+  if (B <= 0) return 0;
+  int waves = (B + 15) / 16;
+  int blocks = (waves + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(cifar_head_tail_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)hid, (const bf16_t*)w2p,
+                     b2, probs, pred, B);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,60 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels.
+// Wave = 64 lanes. All bf16 data is handled as raw 16-bit patterns and widened
+// with shifts; narrowing uses the compiler's v_cvt_pk_bf16_f32 (RNE, NaN-safe).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace dnn {
+
+typedef uint16_t bf16_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ float bf2f_s(short v) { return __uint_as_float(((uint32_t)(uint16_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 16-byte async global->LDS copy. `lds_wave_base` must be wave-uniform: lane i
+// lands at lds_wave_base + 16*i (glds semantics, cdna_hip_programming.md §5).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_wave_base, 16, 0, 0);
+}
+
+// Bijective XCD-aware block remap: blocks that the dispatcher places on the same
+// XCD (b % 8 equal) get a contiguous range of logical tile ids (guide §5, T1).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+}  // namespace dnn

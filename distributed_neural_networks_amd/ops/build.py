@@ -1,0 +1,101 @@
+"""Build the in-tree HIP kernel library ``_dnn_hip`` for gfx950 with hipcc.
+
+No torch cpp_extension (it hipifies sources); plain ``hipcc --offload-arch=gfx950``
+per translation unit, incremental on mtimes, then one shared-object link into
+the package directory so the built ``.so`` ships with the repo snapshot to the
+GPU box.  Usage: ``python -m distributed_neural_networks_amd.ops.build [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "distributed_neural_networks_amd")
+BUILD = os.path.join(ROOT, "build", "hip")
+ARCH = os.environ.get("DNN_OFFLOAD_ARCH", "gfx950")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+LIB_PATH = os.path.join(PKG, "_dnn_hip" + EXT_SUFFIX)
+
+TRANSFORMER_SRCS = ("norm_embed.hip", "attention.hip", "sampler.hip", "gemm_fp8.hip")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.exists(c) or c == "hipcc"):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def sources() -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]
+
+
+def _flags(src: str) -> List[str]:
+    f = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + CSRC, "-Wno-unused-result",
+         "-Wno-unused-command-line-argument"]
+    have_tf = all(os.path.exists(os.path.join(CSRC, "kernels", s)) for s in TRANSFORMER_SRCS)
+    if have_tf:
+        f.append("-DDNN_HAVE_TRANSFORMER")
+    if src.endswith("bindings.cpp"):
+        import pybind11
+        f += ["-x", "hip", "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+    return f
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max([os.path.getmtime(h) for h in hs] + [0.0])
+
+
+def _obj(src: str) -> str:
+    return os.path.join(BUILD, os.path.basename(src) + ".o")
+
+
+def _compile(src: str, force: bool, hm: float) -> str:
+    obj = _obj(src)
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hm):
+        return obj
+    cmd = [_hipcc()] + _flags(src) + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sources()
+    hm = _headers_mtime()
+    jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 4, 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force, hm), srcs))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + ["-o", LIB_PATH]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[build] {LIB_PATH} ({len(objs)} objects, arch {ARCH})")
+    return LIB_PATH
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    build(a.force, a.jobs)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,64 @@
+"""bf16 MFMA GEMM with fused epilogues (``csrc/kernels/gemm_bf16.hip``).
+
+``linear(x, w)`` computes ``x @ w.T (+bias) -> act (+residual)`` with ``w`` in
+``nn.Linear`` layout ``[out, in]``; rows of ``x`` may be strided (``x.stride(0)``),
+the last dim must be contiguous and K a multiple of 64.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_SILU_MUL = 0, 1, 2, 3
+_ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "silu_mul": ACT_SILU_MUL}
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
+           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    a = _ACTS[act] if not isinstance(act, int) else act
+    x2 = x.reshape(-1, x.shape[-1]) if x.dim() != 2 else x
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"linear: x {tuple(x2.shape)} vs w {tuple(w.shape)}")
+    if K % 64:
+        raise ValueError(f"linear: K={K} must be a multiple of 64")
+    if x2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("linear: bf16 operands required")
+    if x2.stride(1) != 1 or w.stride(1) != 1:
+        raise ValueError("linear: inner dims must be contiguous")
+    Nout = N // 2 if a == ACT_SILU_MUL else N
+    if out is None:
+        out = torch.empty((M, Nout), dtype=out_dtype, device=x.device)
+    o2 = out.reshape(-1, out.shape[-1]) if out.dim() != 2 else out
+    if bias is not None and bias.dtype != torch.float32:
+        raise TypeError("linear: bias must be fp32")
+    r2 = None
+    if residual is not None:
+        r2 = residual.reshape(-1, residual.shape[-1]) if residual.dim() != 2 else residual
+    if a == ACT_SILU_MUL and M <= 16:
+        # skinny path: packed gate|up GEMM then the elementwise SwiGLU
+        tmp = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+        check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(tmp), N, 0, 0, 0, M, N, K,
+                              ACT_NONE, 0, stream_ptr()), "gemm_bf16")
+        check(lib().silu_mul_packed(ptr(tmp), N, ptr(o2), o2.stride(0), M, Nout, stream_ptr()), "silu_mul")
+        return out
+    check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
+                          ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
+                          1 if o2.dtype == torch.float32 else 0, stream_ptr()), "gemm_bf16")
+    return out
+
+
+def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """Interleave gate/up rows in 16-row groups: [g0..g15, u0..u15, g16..g31, ...]
+    so the GEMM epilogue sees matching gate/up columns in one lane (ACT_SILU_MUL)."""
+    F, K = gate.shape
+    if F % 16:
+        raise ValueError("ffn dim must be a multiple of 16")
+    g = gate.reshape(F // 16, 16, K)
+    u = up.reshape(F // 16, 16, K)
+    return torch.stack([g, u], dim=1).reshape(2 * F, K).contiguous()
