@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: CIFAR-10 ConvNet 2-stage pipeline inference, images/s.
+
+Metric/config from BASELINE.json (the reference's only measured headline:
+CIFAR-10 2-stage images/s; 3.40-4.15 k img/s on CPU over localhost gRPC,
+BASELINE.md).  Synthetic fp32 images, random-init weights of the reference
+architecture, bf16 compute on the fused gfx950 kernels.  Every timed step runs
+the complete forward of both stages (conv stage + fc/softmax/argmax stage) on
+fresh launches; nothing is cached across steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Placements:
+* N = 1: both stages colocated on the GPU, one HIP graph per step.
+* N > 1 (one process per GPU, RCCL): ``interleaved`` (default) — N pipelines,
+  pipeline r's stage 0 on GPU r and its stage 1 spread over the other N-1
+  GPUs; the stage hop is one all-to-all over the xGMI mesh per microbatch
+  (each GPU uses all of its links instead of one, and every GPU hosts a
+  stage-0 and a stage-1 so the 73/27 stage imbalance cancels), overlapped with
+  the next microbatch's stage-0 compute.  ``linear`` — N/2 replicas of the
+  reference topology (stage 0 on GPU 2k, stage 1 on GPU 2k+1, isend/irecv).
+Scaling is weak: each GPU sources ``--batch`` images per step.
+
+``--model gpt2`` runs the GPT-2 4-stage token throughput bench instead
+(bench/gpt_bench.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+BASELINE_IMG_S = 4150.0  # reference CIFAR-10 2-stage, best batch (255), CPU gRPC
+METRIC = "images/sec CIFAR-10 2-stage"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="images sourced per GPU per step")
+    ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--placement", default="interleaved", choices=["interleaved", "linear"])
+    ap.add_argument("--model", default="cifar10")
+    ap.add_argument("--latency_iters", type=int, default=200)
+    return ap.parse_args()
+
+
+def dist_setup(n):
+    from distributed_neural_networks_amd.parallel import comm
+    if n > 1 or "WORLD_SIZE" in os.environ:
+        info = comm.init("nccl")
+    else:
+        torch.cuda.set_device(0)
+        info = comm.DistInfo(0, 1, 0, "none", torch.device("cuda", 0))
+    return info
+
+
+def stages_for(device):
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
+    s0 = CifarHipStage(ckpt.random_stage_state_dict("cifar10", 0, 1, True, False, 0), 0, 1, device)
+    s1 = CifarHipStage(ckpt.random_stage_state_dict("cifar10", 2, 3, False, True, 0), 2, 3, device)
+    return s0, s1
+
+
+def sync_time(info):
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if info.world > 1:
+        dist.barrier(device_ids=[info.device.index])
+        torch.cuda.synchronize()
+    return time.perf_counter()
+
+
+def max_over_ranks(info, v):
+    import torch.distributed as dist
+    if info.world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=info.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_colocated(args, info):
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    dev = info.device
+    s0, s1 = stages_for(dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    pipe = ColocatedPipeline([s0, s1], args.batch)
+    pipe.x.copy_(torch.randn(pipe.x.shape, device=dev, generator=g))
+    pipe.capture()
+    for _ in range(args.warmup):
+        pipe()
+    t0 = sync_time(info)
+    for _ in range(args.steps):
+        pipe()
+    t1 = sync_time(info)
+    # p50 single-image pipeline latency (both stages, one graph replay)
+    lat = ColocatedPipeline([s0, s1], 1)
+    lat.x.copy_(torch.randn(lat.x.shape, device=dev, generator=g))
+    lat.capture()
+    ts = []
+    for _ in range(args.latency_iters):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        lat()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - a)
+    return t1 - t0, args.batch, statistics.median(ts) * 1e3, "pp2-colocated"
+
+
+def bench_interleaved(args, info):
+    import torch.distributed as dist
+    dev, N, r = info.device, info.world, info.rank
+    s0, s1 = stages_for(dev)
+    M = max(1, args.microbatches)
+    mb = args.batch // M
+    per_peer = mb // (N - 1)
+    mb = per_peer * (N - 1)
+    g = torch.Generator(device=dev).manual_seed(1 + r)
+    xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
+    y0 = [torch.empty((mb, 4096), dtype=torch.bfloat16, device=dev) for _ in range(M)]
+    rx = [torch.empty((mb, 4096), dtype=torch.bfloat16, device=dev) for _ in range(M)]
+    probs = [torch.empty((mb, 10), device=dev) for _ in range(M)]
+    splits = [0 if p == r else per_peer for p in range(N)]
+
+    def step():
+        works = []
+        for i in range(M):
+            s0.forward(xs[i], y0[i])
+            works.append(dist.all_to_all_single(rx[i], y0[i], splits, splits, async_op=True))
+            if i > 0:
+                works[i - 1].wait()
+                s1.forward(rx[i - 1], probs[i - 1])
+        works[M - 1].wait()
+        s1.forward(rx[M - 1], probs[M - 1])
+
+    for _ in range(args.warmup):
+        step()
+    t0 = sync_time(info)
+    for _ in range(args.steps):
+        step()
+    t1 = sync_time(info)
+    # latency: one image per peer through stage0 -> all-to-all -> stage1
+    lx = torch.randn((N - 1, 3, 32, 32), device=dev, generator=g)
+    ly = torch.empty((N - 1, 4096), dtype=torch.bfloat16, device=dev)
+    lr = torch.empty_like(ly)
+    lp = torch.empty((N - 1, 10), device=dev)
+    one = [0 if p == r else 1 for p in range(N)]
+    ts = []
+    for _ in range(min(args.latency_iters, 100)):
+        sync_time(info)
+        a = time.perf_counter()
+        s0.forward(lx, ly)
+        dist.all_to_all_single(lr, ly, one, one)
+        s1.forward(lr, lp)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - a)
+    return t1 - t0, mb * M, statistics.median(ts) * 1e3, f"pp2-interleaved-a2a-x{N}"
+
+
+def bench_linear(args, info):
+    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.runtime.pipeline import run_stage_stream
+    dev, N, r = info.device, info.world, info.rank
+    if N % 2:
+        raise SystemExit("linear placement needs an even number of GPUs")
+    s0, s1 = stages_for(dev)
+    stage_idx = r % 2
+    st = s0 if stage_idx == 0 else s1
+    M = max(1, args.microbatches)
+    mb = args.batch * 2 // M  # a pair sources 2*batch images per step (weak scaling per GPU)
+    g = torch.Generator(device=dev).manual_seed(1 + r)
+    xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)] if stage_idx == 0 else None
+    prev = P2PLink(r - 1, dev) if stage_idx == 1 else None
+    nxt = P2PLink(r + 1, dev) if stage_idx == 0 else None
+
+    def step():
+        run_stage_stream(st, M, mb, prev, nxt, source=(lambda i: xs[i]) if xs else None, depth=2)
+
+    for _ in range(args.warmup):
+        step()
+    t0 = sync_time(info)
+    for _ in range(args.steps):
+        step()
+    t1 = sync_time(info)
+    return t1 - t0, mb * M // 2, float("nan"), f"pp2-linear-x{N // 2}"
+
+
+def main():
+    args = parse()
+    if args.model != "cifar10":
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        import gpt_bench
+        return gpt_bench.main(args)
+    info = dist_setup(args.gpus)
+    N = info.world
+    if N == 1:
+        el, imgs_per_gpu, p50, par = bench_colocated(args, info)
+    elif args.placement == "interleaved":
+        el, imgs_per_gpu, p50, par = bench_interleaved(args, info)
+    else:
+        el, imgs_per_gpu, p50, par = bench_linear(args, info)
+    el = max_over_ranks(info, el)
+    total = imgs_per_gpu * N * args.steps
+    value = total / el
+    if info.rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
+            "dtype": "bf16", "data": "synthetic (random fp32 images, random-init weights)",
+            "p50_latency_ms": None if p50 != p50 else round(p50, 4),
+            "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
+                       "global_batch": imgs_per_gpu * N, "seq_len": None, "parallelism": par,
+                       "stages": 2, "microbatches": args.microbatches if N > 1 else 1},
+        }
+        print(json.dumps(out), flush=True)
+    if N > 1:
+        from distributed_neural_networks_amd.parallel import comm
+        comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

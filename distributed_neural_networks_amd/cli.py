@@ -1,0 +1,398 @@
+"""``node.py`` entry point: one pipeline stage per process (reference CLI).
+
+``python node.py --node_id ID --config PATH [--input_image PATH]`` behaves like
+the reference (``node.py:210-364``): banner, per-stage weight load, gRPC
+server, and stage 0 initiates inference and prints
+``[id] ***** FINAL PREDICTION (Index): k *****``.  Additive flags only.
+
+Transports (config ``transport``):
+
+* ``grpc`` (default, the reference's): nested ``SendTensor`` RPC chain, CPU or
+  GPU compute per node; reference peers interoperate.
+* ``colocated``: the process of the node given by ``--node_id`` hosts every
+  stage on one GPU (HIP graph per step); other nodes have nothing to run.
+* ``rccl`` / ``gloo``: one rank per stage (rank = ``part_index``), activations
+  move with ``torch.distributed`` P2P (RCCL over xGMI on MI355X, gloo on CPU);
+  the last stage returns predictions over the back-edge to
+  ``return_to_node_id`` (resolved but unused in the reference, ``node.py:272-277``).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import sys
+import traceback
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import checkpoint as ckpt
+from .config import ConfigError, NodeContext, banner, load_node
+from .models import cifar, default_ranges, model_info
+from .utils.log import log, set_quiet
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X pipeline-parallel inference node")
+    p.add_argument("--node_id", required=True, help="Unique ID for this node (e.g., node1)")
+    p.add_argument("--config", required=True, help="Path to the JSON configuration file")
+    p.add_argument("--input_image", help="Path to input image (only used by node with part_index 0)")
+    # additive
+    p.add_argument("--num_requests", type=int, default=1, help="requests stage 0 sends (default 1)")
+    p.add_argument("--prompt", default=None, help="GPT/Llama: comma-separated token ids (default: random)")
+    p.add_argument("--shutdown_pipeline", action="store_true",
+                   help="stage 0 asks all peers to exit after its requests complete")
+    p.add_argument("--serve_seconds", type=float, default=None, help="non-initiating nodes exit after this long")
+    p.add_argument("--device", default=None, help="override device: cpu | cuda | cuda:N")
+    p.add_argument("--quiet", action="store_true")
+    return p
+
+
+# --------------------------------------------------------------------------- input
+def load_image(path: Optional[str], nid: str) -> torch.Tensor:
+    """Resize(32,32) + ToTensor + Normalize(0.5,0.5) without torchvision
+    (reference transform, ``node.py:142-144``); dummy ``randn`` on failure (``:149-154``)."""
+    try:
+        from PIL import Image
+        img = Image.open(path).convert("RGB").resize((32, 32), Image.BILINEAR)
+        a = np.asarray(img, dtype=np.float32) / 255.0
+        t = torch.from_numpy(a).permute(2, 0, 1).contiguous()
+        t = (t - 0.5) / 0.5
+        t = t.unsqueeze(0)
+        log(f"[{nid}] Loaded input image '{path}', shape: {t.shape}")
+        return t
+    except FileNotFoundError:
+        log(f"[{nid}] Input image '{path}' not found. Using dummy data.")
+    except Exception as e:  # noqa: BLE001
+        log(f"[{nid}] Error loading image: {e}. Using dummy data.")
+    return torch.randn(1, 3, 32, 32)
+
+
+def make_prompt(ctx: NodeContext, prompt: Optional[str]) -> torch.Tensor:
+    info = model_info(ctx.pipeline.model)
+    if prompt:
+        ids = [int(v) for v in prompt.split(",") if v.strip()]
+        return torch.tensor([ids], dtype=torch.int64)
+    g = torch.Generator().manual_seed(1234)
+    T = ctx.pipeline.prompt_len or ctx.pipeline.seq_len
+    return torch.randint(0, info.cfg.vocab_size, (ctx.pipeline.micro_batch_size, T), generator=g)
+
+
+# --------------------------------------------------------------------------- stages
+def stage_ranges(ctx: NodeContext) -> List[Tuple[int, int]]:
+    from .parallel.partition import resolve_ranges
+    pipe = ctx.pipeline
+    info = model_info(pipe.model)
+    given = [n.layers for n in pipe.stages]
+    if all(g is None for g in given):
+        return default_ranges(pipe.model, pipe.num_parts)
+    return resolve_ranges(info.num_layers, pipe.num_parts, given)
+
+
+def pick_device(ctx: NodeContext, override: Optional[str]) -> torch.device:
+    if override:
+        return torch.device(override)
+    if torch.cuda.is_available() and ctx.pipeline.transport != "gloo":
+        idx = ctx.node.device if ctx.node.device is not None else 0
+        if ctx.pipeline.transport == "rccl" and ctx.node.device is None:
+            idx = ctx.part_index % torch.cuda.device_count()
+        return torch.device("cuda", idx)
+    return torch.device("cpu")
+
+
+def load_stage_weights(ctx: NodeContext, part: int, ranges, full_sd=None):
+    """Per-stage weights; prints the reference's load messages (``node.py:294-317``)."""
+    pipe = ctx.pipeline
+    a, b = ranges[part]
+    first, last = part == 0, part == pipe.num_parts - 1
+    if ckpt.is_synthetic(pipe.model_weights):
+        log(f"[{ctx.node_id}] Using synthetic random-init weights (seed {ckpt.synthetic_seed(pipe.model_weights)})")
+        return ckpt.random_stage_state_dict(pipe.model, a, b, first, last, ckpt.synthetic_seed(pipe.model_weights)), full_sd
+    if full_sd is None:
+        log(f"[{ctx.node_id}] Loading full state dict...")
+        full_sd = ckpt.load_full_state_dict(pipe.model_weights)
+    log(f"[{ctx.node_id}] Loading model part {part}...")
+    sd = ckpt.stage_state_dict(pipe.model, full_sd, a, b, first, last)
+    unexpected = ckpt.unexpected_keys(pipe.model, full_sd, a, b, first, last)
+    if pipe.model == "cifar10" and pipe.num_parts == 2:
+        log(f"[{ctx.node_id}] Expect warnings for {'fc1, fc2' if part == 0 else 'conv1, conv2'} weights "
+            f"(loaded by Node {1 - part})")
+    if unexpected:
+        log(f"[{ctx.node_id}] WARNING: Unexpected keys loading state dict: {unexpected}")
+    return sd, full_sd
+
+
+def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_sd=None):
+    from .runtime.stages import CifarHipStage, TorchStage
+    pipe = ctx.pipeline
+    a, b = ranges[part]
+    first, last = part == 0, part == pipe.num_parts - 1
+    sd, full_sd = load_stage_weights(ctx, part, ranges, full_sd)
+    fam = model_info(pipe.model).family
+    if device.type == "cuda":
+        if fam == "cifar":
+            st = CifarHipStage(sd, a, b, device)
+        else:
+            from .runtime.transformer import build_device_stage
+            st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype)
+    else:
+        st = TorchStage(pipe.model, sd, a, b, first, last, device)
+    log(f"[{ctx.node_id}] Successfully loaded weights into stage {part} (layers [{a},{b}]) on {device}.")
+    return st, full_sd
+
+
+def _forward_fn(stage, fam: str):
+    """(tensor) -> (output tensor, per-row prediction or None)."""
+    from .runtime.stages import StageOutput
+
+    def fwd(x):
+        x = x.to(stage.device)
+        if fam == "cifar" and not stage.first and stage.device.type == "cuda":
+            x = x.to(torch.bfloat16)
+        y = stage.forward(x)
+        if isinstance(y, StageOutput):
+            if stage.device.type == "cuda":
+                torch.cuda.synchronize(stage.device)
+            return y.probs, y.pred.cpu()
+        return y, None
+    return fwd
+
+
+# --------------------------------------------------------------------------- transports
+async def run_grpc(ctx: NodeContext, args, stage) -> int:
+    from .control.service import NodeClient, NodeServicer, decode_prediction, start_server, SHUTDOWN_MSG
+    from .wire import codec, proto
+    nid = ctx.node_id
+    fam = model_info(ctx.pipeline.model).family
+    fwd = _forward_fn(stage, fam)
+    servicer = NodeServicer(nid, fwd, ctx.is_last, ctx.next_address)
+    listen = f"[::]:{ctx.port}"
+    try:
+        server = await start_server(servicer, ctx.port)
+        log(f"[{nid}] Starting gRPC server listening on {listen}")
+        log(f"[{nid}] Server started successfully.")
+    except RuntimeError as e:
+        log(f"!!! [{nid}] CRITICAL ERROR: Failed to bind server to {listen}: {e}")
+        log(f"!!! Check if port {ctx.port} is in use or network issues.")
+        return 1
+    rc = 0
+    try:
+        if ctx.part_index == 0 and (args.input_image or fam != "cifar"):
+            rc = await initiate(ctx, args, stage, fwd, fam)
+            if args.shutdown_pipeline:
+                for n in ctx.pipeline.nodes:
+                    if n.id != nid:
+                        c = NodeClient(n.address)
+                        try:
+                            await c.message(proto.MessageRequest(sender_id=nid, message_text=SHUTDOWN_MSG), timeout=5)
+                        except Exception:  # noqa: BLE001
+                            pass
+                        await c.close()
+            return rc
+        if ctx.part_index == 0:
+            log("WARNING: Node 0 needs --input_image to start inference. Server will run, but no inference initiated.")
+        log(f"[{nid}] Running event loop...")
+        waiter = asyncio.ensure_future(servicer.shutdown_event.wait())
+        await asyncio.wait([waiter], timeout=args.serve_seconds)
+        return 0
+    finally:
+        log(f"[{nid}] Attempting server shutdown...")
+        await servicer.close()
+        await server.stop(grace=1)
+        log(f"[{nid}] Server shutdown complete.")
+
+
+async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
+    """Stage-0 driver (reference ``initiate_inference``, ``node.py:137-200``)."""
+    from .control.service import NodeClient, decode_prediction
+    from .wire import codec, proto
+    nid = ctx.node_id
+    log(f"\n[{nid}] Initiating inference...")
+    if ctx.num_parts > 1 and not ctx.next_address:
+        log(f"[{nid}] ERROR: Cannot initiate inference, NEXT_NODE_ADDRESS is not set.")
+        return 1
+    client = NodeClient(ctx.next_address) if ctx.num_parts > 1 else None
+    if client is not None and not await client.wait_ready(60.0):
+        log(f"!!! [{nid}] next node {ctx.next_address} did not become healthy")
+        await client.close()
+        return 1
+    rc = 0
+    for r in range(args.num_requests):
+        x = load_image(args.input_image, nid) if fam == "cifar" else make_prompt(ctx, args.prompt)
+        log(f"[{nid}] Running model part {ctx.part_index}...")
+        loop = asyncio.get_running_loop()
+        out, pred = await loop.run_in_executor(None, fwd, x)
+        if client is None:  # single-stage pipeline
+            p = pred.tolist()
+            log(f"[{nid}] ***** FINAL PREDICTION (Index): {p[0] if len(p) == 1 else p} *****")
+            continue
+        out = out.detach().cpu()
+        if out.is_floating_point():
+            out = out.float()
+        log(f"[{nid}] Computed intermediate output shape: {tuple(out.shape)}")
+        log(f"[{nid}] Sending intermediate tensor to {ctx.next_address}...")
+        req = proto.TensorRequest(request_id=f"{ctx.pipeline.model}_pipe_{ctx.num_parts}node_{r:03d}",
+                                  tensor=codec.encode(out))
+        try:
+            import grpc
+            resp = await client.send_tensor(req)
+            log(f"[{nid}] Received final status from pipeline: {resp.status}")
+            pred = decode_prediction(resp)
+            if pred is None:
+                log(f"[{nid}] Final result status received, but tensor not included in response.")
+                rc = 1
+            else:
+                p = pred.tolist()
+                log(f"[{nid}] ***** FINAL PREDICTION (Index): {p[0] if len(p) == 1 else p} *****")
+        except Exception as e:  # noqa: BLE001
+            log(f"!!! [{nid}] SendTensor RPC failed during initiation: {e}")
+            rc = 1
+    await client.close() if client is not None else None
+    return rc
+
+
+def run_colocated(ctx: NodeContext, args, device) -> int:
+    from .runtime.pipeline import ColocatedPipeline
+    nid = ctx.node_id
+    if ctx.part_index != 0:
+        log(f"[{nid}] colocated transport: all stages run in the part-0 process; nothing to do here.")
+        return 0
+    ranges = stage_ranges(ctx)
+    fam = model_info(ctx.pipeline.model).family
+    full = None
+    stages = []
+    for p in range(ctx.num_parts):
+        st, full = build_stage(ctx, p, ranges, device, full)
+        stages.append(st)
+    if fam != "cifar":
+        from .runtime.transformer import run_generate_colocated
+        return run_generate_colocated(ctx, args, stages, device)
+    if device.type == "cuda" and ctx.num_parts == 2:
+        # merge the reference split into one fused stage pair on the device
+        pass
+    for r in range(args.num_requests):
+        x = load_image(args.input_image, nid)
+        pipe = ColocatedPipeline(stages, x.shape[0])
+        out = pipe(x.to(device))
+        pred = out.pred.cpu().tolist()
+        log(f"[{nid}] ***** FINAL PREDICTION (Index): {pred[0] if len(pred) == 1 else pred} *****")
+    return 0
+
+
+def run_dist(ctx: NodeContext, args, device) -> int:
+    """One rank per stage over torch.distributed P2P (RCCL/gloo)."""
+    from .parallel import comm
+    from .parallel.links import KIND_DATA, KIND_STOP, P2PLink
+    nid = ctx.node_id
+    pipe = ctx.pipeline
+    backend = "nccl" if pipe.transport == "rccl" else "gloo"
+    if backend == "nccl" and device.type != "cuda":
+        log(f"[{nid}] ERROR: transport 'rccl' needs a GPU")
+        return 1
+    if backend == "gloo":
+        device = torch.device("cpu")
+    s0 = pipe.stage(0)
+    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host,
+                     master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
+    ranges = stage_ranges(ctx)
+    stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device)
+    fam = model_info(pipe.model).family
+    if fam != "cifar":
+        from .runtime.transformer import run_generate_dist
+        rc = run_generate_dist(ctx, args, stage, info)
+        comm.shutdown()
+        return rc
+    ret_rank = 0
+    if pipe.return_to_node_id and pipe.by_id(pipe.return_to_node_id):
+        ret_rank = pipe.by_id(pipe.return_to_node_id).part_index
+    prev = P2PLink(ctx.part_index - 1, info.device) if ctx.part_index > 0 else None
+    nxt = P2PLink(ctx.part_index + 1, info.device) if not ctx.is_last else None
+    back = P2PLink(ret_rank, info.device) if (ctx.is_last and ret_rank != ctx.part_index) else None
+    comm.barrier(info)
+    log(f"[{nid}] rank {info.rank}/{info.world} ready on {info.device} (backend {backend})")
+    rc = 0
+    try:
+        if ctx.part_index == 0:
+            for r in range(args.num_requests):
+                x = load_image(args.input_image, nid).to(info.device)
+                y = stage.forward(x)
+                if ctx.num_parts == 1:
+                    preds = y.pred.cpu().tolist()
+                else:
+                    nxt.send_header(KIND_DATA, x.shape[0], 0, r)
+                    nxt.send(y)
+                    if ret_rank == 0:
+                        rl = P2PLink(ctx.num_parts - 1, info.device)
+                        pr = torch.empty(x.shape[0], dtype=torch.int32, device=info.device)
+                        rl.recv(pr)
+                        preds = pr.cpu().tolist()
+                    else:
+                        preds = None
+                if preds is not None:
+                    log(f"[{nid}] ***** FINAL PREDICTION (Index): {preds[0] if len(preds) == 1 else preds} *****")
+            if nxt is not None:
+                nxt.send_header(KIND_STOP)
+        else:
+            while True:
+                kind, batch, _, tag = prev.recv_header()
+                if kind == KIND_STOP:
+                    if nxt is not None:
+                        nxt.send_header(KIND_STOP)
+                    break
+                shp, dt = stage.in_spec(batch)
+                x = prev.recv(torch.empty(shp, dtype=dt, device=info.device))
+                y = stage.forward(x)
+                if nxt is not None:
+                    nxt.send_header(KIND_DATA, batch, 0, tag)
+                    nxt.send(y)
+                else:
+                    preds = y.pred.cpu().tolist()
+                    log(f"[{nid}] Final Prediction Index: {preds[0] if len(preds) == 1 else preds}")
+                    if back is not None:
+                        back.send(y.pred)
+    except Exception as e:  # noqa: BLE001
+        log(f"!!! [{nid}] pipeline error: {e}")
+        traceback.print_exc()
+        rc = 1
+    comm.shutdown()
+    return rc
+
+
+def main(argv=None) -> int:
+    log("Script started...")
+    args = build_parser().parse_args(argv)
+    set_quiet(args.quiet)
+    nid = args.node_id
+    log(f"Parsed Node ID: {nid}")
+    try:
+        ctx = load_node(args.config, nid)
+        log(f"Loaded configuration from {args.config}")
+    except ConfigError as e:
+        print(str(e), flush=True)
+        return 1
+    device = pick_device(ctx, args.device)
+    log(banner(ctx, str(device)))
+    try:
+        transport = ctx.pipeline.transport
+        if transport == "colocated":
+            return run_colocated(ctx, args, device)
+        if transport in ("rccl", "gloo"):
+            return run_dist(ctx, args, device)
+        ranges = stage_ranges(ctx)
+        stage, _ = build_stage(ctx, ctx.part_index, ranges, device)
+    except FileNotFoundError:
+        log(f"[{nid}] ERROR: Weights file not found at '{ctx.model_weights}'")
+        return 1
+    except Exception as e:  # noqa: BLE001
+        log(f"[{nid}] ERROR loading model/weights: {e}")
+        traceback.print_exc()
+        return 1
+    try:
+        return asyncio.run(run_grpc(ctx, args, stage))
+    except KeyboardInterrupt:
+        log(f"\n[{nid}] KeyboardInterrupt received, shutting down...")
+        return 0
+    finally:
+        log(f"[{nid}] Event loop closed. Exiting.")

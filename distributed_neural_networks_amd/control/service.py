@@ -1,0 +1,186 @@
+"""gRPC ``NodeService`` — control plane, and the data plane of the CPU config.
+
+Wire-compatible with the reference service (``node_service.proto:4-8``,
+method paths ``/node_service.NodeService/{SendMessage,HealthCheck,SendTensor}``)
+so a reference ``node.py`` peer can talk to this one.  Differences from the
+reference servicer (``node.py:34-133``), all deliberate:
+
+* message-size caps lifted (the reference's default 4 MiB receive cap makes
+  CIFAR batches >= 256 and GPT logits > ~20 tokens fail);
+* one persistent channel to the next stage instead of a new channel per
+  request (``node.py:73``);
+* ``HealthCheck`` reports real readiness (model loaded) instead of a constant;
+  the driver polls it instead of ``asyncio.sleep(2)`` (``node.py:203-207``);
+* ``SendMessage`` keeps its echo reply and additionally accepts the control
+  message ``__shutdown__`` so a run can end cleanly (the reference process
+  never exits, ``node.py:123,344``);
+* the stage forward runs in a worker thread so the event loop stays
+  responsive (the reference computes inside the async handler, ``node.py:52``);
+* per-row argmax (the reference flattens the batch, ``node.py:61``).
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+import traceback
+from typing import Callable, Optional
+
+import grpc
+import numpy as np
+import torch
+
+from ..utils.log import log
+from ..wire import codec, proto
+
+UNLIMITED = [("grpc.max_send_message_length", -1), ("grpc.max_receive_message_length", -1)]
+SHUTDOWN_MSG = "__shutdown__"
+
+
+def _handler(fn, req_cls, resp_cls):
+    return grpc.unary_unary_rpc_method_handler(fn, request_deserializer=req_cls.FromString,
+                                               response_serializer=resp_cls.SerializeToString)
+
+
+class NodeServicer:
+    """Implements the three RPCs over a stage ``forward`` callable.
+
+    ``forward(tensor) -> (out_tensor, pred_or_None)`` runs this stage; for the
+    last stage ``pred`` is the per-row argmax.
+    """
+
+    def __init__(self, node_id: str, forward: Optional[Callable], is_last: bool,
+                 next_address: Optional[str] = None, wire_dtype: Optional[torch.dtype] = torch.float32):
+        self.node_id = node_id
+        self.forward = forward
+        self.is_last = is_last
+        self.next_address = next_address
+        self.wire_dtype = wire_dtype
+        self.ready = forward is not None
+        self._channel = None
+        self._lock = threading.Lock()
+        self.shutdown_event = asyncio.Event()
+        self.requests_served = 0
+
+    def _next_call(self):
+        if self._channel is None:
+            self._channel = grpc.aio.insecure_channel(self.next_address, options=UNLIMITED)
+        return self._channel.unary_unary(proto.method_path("SendTensor"),
+                                         request_serializer=proto.TensorRequest.SerializeToString,
+                                         response_deserializer=proto.TensorResponse.FromString)
+
+    async def SendTensor(self, request, context):
+        nid = self.node_id
+        log(f"\n[{nid}] Received tensor request_id: {request.request_id}")
+        log(f"[{nid}] Incoming Tensor - shape: {list(request.tensor.shape)}, dtype: {request.tensor.dtype}")
+        result = None
+        status = f"[{nid}] Error processing tensor."
+        try:
+            x = codec.decode(request.tensor)
+            log(f"[{nid}] Deserialized input tensor shape: {x.shape}")
+            loop = asyncio.get_running_loop()
+            with self._lock:
+                out, pred = await loop.run_in_executor(None, self.forward, x)
+            out = out.detach().to("cpu")
+            if self.wire_dtype is not None and out.is_floating_point():
+                out = out.to(self.wire_dtype)
+            log(f"[{nid}] Computed output tensor shape: {tuple(out.shape)}")
+            self.requests_served += 1
+            if self.is_last:
+                log(f"[{nid}] Reached final node.")
+                p = pred.tolist() if pred is not None else []
+                shown = p[0] if len(p) == 1 else p
+                log(f"[{nid}] Final Prediction Index: {shown}")
+                status = f"[{nid}] Processing complete. Prediction: {shown}"
+                result = codec.encode(out)
+            else:
+                log(f"[{nid}] Forwarding tensor to next node: {self.next_address}")
+                nreq = proto.TensorRequest(request_id=request.request_id, tensor=codec.encode(out))
+                try:
+                    resp = await self._next_call()(nreq)
+                    log(f"[{nid}] Response from next node ({self.next_address}): {resp.status}")
+                    status = f"[{nid}] Forwarded. Next node status: {resp.status}"
+                    if resp.HasField("result_tensor"):
+                        result = resp.result_tensor
+                except grpc.aio.AioRpcError as e:
+                    log(f"!!! [{nid}] Error calling SendTensor on next node ({self.next_address}): "
+                        f"{e.code()} - {e.details()}")
+                    status = f"[{nid}] Error forwarding: {e.details()}"
+                    result = None
+        except Exception as e:  # noqa: BLE001 — reported in-band like the reference
+            log(f"!!! [{nid}] Error processing tensor: {e}")
+            traceback.print_exc()
+            status = f"[{nid}] Error: {e}"
+            result = None
+        return proto.TensorResponse(status=status, result_tensor=result)
+
+    async def HealthCheck(self, request, context):
+        log(f"[{self.node_id}] Health check requested")
+        return proto.HealthCheckResponse(is_healthy=bool(self.ready))
+
+    async def SendMessage(self, request, context):
+        log(f"[{self.node_id}] Received message from {request.sender_id}")
+        if request.message_text == SHUTDOWN_MSG:
+            self.shutdown_event.set()
+        return proto.MessageReply(confirmation_text=f"[{self.node_id}] got msg '{request.message_text}'")
+
+    def generic_handler(self):
+        return grpc.method_handlers_generic_handler(proto.SERVICE_FULL, {
+            "SendMessage": _handler(self.SendMessage, proto.MessageRequest, proto.MessageReply),
+            "HealthCheck": _handler(self.HealthCheck, proto.Empty, proto.HealthCheckResponse),
+            "SendTensor": _handler(self.SendTensor, proto.TensorRequest, proto.TensorResponse),
+        })
+
+    async def close(self):
+        if self._channel is not None:
+            await self._channel.close()
+
+
+async def start_server(servicer: NodeServicer, port: int, host: str = "[::]"):
+    server = grpc.aio.server(options=UNLIMITED)
+    server.add_generic_rpc_handlers((servicer.generic_handler(),))
+    listen = f"{host}:{port}"
+    bound = server.add_insecure_port(listen)
+    if bound == 0:
+        raise RuntimeError(f"Failed to bind server to {listen}")
+    await server.start()
+    return server
+
+
+class NodeClient:
+    """Persistent-channel client for the three RPCs."""
+
+    def __init__(self, address: str):
+        self.address = address
+        self.channel = grpc.aio.insecure_channel(address, options=UNLIMITED)
+
+        def mk(name):
+            req, resp = proto.METHODS[name]
+            return self.channel.unary_unary(proto.method_path(name), request_serializer=req.SerializeToString,
+                                            response_deserializer=resp.FromString)
+        self.send_tensor = mk("SendTensor")
+        self.health = mk("HealthCheck")
+        self.message = mk("SendMessage")
+
+    async def wait_ready(self, timeout_s: float = 60.0, interval_s: float = 0.05) -> bool:
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout_s
+        while loop.time() < deadline:
+            try:
+                r = await self.health(proto.Empty(), timeout=max(0.5, interval_s * 10))
+                if r.is_healthy:
+                    return True
+            except grpc.aio.AioRpcError:
+                pass
+            await asyncio.sleep(interval_s)
+        return False
+
+    async def close(self):
+        await self.channel.close()
+
+
+def decode_prediction(resp) -> Optional[np.ndarray]:
+    if not resp.HasField("result_tensor"):
+        return None
+    out = codec.decode_numpy(resp.result_tensor)
+    out = out.reshape(out.shape[0], -1) if out.ndim > 1 else out.reshape(1, -1)
+    return out.argmax(axis=-1)

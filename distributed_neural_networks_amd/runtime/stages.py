@@ -1,0 +1,145 @@
+"""Stage compute objects: one pipeline stage's forward over preallocated buffers.
+
+``StageCompute`` is what a pipeline rank runs per microbatch.  Two families:
+
+* ``CifarHipStage`` — the MI355X path: fused gfx950 kernels over bf16 weights
+  packed once at load (``ops/cifar.py``); no torch op runs in ``forward``.
+* ``TorchStage`` — the golden torch module on CPU (fp32): the data path of the
+  reference's CPU/gRPC configuration (``BASELINE.json`` configs[0]) and the
+  oracle in tests.  It is never used on a GPU device.
+
+The GPT-2 / Llama stages live in ``runtime/transformer.py`` (same interface).
+Reference: the stage forward is ``my_model_part(input_torch)`` in
+``node.py:52-53``; the result argmax is ``node.py:61`` (there over the flattened
+batch; here per row).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from ..models import cifar, model_info
+
+Spec = Tuple[Tuple[int, ...], torch.dtype]
+
+
+@dataclass
+class StageOutput:
+    """Last-stage result: probabilities/logits and per-row predictions."""
+    probs: torch.Tensor
+    pred: torch.Tensor
+
+
+class StageCompute:
+    first: bool
+    last: bool
+    device: torch.device
+
+    def in_spec(self, batch: int) -> Spec:
+        raise NotImplementedError
+
+    def out_spec(self, batch: int) -> Spec:
+        raise NotImplementedError
+
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None):
+        raise NotImplementedError
+
+
+class CifarHipStage(StageCompute):
+    """CIFAR units [start, end] on the fused HIP kernels. Supported splits:
+    (0,1) = reference part 0, (2,3) = reference part 1, (0,3) = whole model."""
+
+    SUPPORTED = {(0, 1), (2, 3), (0, 3)}
+
+    def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device):
+        from ..ops import cifar as cops
+        if (start, end) not in self.SUPPORTED:
+            raise ValueError(f"HIP CIFAR backend supports unit ranges {sorted(self.SUPPORTED)}, got ({start},{end})")
+        self.start, self.end, self.device = start, end, torch.device(device)
+        self.first, self.last = start == 0, end == cifar.NUM_UNITS - 1
+        self._cops = cops
+        self.w0 = cops.pack_stage0(sd, self.device) if start == 0 else None
+        self.wh = cops.pack_head(sd, self.device) if end == 3 else None
+        self._scratch: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def in_spec(self, batch):
+        return ((batch, 3, 32, 32), torch.float32) if self.first else ((batch, cifar.FLAT_DIM), torch.bfloat16)
+
+    def out_spec(self, batch):
+        return ((batch, 10), torch.float32) if self.last else ((batch, cifar.FLAT_DIM), torch.bfloat16)
+
+    def _buf(self, batch):
+        b = self._scratch.get(batch)
+        if b is None:
+            d = self.device
+            b = {}
+            if self.first and self.last:
+                b["mid"] = torch.empty((batch, 4096), dtype=torch.bfloat16, device=d)
+            if self.last:
+                b["hid"] = torch.empty((batch, 512), dtype=torch.bfloat16, device=d)
+                b["pred"] = torch.empty((batch,), dtype=torch.int32, device=d)
+            self._scratch[batch] = b
+        return b
+
+    def forward(self, x, out=None):
+        B = x.shape[0]
+        buf = self._buf(B)
+        if self.first:
+            if x.dtype != torch.float32:
+                x = x.float()
+            x = x.contiguous()
+            mid = buf["mid"] if self.last else out
+            h = self._cops.stage0_forward(x, self.w0, mid)
+            if not self.last:
+                return h
+        else:
+            h = x
+        probs, pred = self._cops.head_forward(h, self.wh, buf["hid"], out, buf["pred"])
+        return StageOutput(probs, pred)
+
+
+class TorchStage(StageCompute):
+    """Golden torch module as a stage (CPU fp32 plumbing path / tests)."""
+
+    def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
+                 device="cpu", dtype=torch.float32):
+        from ..models import build_golden_stage
+        self.model, self.start, self.end, self.first, self.last = model, start, end, first, last
+        self.device = torch.device(device)
+        self.family = model_info(model).family
+        self.module = build_golden_stage(model, start, end, first, last)
+        missing, unexpected = self.module.load_state_dict(sd, strict=False)
+        if missing:
+            raise KeyError(f"stage [{start},{end}] missing weights: {missing[:8]}")
+        self.module = self.module.to(device=self.device, dtype=dtype).eval()
+        self.dtype = dtype
+
+    def in_spec(self, batch, seq: int = 0):
+        if self.family == "cifar":
+            return cifar.input_shape(self.start, batch), self.dtype
+        info = model_info(self.model)
+        if self.first:
+            return (batch, seq), torch.int64
+        return (batch, seq, info.cfg.n_embd), self.dtype
+
+    def out_spec(self, batch, seq: int = 0):
+        if self.family == "cifar":
+            return cifar.output_shape(self.end, batch), self.dtype
+        info = model_info(self.model)
+        if self.last:
+            return (batch, seq, info.cfg.vocab_size), self.dtype
+        return (batch, seq, info.cfg.n_embd), self.dtype
+
+    @torch.no_grad()
+    def forward(self, x, out=None):
+        y = self.module(x.to(self.device))
+        if self.last:
+            if self.family == "cifar":
+                return StageOutput(y, y.argmax(dim=1).to(torch.int32))
+            return StageOutput(y, y[:, -1, :].argmax(dim=-1).to(torch.int32))
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y

@@ -1,0 +1,94 @@
+"""Config schema + topology: reference error strings/exit semantics (node.py:222-290)."""
+import json
+
+import pytest
+
+from distributed_neural_networks_amd.config import ConfigError, load_node, resolve_node, banner
+
+REF = {
+    "nodes": [{"id": "node1", "address": "192.168.1.101:50051", "part_index": 0},
+              {"id": "node2", "address": "192.168.1.120:50051", "part_index": 1}],
+    "model_weights": "./cifar10_model.pth", "num_parts": 2, "return_to_node_id": "node1",
+}
+
+
+def test_reference_config_resolves():
+    a = resolve_node(REF, "node1")
+    assert a.part_index == 0 and not a.is_last and a.next_address == "192.168.1.120:50051" and a.port == 50051
+    b = resolve_node(REF, "node2")
+    assert b.is_last and b.next_address is None and b.return_address == "192.168.1.101:50051"
+    assert "Part Index: 1 / 1" in banner(b, "cpu")
+
+
+def test_missing_file(tmp_path):
+    with pytest.raises(ConfigError, match="Config file not found"):
+        load_node(str(tmp_path / "nope.json"), "node1")
+
+
+def test_bad_json(tmp_path):
+    p = tmp_path / "c.json"
+    p.write_text("{nodes: ")
+    with pytest.raises(ConfigError, match="Invalid JSON in config file"):
+        load_node(str(p), "node1")
+
+
+def test_unknown_node():
+    with pytest.raises(ConfigError, match="Node ID 'node9' not found"):
+        resolve_node(REF, "node9")
+
+
+def test_missing_fields():
+    c = json.loads(json.dumps(REF))
+    del c["model_weights"]
+    with pytest.raises(ConfigError, match="missing required fields"):
+        resolve_node(c, "node1")
+
+
+def test_bad_address():
+    c = json.loads(json.dumps(REF))
+    c["nodes"][0]["address"] = "hostonly:abc"
+    with pytest.raises(ConfigError, match="Invalid format for MY_ADDRESS"):
+        resolve_node(c, "node1")
+
+
+def test_num_parts_generalised():
+    # reference rejects num_parts != 2 (node.py:246); here any permutation of 0..n-1 works
+    c = {"nodes": [{"id": f"n{i}", "address": f"127.0.0.1:{5000 + i}", "part_index": i} for i in range(4)],
+         "model_weights": "synthetic", "num_parts": 4, "model": "gpt2"}
+    ctx = resolve_node(c, "n2")
+    assert ctx.next_address == "127.0.0.1:5003" and not ctx.is_last
+    c["num_parts"] = 3
+    with pytest.raises(ConfigError, match="part_index"):
+        resolve_node(c, "n0")
+
+
+def test_next_missing():
+    c = json.loads(json.dumps(REF))
+    c["nodes"][1]["part_index"] = 5
+    c["num_parts"] = 2
+    with pytest.raises(ConfigError):
+        resolve_node(c, "node1")
+
+
+def test_extension_fields():
+    c = json.loads(json.dumps(REF))
+    c.update(transport="rccl", micro_batch_size=8, num_microbatches=4, model="cifar10")
+    c["nodes"][0]["layers"] = [0, 1]
+    c["nodes"][1]["layers"] = [2, 3]
+    ctx = resolve_node(c, "node1")
+    assert ctx.pipeline.transport == "rccl" and ctx.pipeline.micro_batch_size == 8
+    assert ctx.pipeline.stage(1).layers == (2, 3)
+    c["transport"] = "carrier-pigeon"
+    with pytest.raises(ConfigError, match="unknown transport"):
+        resolve_node(c, "node1")
+
+
+def test_repo_configs_parse():
+    import glob
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = [os.path.join(root, "config.json")] + glob.glob(os.path.join(root, "configs", "*.json"))
+    for f in files:
+        d = json.load(open(f))
+        for n in d["nodes"]:
+            resolve_node(d, n["id"], f)
