@@ -60,8 +60,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st) {
     return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st));
   });
-  m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, u64 st) {
-    return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, ST(st));
+  m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, int kpad, u64 st) {
+    return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, kpad, ST(st));
   });
   m.def("gemm_fp8", [](u64 A, u64 sa, u64 W, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N, int K,
                        int act, u64 st) {

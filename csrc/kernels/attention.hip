@@ -1,0 +1,417 @@
+// Attention kernels for gfx950: QKV split (+RoPE, KV-cache write), causal
+// flash-attention prefill on MFMA, and split-K decode attention.
+//
+// Replaces nanoGPT's CausalSelfAttention internals (qkv split, causal SDPA;
+// Block of partitions/gpt_model_parts.py:20-21,32-33,46-47) and the Llama GQA
+// attention. The reference recomputes the full prefix every call (no KV cache);
+// here K/V live in a per-stage cache [B][Hkv][S][hd] (bf16, sized from the 288
+// GB HBM) and positions/lengths are read from device memory so decode steps
+// replay one captured HIP graph.
+//
+// Flash prefill structure (cdna_hip_programming.md App. B + §3 "accumulator as
+// next operand"): 4 waves x 32 query rows; per 64-key block each wave computes
+// S^T = K.Q^T with v_mfma_f32_32x32x16_bf16 (query on the lane, keys in the 16
+// accumulator registers, so the row max/sum are in-register + one xor-32
+// shuffle), then O^T += V^T . P^T with the S^T accumulators converted to bf16
+// as the B operand (no LDS round trip for P) and V^T fragments fetched with
+// ds_read_b64_tr_b16 (hardware transpose) from a row-padded V tile. K rows are
+// XOR-swizzled so the A-fragment ds_read_b128 reads are conflict-free.
+#include "common.h"
+
+namespace dnn {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// QKV split: qkv rows r = b*T + t, columns [q H*hd | k Hkv*hd | v Hkv*hd].
+// q -> q_out[b][h][t][:] (RoPE'd when rope), k/v -> cache[b][hkv][pos[b]+t][:].
+// One thread = 8 elements of the first half + the matching 8 of the second
+// half of one head (rotate-half pairs).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ q,
+                                                        bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int B, int T,
+                                                        int H, int Hkv, int hd, int S, const int* __restrict__ pos,
+                                                        const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                                        int rope) {
+  const int half = hd / 2, groups = half / 8;
+  const int heads = H + 2 * Hkv;
+  const long total = (long)B * T * heads * groups;
+  const int ld = heads * hd;
+  for (long gi = blockIdx.x * (long)blockDim.x + threadIdx.x; gi < total; gi += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(gi % groups);
+    long r = gi / groups;
+    const int hh = (int)(r % heads);
+    r /= heads;
+    const int t = (int)(r % T), b = (int)(r / T);
+    const int p = (pos != nullptr ? pos[b] : 0) + t;
+    const bf16_t* src = qkv + (size_t)(b * T + t) * ld + hh * hd;
+    const int i0 = g * 8;
+    const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(src + i0);
+    const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(src + half + i0);
+    bf16x8 y1 = x1, y2 = x2;
+    if (rope && hh < H + Hkv) {
+      const float* cr = cosT + (size_t)p * half + i0;
+      const float* sr = sinT + (size_t)p * half + i0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = bf2f_s(x1[j]), c = bf2f_s(x2[j]), co = cr[j], si = sr[j];
+        y1[j] = (short)f2bf(a * co - c * si);
+        y2[j] = (short)f2bf(c * co + a * si);
+      }
+    }
+    bf16_t* dst;
+    if (hh < H) {
+      dst = q + (((size_t)b * H + hh) * T + t) * hd;
+    } else if (hh < H + Hkv) {
+      dst = kc + (((size_t)b * Hkv + (hh - H)) * S + p) * hd;
+    } else {
+      dst = vc + (((size_t)b * Hkv + (hh - H - Hkv)) * S + p) * hd;
+    }
+    *reinterpret_cast<bf16x8*>(dst + i0) = y1;
+    *reinterpret_cast<bf16x8*>(dst + half + i0) = y2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Causal flash-attention prefill (chunked: queries at absolute pos[b]+t attend
+// keys 0..pos[b]+t of the cache).
+// ---------------------------------------------------------------------------
+constexpr int FA_QB = 128, FA_KB = 64;
+
+template <int HD>
+struct FaSmem {
+  static constexpr int K_BYTES = FA_KB * HD * 2;
+  static constexpr int V_STRIDE = HD * 2 + 64;  // padded row: conflict-free tr reads
+  static constexpr int V_BYTES = FA_KB * V_STRIDE;
+  static constexpr int TOTAL = K_BYTES + V_BYTES;
+};
+
+template <int HD>
+__device__ __forceinline__ int k_swz(int key, int chunk) {
+  return HD == 64 ? (chunk ^ ((key >> 1) & 7)) : (chunk ^ (key & 15));
+}
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                            const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
+                                                            int H, int Hkv, int S, const int* __restrict__ pos,
+                                                            float scale_log2) {
+  using SM = FaSmem<HD>;
+  __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL];
+  char* ks = smem;
+  char* vs = smem + SM::K_BYTES;
+  constexpr int NKS = HD / 16;  // k-steps of the QK^T contraction
+  constexpr int NDT = HD / 32;  // 32-wide d tiles of O
+  constexpr int CH = HD / 8;    // 16-B chunks per row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int qb = blockIdx.x, hh = blockIdx.y, b = blockIdx.z;
+  const int kvh = hh / (H / Hkv);
+  const int p0 = pos != nullptr ? pos[b] : 0;
+  const int kv_len = p0 + T;
+  const int qrow0 = qb * FA_QB + wave * 32;            // this wave's first query (chunk-relative)
+  const int qrow = qrow0 + r32;                        // this lane's query
+  const int q_abs = p0 + min(qrow, T - 1);
+  const int wave_qmax = p0 + min(qrow0 + 31, T - 1);   // wave-uniform
+  const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
+  const int kv_end = min(kv_len, blk_qmax + 1);
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qrow][ks*16 + 8h + j]
+  bf16x8 qf[NKS];
+  {
+    const bf16_t* qp = q + (((size_t)b * H + hh) * T + min(qrow, T - 1)) * HD + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + s * 16);
+  }
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) oacc[i] = f32x16{};
+  float m_i = -INFINITY, l_i = 0.f;
+
+  const bf16_t* kbase = kc + ((size_t)b * Hkv + kvh) * S * HD;
+  const bf16_t* vbase = vc + ((size_t)b * Hkv + kvh) * S * HD;
+
+  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
+    // ---- stage K (swizzled) and V (padded rows) ----
+#pragma unroll
+    for (int it = 0; it < (FA_KB * CH) / 256; ++it) {
+      const int e = it * 256 + tid;
+      const int key = e / CH, c = e % CH;
+      const int kk = min(kb0 + key, kv_len - 1);
+      const uint4 kv = *reinterpret_cast<const uint4*>(kbase + (size_t)kk * HD + c * 8);
+      const uint4 vv = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + c * 8);
+      *reinterpret_cast<uint4*>(ks + key * HD * 2 + (k_swz<HD>(key, c) << 4)) = kv;
+      *reinterpret_cast<uint4*>(vs + key * SM::V_STRIDE + c * 16) = vv;
+    }
+    __syncthreads();
+    if (kb0 <= wave_qmax) {
+      // ---- S^T for two 32-key tiles ----
+      f32x16 sacc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        sacc[kt] = f32x16{};
+        const int key = kt * 32 + r32;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + key * HD * 2 + (k_swz<HD>(key, 2 * s + h) << 4));
+          sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
+        }
+      }
+      // ---- mask + online softmax (lane = one query; keys in registers) ----
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int key = kb0 + kt * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+          float v = sacc[kt][g] * scale_log2;
+          if (key > q_abs || key >= kv_len) v = -INFINITY;
+          sacc[kt][g] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_i, mx);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = exp2f(m_i - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const float pv = exp2f(sacc[kt][g] - m_use);
+          sacc[kt][g] = pv;
+          rs += pv;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_i = l_i * alpha + rs;
+      m_i = m_new;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) oacc[i] *= alpha;
+      // ---- O^T += V^T . P^T ----
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(sacc[kt][8 * s + j]);
+          const int krow = kt * 32 + 16 * s + 4 * h + ((lane & 15) >> 2);
+          const int gsub = (lane >> 4) & 1;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const int dcol = dt * 32 + gsub * 16 + 4 * (lane & 3);
+            const char* a0 = vs + krow * SM::V_STRIDE + dcol * 2;
+            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a0));
+            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a0 + 8 * SM::V_STRIDE));
+            bf16x8 vf;
+            vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
+            vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
+            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[dt], 0, 0, 0);
+          }
+        }
+    }
+    __syncthreads();
+  }
+  // ---- normalise + store: lane = query, regs = d ----
+  if (qrow < T) {
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    bf16_t* op = o + ((size_t)b * T + qrow) * (size_t)(H * HD) + hh * HD;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        uint2 w;
+        w.x = pack2bf(oacc[dt][4 * g4 + 0] * inv, oacc[dt][4 * g4 + 1] * inv);
+        w.y = pack2bf(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(op + d) = w;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Decode attention (one query token per sequence), split over the key axis.
+// grid = (B*Hkv, NS); each workgroup handles the G = H/Hkv query heads of one
+// kv head over keys [split*chunk, (split+1)*chunk) ∩ [0, lens[b]) and writes an
+// unnormalised partial (o, m, l) to ws; decode_combine merges the splits.
+// ---------------------------------------------------------------------------
+constexpr int DEC_MAXG = 8;
+
+template <int HD, int G>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                          const bf16_t* __restrict__ vc, float* __restrict__ ws, int H,
+                                                          int Hkv, int S, const int* __restrict__ lens, float scale_log2,
+                                                          int chunk) {
+  constexpr int LPK = HD / 8;           // lanes per key row (16 B each)
+  constexpr int GPB = 256 / LPK;        // key groups per block
+  extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk] scores, then reduction scratch
+  const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
+  const int b = bk / Hkv, kvh = bk % Hkv;
+  const int len = lens[b];
+  const int k0 = split * chunk, k1 = min(len, k0 + chunk);
+  const int tid = threadIdx.x, sub = tid % LPK, grp = tid / LPK;
+  float* wsp = ws + ((size_t)bk * NS + split) * G * (HD + 2);
+  if (k0 >= k1) {
+    for (int i = tid; i < G * (HD + 2); i += 256) {
+      const int c = i % (HD + 2);
+      wsp[i] = c == HD ? -INFINITY : 0.f;
+    }
+    return;
+  }
+  const bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD;
+  const bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD;
+  float qv[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bf16x8 p = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[g][j] = bf2f_s(p[j]);
+  }
+  float* sc = dsm;  // [G][chunk]
+  const int n = k1 - k0;
+  for (int kk = grp; kk < n; kk += GPB) {
+    const bf16x8 kr = *reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
+    float kf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kf[j] = bf2f_s(kr[j]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
+#pragma unroll
+      for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (sub == 0) sc[g * chunk + kk] = d * scale_log2;
+    }
+  }
+  __syncthreads();
+  // per-head max and exp (one wave per head, strided)
+  __shared__ float mh[DEC_MAXG], lh[DEC_MAXG];
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int g = wave; g < G; g += 4) {
+    float mx = -INFINITY;
+    for (int i = lane; i < n; i += 64) mx = fmaxf(mx, sc[g * chunk + i]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int i = lane; i < n; i += 64) {
+      const float e = exp2f(sc[g * chunk + i] - mx);
+      sc[g * chunk + i] = e;
+      s += e;
+    }
+    s = wave_sum(s);
+    if (lane == 0) { mh[g] = mx; lh[g] = s; }
+  }
+  __syncthreads();
+  // P.V: thread owns d chunk `sub` for key group `grp`
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  for (int kk = grp; kk < n; kk += GPB) {
+    const bf16x8 vr = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+    float vf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vf[j] = bf2f_s(vr[j]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float pw = sc[g * chunk + kk];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] += pw * vf[j];
+    }
+  }
+  __syncthreads();  // scores no longer needed: reuse dsm as [GPB][G][HD] reduction scratch
+  float* red = dsm;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[((size_t)grp * G + g) * HD + sub * 8 + j] = acc[g][j];
+  __syncthreads();
+  for (int i = tid; i < G * HD; i += 256) {
+    const int g = i / HD, d = i % HD;
+    float s = 0.f;
+    for (int r = 0; r < GPB; ++r) s += red[((size_t)r * G + g) * HD + d];
+    wsp[g * (HD + 2) + d] = s;
+  }
+  if (tid < G) {
+    wsp[tid * (HD + 2) + HD] = mh[tid];
+    wsp[tid * (HD + 2) + HD + 1] = lh[tid];
+  }
+}
+
+__global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H, int Hkv,
+                                      int HD, int NS) {
+  const int bh = blockIdx.x;  // b*H + h
+  const int b = bh / H, hh = bh % H;
+  const int G = H / Hkv, kvh = hh / G, g = hh % G;
+  const float* base = ws + ((size_t)(b * Hkv + kvh) * NS) * G * (HD + 2) + g * (HD + 2);
+  float m = -INFINITY;
+  for (int s = 0; s < NS; ++s) m = fmaxf(m, base[(size_t)s * G * (HD + 2) + HD]);
+  float l = 0.f;
+  for (int s = 0; s < NS; ++s) {
+    const float ms = base[(size_t)s * G * (HD + 2) + HD];
+    if (ms != -INFINITY) l += base[(size_t)s * G * (HD + 2) + HD + 1] * exp2f(ms - m);
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  for (int d = threadIdx.x; d < HD; d += blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < NS; ++s) {
+      const float ms = base[(size_t)s * G * (HD + 2) + HD];
+      if (ms != -INFINITY) acc += base[(size_t)s * G * (HD + 2) + d] * exp2f(ms - m);
+    }
+    o[(size_t)b * H * HD + hh * HD + d] = f2bf(acc * inv);
+  }
+}
+
+}  // namespace dnn
+
+using namespace dnn;
+
+extern "C" int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
+                             const int* pos, const float* cos, const float* sin, int rope, hipStream_t st) {
+  if (hd % 16 != 0 || H % Hkv != 0) return -1;
+  const long total = (long)B * T * (H + 2 * Hkv) * (hd / 16);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(qkv_split_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)q, (bf16_t*)kc,
+                     (bf16_t*)vc, B, T, H, Hkv, hd, S, pos, cos, sin, rope);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,
+                              int hd, int S, const int* pos, float scale, hipStream_t st) {
+  if (H % Hkv != 0) return -1;
+  dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (hd == 64) {
+    hipLaunchKernelGGL((flash_attn_kernel<64>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
+                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+  } else if (hd == 128) {
+    hipLaunchKernelGGL((flash_attn_kernel<128>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
+                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+  } else {
+    return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd,
+                               int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {
+  const int G = H / Hkv;
+  if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
+  const int chunk = (S + splits - 1) / splits;
+  const int gpb = 256 / (hd / 8);
+  size_t smem = sizeof(float) * (size_t)G * (size_t)(chunk > gpb * hd ? chunk : gpb * hd);
+  if (smem > 160 * 1024) return -3;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid(B * Hkv, splits);
+#define DEC(HDV, GV)                                                                                               \
+  if (hd == HDV && G == GV) {                                                                                      \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV>), grid, dim3(256), smem, st, (const bf16_t*)q, (const bf16_t*)kc, \
+                       (const bf16_t*)vc, ws, H, Hkv, S, lens, sl2, chunk);                                        \
+  } else
+  DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(128, 1) DEC(128, 2) DEC(128, 4) DEC(128, 8) { return -2; }
+#undef DEC
+  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
+  return (int)hipGetLastError();
+}

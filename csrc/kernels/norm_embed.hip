@@ -1,0 +1,131 @@
+// LayerNorm / RMSNorm and the GPT-2 token+position embedding (gfx950).
+//
+// LayerNorm with bias replaces nanoGPT's ln_1 / ln_2 / ln_f
+// (partitions/gpt_model_parts.py:41,48 and the Block internals); RMSNorm serves
+// Llama-3. One wave per row, 16-byte vector loads (guide G13), the row cached
+// in registers between the statistics pass and the normalise pass, fp32 math,
+// bf16 out. The embedding kernel fuses wte gather + wpe add
+// (gpt_model_parts.py:16-19) and reads per-sequence start positions from device
+// memory so one HIP graph serves every decode step.
+#include "common.h"
+
+namespace dnn {
+
+template <int NC, bool RMS>
+__global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ w,
+                                                   const float* __restrict__ b, bf16_t* __restrict__ y, int ldy, int M,
+                                                   int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  float v[NC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+      const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / N + eps);
+  bf16_t* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + c), w1 = *reinterpret_cast<const float4*>(w + c + 4);
+      const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (!RMS && b != nullptr) {
+        const float4 b0 = *reinterpret_cast<const float4*>(b + c), b1 = *reinterpret_cast<const float4*>(b + c + 4);
+        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+      }
+      uint4 o;
+      uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a0 = (v[i][2 * j] - mean) * rstd * ww[2 * j] + bb[2 * j];
+        const float a1 = (v[i][2 * j + 1] - mean) * rstd * ww[2 * j + 1] + bb[2 * j + 1];
+        op[j] = pack2bf(a0, a1);
+      }
+      *reinterpret_cast<uint4*>(yr + c) = o;
+    }
+  }
+}
+
+// out[r, :] = wte[idx[r], :] (+ wpe[pos[b] + t, :]) with r = b*T + t.
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ wte,
+                                                    const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int B,
+                                                    int T, int d, const int* __restrict__ pos) {
+  const int chunks = d / 8;
+  const long total = (long)B * T * chunks;
+  for (long g = blockIdx.x * (long)blockDim.x + threadIdx.x; g < total; g += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(g % chunks);
+    const long r = g / chunks;
+    const int b = (int)(r / T), t = (int)(r % T);
+    const int tok = idx[r];
+    const bf16x8 e = *reinterpret_cast<const bf16x8*>(wte + (size_t)tok * d + c * 8);
+    uint4 o;
+    if (wpe != nullptr) {
+      const int p = (pos != nullptr ? pos[b] : 0) + t;
+      const bf16x8 q = *reinterpret_cast<const bf16x8*>(wpe + (size_t)p * d + c * 8);
+      uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        op[j] = pack2bf(bf2f_s(e[2 * j]) + bf2f_s(q[2 * j]), bf2f_s(e[2 * j + 1]) + bf2f_s(q[2 * j + 1]));
+    } else {
+      o = *reinterpret_cast<const uint4*>(&e);
+    }
+    *reinterpret_cast<uint4*>(out + r * d + c * 8) = o;
+  }
+}
+
+}  // namespace dnn
+
+using namespace dnn;
+
+extern "C" int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N,
+                             float eps, int rms, hipStream_t st) {
+  if (N % 8 != 0 || N > 8192) return -1;
+  const int nc = (N / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), blk(256);
+#define L(NCV)                                                                                                      \
+  if (nc <= NCV) {                                                                                                  \
+    if (rms) hipLaunchKernelGGL((norm_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b, (bf16_t*)y, \
+                                ldy, M, N, eps);                                                                    \
+    else hipLaunchKernelGGL((norm_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b, (bf16_t*)y,   \
+                            ldy, M, N, eps);                                                                        \
+    return (int)hipGetLastError();                                                                                  \
+  }
+  L(1) L(2) L(4) L(8) L(16)
+#undef L
+  return -1;
+}
+
+extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d,
+                              const int* pos, hipStream_t st) {
+  if (d % 8 != 0) return -1;
+  const long total = (long)B * T * (d / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(embed_kernel, dim3(blocks), dim3(256), 0, st, idx, (const bf16_t*)wte, (const bf16_t*)wpe,
+                     (bf16_t*)out, B, T, d, pos);
+  return (int)hipGetLastError();
+}

@@ -56,7 +56,9 @@ def _headers_mtime() -> float:
 
 
 def _obj(src: str) -> str:
-    return os.path.join(BUILD, os.path.basename(src) + ".o")
+    import hashlib
+    tag = hashlib.sha1(" ".join(_flags(src)).encode()).hexdigest()[:8]
+    return os.path.join(BUILD, f"{os.path.basename(src)}.{tag}.o")
 
 
 def _compile(src: str, force: bool, hm: float) -> str:

@@ -1,0 +1,75 @@
+"""FP8 (OCP e4m3fn) weight quantisation and the scaled-MFMA GEMM.
+
+Weights: per-output-channel absmax scale, quantised once at load on the host
+(``torch.float8_e4m3fn`` is OCP e4m3 — the gfx950 format, not MI300's fnuz).
+Activations: per-token absmax scale, quantised on device by
+``quant_fp8_rows`` right before each GEMM (fused into the GEMM's producer is a
+later optimisation).  ``linear_fp8`` = ``quant -> gemm_fp8`` with the bf16
+epilogue (bias / act / residual) of the bf16 GEMM.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr
+
+FP8_MAX = 448.0
+
+
+@dataclass
+class Fp8Weight:
+    q: torch.Tensor      # (N, Kpad) float8_e4m3fn, K zero-padded to a multiple of 128
+    scale: torch.Tensor  # (N,) fp32
+    k: int = 0           # logical K
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+
+def kpad_of(k: int) -> int:
+    return -(-k // 128) * 128
+
+
+def quantize_weight(w: torch.Tensor, device) -> Fp8Weight:
+    wf = w.float()
+    N, K = wf.shape
+    amax = wf.abs().amax(dim=1).clamp_min(1e-12)
+    s = amax / FP8_MAX
+    q = torch.zeros((N, kpad_of(K)), dtype=torch.float8_e4m3fn)
+    q[:, :K] = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return Fp8Weight(q.to(device).contiguous(), s.to(device=device, dtype=torch.float32).contiguous(), K)
+
+
+def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: Optional[int] = None):
+    """Per-row e4m3 quantisation; q_out rows are zero-padded to kpad_of(K)."""
+    M = rows if rows is not None else x.shape[0]
+    K = x.shape[-1]
+    kp = kpad_of(K)
+    if q_out.dtype not in (torch.uint8, torch.float8_e4m3fn) or q_out.numel() < M * kp:
+        raise ValueError("quant_rows: bad output buffer")
+    check(lib().quant_fp8_rows(ptr(x), x.stride(0), ptr(q_out), ptr(s_out), M, K, kp, stream_ptr()),
+          "quant_fp8_rows")
+
+
+def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
+               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+               qbuf: Optional[torch.Tensor] = None, sbuf: Optional[torch.Tensor] = None) -> torch.Tensor:
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N, kp = w.q.shape
+    if kp != kpad_of(K) or (w.k and w.k != K):
+        raise ValueError(f"linear_fp8: x K={K} vs weight K={w.k} (padded {kp})")
+    qbuf = qbuf if qbuf is not None else torch.empty((M, kp), dtype=torch.uint8, device=x.device)
+    sbuf = sbuf if sbuf is not None else torch.empty((M,), dtype=torch.float32, device=x.device)
+    quant_rows(x2, qbuf, sbuf, M)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    o2 = out.reshape(-1, out.shape[-1])
+    r2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
+    check(lib().gemm_fp8(ptr(qbuf), ptr(sbuf), ptr(w.q), ptr(w.scale), ptr(o2), o2.stride(0), ptr(bias), ptr(r2),
+                         0 if r2 is None else r2.stride(0), M, N, kp, act, stream_ptr()), "gemm_fp8")
+    return out

@@ -1,0 +1,103 @@
+"""Thin wrappers over the transformer kernels (norms, embedding, attention,
+sampler, fp8).  Shapes are validated on the host before launch — a kernel is
+only ever launched with the operand shapes its grid assumes."""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr
+
+
+def _bf16_2d(x: torch.Tensor, name: str) -> None:
+    if x.dtype != torch.bfloat16 or x.stride(-1) != 1:
+        raise ValueError(f"{name}: expected bf16 with contiguous last dim, got {x.dtype} strides {x.stride()}")
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor, eps: float = 1e-5,
+              rms: bool = False, rows: Optional[int] = None, ldx: Optional[int] = None) -> torch.Tensor:
+    """Row-wise LayerNorm (rms=False, with bias) or RMSNorm over the last dim.
+    ``rows``/``ldx`` allow normalising a strided subset of rows (e.g. the last
+    position of every sequence: ldx = T*d, x pointing at row T-1)."""
+    _bf16_2d(x, "layernorm")
+    N = x.shape[-1]
+    M = rows if rows is not None else x.numel() // N
+    ldx = ldx if ldx is not None else N
+    if w.dtype != torch.float32 or (b is not None and b.dtype != torch.float32):
+        raise TypeError("layernorm: fp32 weight/bias expected")
+    if N % 8 or N > 8192:
+        raise ValueError(f"layernorm: unsupported width {N}")
+    if out.numel() < M * N:
+        raise ValueError("layernorm: output too small")
+    check(lib().layernorm(ptr(x), ldx, ptr(w), ptr(b), ptr(out), N, M, N, eps, 1 if rms else 0, stream_ptr()),
+          "layernorm")
+    return out
+
+
+def embed(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], out: torch.Tensor,
+          pos: Optional[torch.Tensor]) -> torch.Tensor:
+    """out[b*T+t] = wte[idx[b,t]] (+ wpe[pos[b]+t]). idx int32 (B,T)."""
+    if idx.dtype != torch.int32 or idx.dim() != 2:
+        raise ValueError("embed: idx must be int32 (B,T)")
+    B, T = idx.shape
+    d = wte.shape[1]
+    if out.numel() < B * T * d:
+        raise ValueError("embed: output too small")
+    check(lib().embed_gpt2(ptr(idx), ptr(wte), ptr(wpe), ptr(out), B, T, d, ptr(pos), stream_ptr()), "embed")
+    return out
+
+
+def qkv_split(qkv: torch.Tensor, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, B: int, T: int, H: int,
+              Hkv: int, hd: int, pos: torch.Tensor, cos: Optional[torch.Tensor] = None,
+              sin: Optional[torch.Tensor] = None) -> None:
+    S = kc.shape[2]
+    if kc.shape[:2] != (B, Hkv) or kc.shape[3] != hd or vc.shape != kc.shape:
+        raise ValueError(f"qkv_split: cache {tuple(kc.shape)} does not match B={B} Hkv={Hkv} hd={hd}")
+    if qkv.numel() < B * T * (H + 2 * Hkv) * hd or q.numel() < B * T * H * hd:
+        raise ValueError("qkv_split: buffers too small")
+    rope = cos is not None
+    check(lib().qkv_split(ptr(qkv), ptr(q), ptr(kc), ptr(vc), B, T, H, Hkv, hd, S, ptr(pos), ptr(cos), ptr(sin),
+                          1 if rope else 0, stream_ptr()), "qkv_split")
+
+
+def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,
+               Hkv: int, hd: int, pos: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
+    """Causal attention of T new queries per sequence against the cache
+    (positions 0..pos[b]+T-1). q (B,H,T,hd); out (B*T, H*hd)."""
+    if hd not in (64, 128):
+        raise ValueError(f"flash_attn: head_dim {hd} unsupported (64/128)")
+    S = kc.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    check(lib().flash_attn(ptr(q), ptr(kc), ptr(vc), ptr(out), B, T, H, Hkv, hd, S, ptr(pos), scale, stream_ptr()),
+          "flash_attn")
+    return out
+
+
+def decode_splits(S: int, B: int, Hkv: int) -> int:
+    """Split-K factor for decode attention: enough workgroups to cover the CUs,
+    chunks of >= 256 keys."""
+    want = max(1, -(-512 // max(1, B * Hkv)))
+    return max(1, min(want, -(-S // 256)))
+
+
+def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, H: int, Hkv: int,
+                hd: int, lens: torch.Tensor, ws: torch.Tensor, splits: int, scale: Optional[float] = None):
+    S = kc.shape[2]
+    G = H // Hkv
+    need = B * Hkv * splits * G * (hd + 2)
+    if ws.numel() < need or ws.dtype != torch.float32:
+        raise ValueError(f"attn_decode: workspace needs {need} fp32")
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    check(lib().attn_decode(ptr(q), ptr(kc), ptr(vc), ptr(out), B, H, Hkv, hd, S, ptr(lens), scale, splits, ptr(ws),
+                            stream_ptr()), "attn_decode")
+    return out
+
+
+def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
+    M = x.shape[0]
+    N = n if n is not None else x.shape[1]
+    check(lib().argmax_rows(ptr(x), x.stride(0), M, N, ptr(out), 1 if x.dtype == torch.float32 else 0,
+                            stream_ptr()), "argmax_rows")
+    return out

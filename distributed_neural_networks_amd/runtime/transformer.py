@@ -1,0 +1,409 @@
+"""GPT-2 / Llama-3 pipeline stages on the gfx950 kernels, with a KV cache.
+
+Reference semantics (``partitions/gpt_model_parts.py``): first stage =
+``wte(idx) + wpe(arange(T))`` + blocks, middle = blocks, last = blocks +
+``ln_f`` + ``lm_head``.  The reference recomputes the whole prefix for every
+token and returns full-T fp32 logits over gRPC; here each stage keeps a bf16
+KV cache ``[B][Hkv][S][hd]`` per layer (sized up front; 288 GB HBM per GPU),
+prefill runs flash attention over the new tokens, decode runs split-K decode
+attention, and the last stage applies ``ln_f`` + ``lm_head`` to the last
+position only and samples greedily on device (``last_only=False`` gives the
+reference's all-position logits).
+
+Per layer (GPT-2): LN -> QKV GEMM(+bias) -> split(+cache write) -> attention ->
+O-proj GEMM(+bias, +residual in the epilogue) -> LN -> FC GEMM(+bias, GELU in
+the epilogue) -> proj GEMM(+bias, +residual).  Llama: RMSNorm, RoPE in the
+split kernel, GQA, gate|up packed so SiLU(g)*u happens in the GEMM epilogue.
+With ``fp8=True`` every projection uses e4m3 weights (per-channel scales) and
+per-token-quantised activations on the scaled MFMA (GPT-2 XL config).
+All positions/lengths live in device memory so a decode step is one graph.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from ..models import model_info
+from ..models.llama3 import rope_tables
+from ..ops import transformer_ops as T_
+from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, linear, pack_gate_up
+from .stages import StageCompute, StageOutput
+
+
+def _bf(t, dev):
+    return t.to(device=dev, dtype=torch.bfloat16).contiguous()
+
+
+def _f32(t, dev):
+    return t.to(device=dev, dtype=torch.float32).contiguous()
+
+
+@dataclass
+class LayerW:
+    ln1_w: torch.Tensor
+    ln1_b: Optional[torch.Tensor]
+    w_qkv: object
+    b_qkv: Optional[torch.Tensor]
+    w_o: object
+    b_o: Optional[torch.Tensor]
+    ln2_w: torch.Tensor
+    ln2_b: Optional[torch.Tensor]
+    w_up: object          # gpt2: c_fc; llama: packed gate|up
+    b_up: Optional[torch.Tensor]
+    w_down: object
+    b_down: Optional[torch.Tensor]
+
+
+class TransformerStage(StageCompute):
+    def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
+                 device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
+                 fp8: bool = False):
+        info = model_info(model)
+        self.model, self.family, self.cfg = model, info.family, info.cfg
+        self.start, self.end, self.first, self.last = start, end, first, last
+        self.device = dev = torch.device(device)
+        self.fp8 = fp8
+        c = self.cfg
+        self.d = c.n_embd
+        self.H = c.n_head
+        self.Hkv = getattr(c, "n_kv_head", c.n_head)
+        self.hd = c.n_embd // c.n_head
+        self.V = c.vocab_size
+        self.Vpad = -(-self.V // 64) * 64
+        self.eps = 1e-5 if self.family == "gpt2" else c.norm_eps
+        self.rms = self.family == "llama3"
+        self.max_batch, self.max_seq = max_batch, max_seq
+        self.max_tokens = max_tokens or max_batch * max_seq
+        self.layers: List[LayerW] = [self._pack_layer(sd, j) for j in range(end - start + 1)]
+        if first:
+            if self.family == "gpt2":
+                self.wte, self.wpe = _bf(sd["wte.weight"], dev), _bf(sd["wpe.weight"], dev)
+            else:
+                self.wte, self.wpe = _bf(sd["embed_tokens.weight"], dev), None
+        if last:
+            if self.family == "gpt2":
+                self.lnf_w, self.lnf_b = _f32(sd["ln_f.weight"], dev), _f32(sd["ln_f.bias"], dev)
+            else:
+                self.lnf_w, self.lnf_b = _f32(sd["norm.weight"], dev), None
+            self.w_head = self._w(sd["lm_head.weight"])
+        # RoPE tables (Llama)
+        self.cos = self.sin = None
+        if self.family == "llama3":
+            cos, sin = rope_tables(c, max_seq)
+            self.cos, self.sin = _f32(cos, dev), _f32(sin, dev)
+        # KV cache: [layer] -> (B, Hkv, S, hd)
+        L = len(self.layers)
+        self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=torch.bfloat16, device=dev)
+        self.vc = torch.zeros_like(self.kc)
+        self._alloc(self.max_tokens)
+
+    # ------------------------------------------------------------------ weights
+    def _w(self, w):
+        if self.fp8:
+            from ..ops.fp8 import quantize_weight
+            return quantize_weight(w, self.device)
+        return _bf(w, self.device)
+
+    def _pack_layer(self, sd, j) -> LayerW:
+        dev = self.device
+        if self.family == "gpt2":
+            p = f"h.{j}."
+            return LayerW(_f32(sd[p + "ln_1.weight"], dev), _f32(sd[p + "ln_1.bias"], dev),
+                          self._w(sd[p + "attn.c_attn.weight"]), _f32(sd[p + "attn.c_attn.bias"], dev),
+                          self._w(sd[p + "attn.c_proj.weight"]), _f32(sd[p + "attn.c_proj.bias"], dev),
+                          _f32(sd[p + "ln_2.weight"], dev), _f32(sd[p + "ln_2.bias"], dev),
+                          self._w(sd[p + "mlp.c_fc.weight"]), _f32(sd[p + "mlp.c_fc.bias"], dev),
+                          self._w(sd[p + "mlp.c_proj.weight"]), _f32(sd[p + "mlp.c_proj.bias"], dev))
+        p = f"layers.{j}."
+        qkv = torch.cat([sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"],
+                         sd[p + "self_attn.v_proj.weight"]], dim=0)
+        if self.fp8:
+            raise NotImplementedError("fp8 path is implemented for GPT-2 family")
+        gu = pack_gate_up(sd[p + "mlp.gate_proj.weight"].float(), sd[p + "mlp.up_proj.weight"].float())
+        return LayerW(_f32(sd[p + "input_layernorm.weight"], dev), None, self._w(qkv), None,
+                      self._w(sd[p + "self_attn.o_proj.weight"]), None,
+                      _f32(sd[p + "post_attention_layernorm.weight"], dev), None,
+                      self._w(gu), None, self._w(sd[p + "mlp.down_proj.weight"]), None)
+
+    def _alloc(self, ntok: int):
+        dev, c = self.device, self.cfg
+        d, H, Hkv, hd = self.d, self.H, self.Hkv, self.hd
+        ffn = 4 * d if self.family == "gpt2" else c.ffn_dim
+        bf = torch.bfloat16
+        self.buf_h = torch.empty((ntok, d), dtype=bf, device=dev)
+        self.buf_a = torch.empty((ntok, d), dtype=bf, device=dev)
+        self.buf_qkv = torch.empty((ntok, (H + 2 * Hkv) * hd), dtype=bf, device=dev)
+        self.buf_q = torch.empty((ntok * H * hd,), dtype=bf, device=dev)
+        self.buf_att = torch.empty((ntok, H * hd), dtype=bf, device=dev)
+        self.buf_f = torch.empty((ntok, ffn), dtype=bf, device=dev)
+        self.lens = torch.zeros((self.max_batch,), dtype=torch.int32, device=dev)
+        self.splits = T_.decode_splits(self.max_seq, self.max_batch, Hkv)
+        G = H // Hkv
+        self.ws = torch.empty((self.max_batch * Hkv * self.splits * G * (hd + 2),), dtype=torch.float32, device=dev)
+        if self.fp8:
+            from ..ops.fp8 import kpad_of
+            kmax = max(kpad_of(d), kpad_of(ffn))
+            self.q8 = torch.empty((ntok * kmax,), dtype=torch.uint8, device=dev)
+            self.s8 = torch.empty((ntok,), dtype=torch.float32, device=dev)
+        if self.last:
+            self.buf_lnf = torch.empty((ntok, d), dtype=bf, device=dev)
+            self.logits = torch.empty((ntok, self.Vpad), dtype=bf, device=dev)
+            self.next_ids = torch.empty((ntok,), dtype=torch.int32, device=dev)
+
+    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None):
+        if self.fp8:
+            from ..ops.fp8 import linear_fp8
+            return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
+        return linear(x, w, b, act, residual, out)
+
+    # ------------------------------------------------------------------ specs
+    def in_spec(self, batch: int, T: int = 1):
+        if self.first:
+            return (batch, T), torch.int32
+        return (batch * T, self.d), torch.bfloat16
+
+    def out_spec(self, batch: int, T: int = 1):
+        if self.last:
+            return (batch,), torch.int32
+        return (batch * T, self.d), torch.bfloat16
+
+    # ------------------------------------------------------------------ forward
+    def step(self, x: torch.Tensor, pos: torch.Tensor, B: int, T: int, b0: int = 0, out: Optional[torch.Tensor] = None,
+             last_only: bool = True):
+        """Run this stage for B sequences x T new tokens at cache rows
+        [b0, b0+B) and positions ``pos`` (device int32 (B,), tokens already
+        cached).  Returns hidden (B*T, d) bf16, or StageOutput for the last stage."""
+        ntok = B * T
+        if ntok > self.buf_h.shape[0]:
+            raise ValueError(f"stage buffers hold {self.buf_h.shape[0]} tokens, got {ntok}")
+        if b0 + B > self.max_batch:
+            raise ValueError("batch slice exceeds the KV cache")
+        d = self.d
+        if self.first:
+            if x.dtype != torch.int32 or tuple(x.shape) != (B, T):
+                raise ValueError(f"first stage expects int32 ids (B,T)=({B},{T}), got {x.dtype} {tuple(x.shape)}")
+            T_.embed(x, self.wte, self.wpe, self.buf_h, pos)
+            h_in = self.buf_h[:ntok]
+        else:
+            h_in = x.reshape(ntok, d)
+        h = self.buf_h[:ntok]
+        a = self.buf_a[:ntok]
+        if T == 1:
+            torch.add(pos, 1, out=self.lens[:B])
+        for li, L in enumerate(self.layers):
+            kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
+            T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
+            qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[:ntok])
+            T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
+            att = self.buf_att[:ntok]
+            if T == 1:
+                T_.attn_decode(self.buf_q, kc, vc, att, B, self.H, self.Hkv, self.hd, self.lens[:B], self.ws,
+                               self.splits)
+            else:
+                T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
+            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h)
+            T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
+            if self.family == "gpt2":
+                f = self._lin(a, L.w_up, L.b_up, act=ACT_GELU, out=self.buf_f[:ntok])
+            else:
+                f = self._lin(a, L.w_up, None, act=ACT_SILU_MUL, out=self.buf_f[:ntok])
+            self._lin(f, L.w_down, L.b_down, residual=h, out=h)
+            h_in = h
+        if not self.last:
+            if out is not None:
+                out.view(ntok, d).copy_(h)
+                return out
+            return h
+        if last_only:
+            rows, src, ldx = B, h[T - 1:], T * d
+        else:
+            rows, src, ldx = ntok, h, d
+        lnf = self.buf_lnf[:rows]
+        T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)
+        logits = self.logits[:rows]
+        if self.fp8:
+            self._head_fp8(lnf, logits)
+        else:
+            linear(lnf, self.w_head, None, out=logits[:, :self.V])
+        nxt = self.next_ids[:rows]
+        T_.argmax_rows(logits, nxt, n=self.V)
+        if last_only and out is not None:
+            out.copy_(nxt)
+        return StageOutput(logits[:, :self.V], nxt)
+
+    def _head_fp8(self, lnf, logits):
+        from ..ops.fp8 import linear_fp8
+        linear_fp8(lnf, self.w_head, None, 0, None, logits[:, :self.V], self.q8, self.s8)
+
+    def reset(self):
+        self.kc.zero_()
+        self.vc.zero_()
+
+
+def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
+                       max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None):
+    fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
+    info = model_info(model)
+    max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))
+    return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8)
+
+
+# ---------------------------------------------------------------------- drivers
+class ColocatedGenerator:
+    """All stages on one GPU: prefill, then greedy decode with the whole
+    multi-stage decode step captured as one HIP graph."""
+
+    def __init__(self, stages: List[TransformerStage], B: int):
+        self.stages, self.B = stages, B
+        dev = stages[0].device
+        self.pos = torch.zeros((B,), dtype=torch.int32, device=dev)
+        self.ids = torch.zeros((B, 1), dtype=torch.int32, device=dev)
+        self._graph = None
+
+    def _run(self, x, T):
+        h = x
+        for s in self.stages:
+            h = s.step(h, self.pos, self.B, T)
+        return h
+
+    def prefill(self, prompt: torch.Tensor) -> torch.Tensor:
+        B, T = prompt.shape
+        self.pos.zero_()
+        out = self._run(prompt.to(self.stages[0].device, torch.int32).contiguous(), T)
+        self.pos.add_(T)
+        self.ids.copy_(out.pred.view(B, 1))
+        return out.pred
+
+    def _decode_body(self):
+        out = self._run(self.ids, 1)
+        self.pos.add_(1)
+        self.ids.copy_(out.pred.view(self.B, 1))
+        return out.pred
+
+    def capture(self):
+        from .graph import GraphedStep
+        # warmup inside GraphedStep advances pos; snapshot and restore
+        snap_pos, snap_ids = self.pos.clone(), self.ids.clone()
+        self._graph = GraphedStep(self._decode_body, self.stages[0].device, warmup=1)
+        self.pos.copy_(snap_pos)
+        self.ids.copy_(snap_ids)
+
+    def decode(self) -> torch.Tensor:
+        if self._graph is not None:
+            return self._graph()
+        return self._decode_body()
+
+    def generate(self, prompt: torch.Tensor, steps: int, graph: bool = True) -> torch.Tensor:
+        toks = [self.prefill(prompt).clone()]
+        if steps > 1 and graph and self._graph is None:
+            self.capture()
+        for _ in range(steps - 1):
+            toks.append(self.decode().clone())
+        return torch.stack(toks, dim=1)
+
+
+def run_generate_colocated(ctx, args, stages, device) -> int:
+    from ..cli import make_prompt
+    from ..utils.log import log
+    prompt = make_prompt(ctx, args.prompt)
+    B, T = prompt.shape
+    steps = max(1, ctx.pipeline.decode_steps or 1)
+    for s in stages:
+        if s.max_batch < B or s.max_seq < T + steps:
+            raise ValueError("prompt/decode length exceeds the stage KV cache")
+    gen = ColocatedGenerator(stages, B)
+    toks = gen.generate(prompt, steps)
+    torch.cuda.synchronize(device)
+    first = toks[:, 0].tolist()
+    log(f"[{ctx.node_id}] ***** FINAL PREDICTION (Index): {first[0] if len(first) == 1 else first} *****")
+    log(f"[{ctx.node_id}] generated tokens: {toks.tolist()}")
+    return 0
+
+
+def run_generate_dist(ctx, args, stage, info) -> int:
+    """One rank per stage; greedy decode with the token back-edge last -> stage 0."""
+    from ..cli import make_prompt
+    from ..parallel.links import P2PLink
+    from ..utils.log import log
+    pipe = ctx.pipeline
+    S = pipe.num_parts
+    r = ctx.part_index
+    dev = info.device
+    prompt = make_prompt(ctx, args.prompt)
+    B, T = prompt.shape
+    steps = max(1, pipe.decode_steps or 1)
+    pos = torch.zeros((B,), dtype=torch.int32, device=dev)
+    prev = P2PLink(r - 1, dev) if r > 0 else None
+    nxt = P2PLink(r + 1, dev) if r < S - 1 else None
+    back = P2PLink(S - 1 if r == 0 else 0, dev) if S > 1 else None
+    ids = prompt.to(dev, torch.int32)
+    toks = []
+    for step in range(steps):
+        Tn = T if step == 0 else 1
+        if r == 0:
+            x = ids
+        else:
+            x = torch.empty((B * Tn, stage.d), dtype=torch.bfloat16, device=dev)
+            prev.recv(x)
+        y = stage.step(x, pos, B, Tn)
+        pos.add_(Tn)
+        if nxt is not None:
+            nxt.send(y)
+        if stage.last:
+            nid = y.pred.clone()
+            if S > 1:
+                back.send(nid)
+            toks.append(nid)
+        if r == 0:
+            if S > 1:
+                nid = torch.empty((B,), dtype=torch.int32, device=dev)
+                back.recv(nid)
+                toks.append(nid)
+            ids = toks[-1].view(B, 1).contiguous()
+    if r == 0:
+        t = torch.stack(toks, 1).cpu()
+        first = t[:, 0].tolist()
+        log(f"[{ctx.node_id}] ***** FINAL PREDICTION (Index): {first[0] if len(first) == 1 else first} *****")
+        log(f"[{ctx.node_id}] generated tokens: {t.tolist()}")
+    return 0
+
+
+# ---------------------------------------------------------------------- smoke / golden check
+def smoke(dev) -> None:
+    """GPT-2-tiny and Llama-tiny, 2 stages each, vs the torch golden model."""
+    from .. import checkpoint as ckpt
+    from ..models import build_golden_stage
+    for model in ("gpt2-tiny", "llama3-tiny"):
+        n = model_info(model).num_layers
+        ranges = [(0, n // 2 - 1), (n // 2, n - 1)]
+        sds = [ckpt.random_stage_state_dict(model, a, b, i == 0, i == 1, 7) for i, (a, b) in enumerate(ranges)]
+        stages = [TransformerStage(model, sds[i], a, b, i == 0, i == 1, dev, max_batch=2, max_seq=64)
+                  for i, (a, b) in enumerate(ranges)]
+        golden = []
+        for i, (a, b) in enumerate(ranges):
+            g = build_golden_stage(model, a, b, i == 0, i == 1)
+            g.load_state_dict(sds[i])
+            golden.append(g.eval())
+        g = torch.Generator().manual_seed(3)
+        prompt = torch.randint(0, model_info(model).cfg.vocab_size, (2, 16), generator=g)
+        gen = ColocatedGenerator(stages, 2)
+        toks = gen.generate(prompt, 3, graph=True)
+        torch.cuda.synchronize(dev)
+        # golden greedy (full recompute, fp32)
+        seq = prompt.clone()
+        ref = []
+        with torch.no_grad():
+            for _ in range(3):
+                h = seq
+                for gs in golden:
+                    h = gs(h)
+                nid = h[:, -1].argmax(-1)
+                ref.append(nid)
+                seq = torch.cat([seq, nid[:, None]], 1)
+        ref = torch.stack(ref, 1)
+        agree = (toks.cpu().long() == ref).float().mean().item()
+        if agree < 0.66:
+            raise AssertionError(f"smoke {model}: greedy tokens disagree with golden ({toks.tolist()} vs {ref.tolist()})")
