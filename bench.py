@@ -50,11 +50,14 @@ def parse():
     ap.add_argument("--placement", default="interleaved", choices=["interleaved", "linear"])
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
+    ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     return ap.parse_args()
 
 
-def dist_setup(n):
+def dist_setup(n, cpu=False):
     from distributed_neural_networks_amd.parallel import comm
+    if cpu:
+        return comm.init("gloo")
     if n > 1 or "WORLD_SIZE" in os.environ:
         info = comm.init("nccl")
     else:
@@ -65,18 +68,29 @@ def dist_setup(n):
 
 def stages_for(device):
     from distributed_neural_networks_amd import checkpoint as ckpt
-    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
-    s0 = CifarHipStage(ckpt.random_stage_state_dict("cifar10", 0, 1, True, False, 0), 0, 1, device)
-    s1 = CifarHipStage(ckpt.random_stage_state_dict("cifar10", 2, 3, False, True, 0), 2, 3, device)
-    return s0, s1
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage, TorchStage
+    sd0 = ckpt.random_stage_state_dict("cifar10", 0, 1, True, False, 0)
+    sd1 = ckpt.random_stage_state_dict("cifar10", 2, 3, False, True, 0)
+    if device.type == "cpu":  # schedule-test mode only (never used for a reported number)
+        return (TorchStage("cifar10", sd0, 0, 1, True, False, device),
+                TorchStage("cifar10", sd1, 2, 3, False, True, device))
+    return CifarHipStage(sd0, 0, 1, device), CifarHipStage(sd1, 2, 3, device)
+
+
+def dsync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def sync_time(info):
     import torch.distributed as dist
-    torch.cuda.synchronize()
+    dsync(info.device)
     if info.world > 1:
-        dist.barrier(device_ids=[info.device.index])
-        torch.cuda.synchronize()
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.device.index])
+        else:
+            dist.barrier()
+        dsync(info.device)
     return time.perf_counter()
 
 
@@ -127,8 +141,9 @@ def bench_interleaved(args, info):
     mb = per_peer * (N - 1)
     g = torch.Generator(device=dev).manual_seed(1 + r)
     xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
-    y0 = [torch.empty((mb, 4096), dtype=torch.bfloat16, device=dev) for _ in range(M)]
-    rx = [torch.empty((mb, 4096), dtype=torch.bfloat16, device=dev) for _ in range(M)]
+    bdt = s0.out_spec(1)[1]
+    y0 = [torch.empty((mb, 4096), dtype=bdt, device=dev) for _ in range(M)]
+    rx = [torch.empty((mb, 4096), dtype=bdt, device=dev) for _ in range(M)]
     probs = [torch.empty((mb, 10), device=dev) for _ in range(M)]
     splits = [0 if p == r else per_peer for p in range(N)]
 
@@ -151,7 +166,7 @@ def bench_interleaved(args, info):
     t1 = sync_time(info)
     # latency: one image per peer through stage0 -> all-to-all -> stage1
     lx = torch.randn((N - 1, 3, 32, 32), device=dev, generator=g)
-    ly = torch.empty((N - 1, 4096), dtype=torch.bfloat16, device=dev)
+    ly = torch.empty((N - 1, 4096), dtype=bdt, device=dev)
     lr = torch.empty_like(ly)
     lp = torch.empty((N - 1, 10), device=dev)
     one = [0 if p == r else 1 for p in range(N)]
@@ -162,7 +177,7 @@ def bench_interleaved(args, info):
         s0.forward(lx, ly)
         dist.all_to_all_single(lr, ly, one, one)
         s1.forward(lr, lp)
-        torch.cuda.synchronize()
+        dsync(dev)
         ts.append(time.perf_counter() - a)
     return t1 - t0, mb * M, statistics.median(ts) * 1e3, f"pp2-interleaved-a2a-x{N}"
 
@@ -201,7 +216,7 @@ def main():
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
         import gpt_bench
         return gpt_bench.main(args)
-    info = dist_setup(args.gpus)
+    info = dist_setup(args.gpus, args.cpu)
     N = info.world
     if N == 1:
         el, imgs_per_gpu, p50, par = bench_colocated(args, info)

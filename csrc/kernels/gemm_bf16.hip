@@ -149,50 +149,64 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
 // straight to VGPRs (no LDS round trip: guide §5 table, GEMV row). A (tiny) is
 // read through L1/L2. Uses mfma_f32_16x16x32_bf16 with M padded to 16.
 // ---------------------------------------------------------------------------
-template <int ACT, bool OUT_F32>
+template <int ACT, bool OUT_F32, int MT>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
     int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) f32x4 red[4][64];
+  // MT 16-row M tiles share every W fragment (M <= 16*MT rows).
+  __shared__ __attribute__((aligned(16))) f32x4 red[4][MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const int n = n0 + (lane & 15);
   const int nc = n < N ? n : N - 1;
-  const int mrow = lane & 15;
-  const int mc = mrow < M ? mrow : M - 1;
   const int kq = (lane >> 4) * 8;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[MT];
+  const bf16_t* ap[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int mrow = t * 16 + (lane & 15);
+    ap[t] = A + (size_t)(mrow < M ? mrow : M - 1) * lda;
+  }
   // K split into 4 contiguous quarters (one per wave), each a multiple of 32
   const int kper = ((K / 32 + 3) / 4) * 32;
   const int kbeg = wave * kper;
   const int kend = min(K, kbeg + kper);
   const bf16_t* wp = W + (size_t)nc * ldw;
-  const bf16_t* ap = A + (size_t)mc * lda;
   int k = kbeg;
   for (; k + 128 <= kend; k += 128) {
-    bf16x8 b[4], a[4];
+    bf16x8 b[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const bf16x8*>(wp + k + u * 32 + kq);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(ap + k + u * 32 + kq);
+    for (int t = 0; t < MT; ++t) {
+      bf16x8 a[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
+      for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(ap[t] + k + u * 32 + kq);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc[t], 0, 0, 0);
+    }
   }
   for (; k < kend; k += 32) {
-    bf16x8 b = *reinterpret_cast<const bf16x8*>(wp + k + kq);
-    bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + k + kq);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-  }
-  red[wave][lane] = acc;
-  __syncthreads();
-  if (wave == 0) {
-    f32x4 s = red[0][lane];
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(wp + k + kq);
 #pragma unroll
-    for (int w = 1; w < 4; ++w) s += red[w][lane];
-    const float bb = (bias != nullptr && n < N) ? bias[n] : 0.f;
+    for (int t = 0; t < MT; ++t) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap[t] + k + kq);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t) red[wave][t][lane] = acc[t];
+  __syncthreads();
+  // reduction + epilogue: wave w handles M tiles t = w, w+4, ...
+  const float bb = (bias != nullptr && n < N) ? bias[n] : 0.f;
+  for (int t = wave; t < MT; t += 4) {
+    f32x4 s = red[0][t][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) s += red[w][t][lane];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = (lane >> 4) * 4 + r;
+      const int m = t * 16 + (lane >> 4) * 4 + r;
       if (m < M && n < N) {
         float v = s[r] + bb;
         if (ACT == ACT_RELU) v = fmaxf(v, 0.f);
@@ -226,10 +240,15 @@ using namespace dnn;
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                         const void* R, int ldr, int M, int N, int K, hipStream_t st) {
-  if (M <= 16 && ACT != ACT_SILU_MUL) {
+  if (M <= 64 && ACT != ACT_SILU_MUL) {
     dim3 grid((N + 15) / 16);
-    hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32>), grid, dim3(256), 0, st, (const bf16_t*)A, lda,
-                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);
+#define SK(MTV)                                                                                         \
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MTV>), grid, dim3(256), 0, st, (const bf16_t*)A, lda, \
+                     (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K)
+    if (M <= 16) SK(1);
+    else if (M <= 32) SK(2);
+    else SK(4);
+#undef SK
     return;
   }
   const int tiles = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);

@@ -214,10 +214,17 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
         log(f"[{nid}] ERROR: Cannot initiate inference, NEXT_NODE_ADDRESS is not set.")
         return 1
     client = NodeClient(ctx.next_address) if ctx.num_parts > 1 else None
-    if client is not None and not await client.wait_ready(60.0):
-        log(f"!!! [{nid}] next node {ctx.next_address} did not become healthy")
-        await client.close()
-        return 1
+    # readiness barrier over every downstream stage (replaces the reference's sleep(2))
+    for n in ctx.pipeline.stages[1:]:
+        c = client if n.address == ctx.next_address else NodeClient(n.address)
+        ok = await c.wait_ready(120.0)
+        if c is not client:
+            await c.close()
+        if not ok:
+            log(f"!!! [{nid}] node {n.id} ({n.address}) did not become healthy")
+            if client is not None:
+                await client.close()
+            return 1
     rc = 0
     for r in range(args.num_requests):
         x = load_image(args.input_image, nid) if fam == "cifar" else make_prompt(ctx, args.prompt)

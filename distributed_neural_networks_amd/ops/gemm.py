@@ -40,7 +40,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     r2 = None
     if residual is not None:
         r2 = residual.reshape(-1, residual.shape[-1]) if residual.dim() != 2 else residual
-    if a == ACT_SILU_MUL and M <= 16:
+    if a == ACT_SILU_MUL and M <= 64:
         # skinny path: packed gate|up GEMM then the elementwise SwiGLU
         tmp = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
         check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(tmp), N, 0, 0, 0, M, N, K,

@@ -132,6 +132,37 @@ class TorchStage(StageCompute):
             return (batch, seq, info.cfg.vocab_size), self.dtype
         return (batch, seq, info.cfg.n_embd), self.dtype
 
+    @property
+    def d(self) -> int:
+        return model_info(self.model).cfg.n_embd
+
+    @property
+    def act_dtype(self) -> torch.dtype:
+        return self.dtype
+
+    @torch.no_grad()
+    def step(self, x, pos, B: int, T: int, b0: int = 0, out=None, last_only: bool = True):
+        """KV-cached transformer step (CPU golden path; same contract as
+        ``TransformerStage.step``): x = ids (B,T) on the first stage, else
+        hidden (B*T, d); ``pos`` = tokens already cached (uniform per batch)."""
+        cfg = model_info(self.model).cfg
+        p = int(pos[0]) if isinstance(pos, torch.Tensor) else int(pos)
+        if getattr(self, "_kv", None) is None or self._kv[0][0].shape[0] != B:
+            S = getattr(cfg, "block_size", getattr(cfg, "max_seq", 1024))
+            hkv = getattr(cfg, "n_kv_head", cfg.n_head)
+            hd = cfg.n_embd // cfg.n_head
+            self._kv = [(torch.zeros(B, hkv, S, hd, dtype=self.dtype), torch.zeros(B, hkv, S, hd, dtype=self.dtype))
+                        for _ in range(len(self.module.h if self.family == "gpt2" else self.module.layers))]
+        if self.first:
+            h = x.to(torch.int64).view(B, T)
+        else:
+            h = x.view(B, T, cfg.n_embd).to(self.dtype)
+        y = self.module(h, self._kv, p, last_only=last_only)
+        if self.last:
+            logits = y[:, -1, :] if last_only else y.reshape(B * T, -1)
+            return StageOutput(logits, y[:, -1, :].argmax(dim=-1).to(torch.int32))
+        return y.reshape(B * T, cfg.n_embd)
+
     @torch.no_grad()
     def forward(self, x, out=None):
         y = self.module(x.to(self.device))

@@ -332,21 +332,28 @@ def run_generate_dist(ctx, args, stage, info) -> int:
     S = pipe.num_parts
     r = ctx.part_index
     dev = info.device
-    prompt = make_prompt(ctx, args.prompt)
-    B, T = prompt.shape
-    steps = max(1, pipe.decode_steps or 1)
-    pos = torch.zeros((B,), dtype=torch.int32, device=dev)
+    from ..parallel.links import KIND_DATA
     prev = P2PLink(r - 1, dev) if r > 0 else None
     nxt = P2PLink(r + 1, dev) if r < S - 1 else None
     back = P2PLink(S - 1 if r == 0 else 0, dev) if S > 1 else None
-    ids = prompt.to(dev, torch.int32)
+    steps = max(1, pipe.decode_steps or 1)
+    # stage 0 owns the prompt; its shape travels down the chain in a header
+    if r == 0:
+        prompt = make_prompt(ctx, args.prompt)
+        B, T = prompt.shape
+        ids = prompt.to(dev, torch.int32)
+    else:
+        _, B, T, steps = prev.recv_header()
+    if nxt is not None:
+        nxt.send_header(KIND_DATA, B, T, steps)
+    pos = torch.zeros((B,), dtype=torch.int32, device=dev)
     toks = []
     for step in range(steps):
         Tn = T if step == 0 else 1
         if r == 0:
             x = ids
         else:
-            x = torch.empty((B * Tn, stage.d), dtype=torch.bfloat16, device=dev)
+            x = torch.empty((B * Tn, stage.d), dtype=getattr(stage, "act_dtype", torch.bfloat16), device=dev)
             prev.recv(x)
         y = stage.step(x, pos, B, Tn)
         pos.add_(Tn)
