@@ -34,6 +34,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("cifar_stage0", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
     return dnn_cifar_stage0(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
   });
+  m.def("cifar_stage0_v2", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
+    return dnn_cifar_stage0_v2(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
+  });
   m.def("cifar_head_tail", [](u64 hid, u64 w2p, u64 b2, u64 probs, u64 pred, int B, u64 st) {
     return dnn_cifar_head_tail(CP(hid), CP(w2p), CFP(b2), FP(probs), IP(pred), B, ST(st));
   });

@@ -222,9 +222,191 @@ __global__ __launch_bounds__(256) void cifar_head_tail_kernel(const bf16_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stage 0, v2. Same math, re-laid-out for the LDS:
+//  * input staged as HWC4 bf16 [34][40][4] (3 channels + 1 zero): conv1's
+//    im2col K = (ky, kx<4, c<4) = 48 (3 MFMA k-steps of 16, zero weights on
+//    kx=3/c=3), so a lane's 8 A-values for a k-step are the 2 adjacent pixels
+//    (x+2h, x+2h+1) x 4 channels = 2 x ds_read_b64 (vs 27 scalar reads in v1);
+//    the 320-B row pitch puts the 4 rows of a 4x8 pixel block on disjoint banks.
+//  * act1 = padded HWC [18][24 pitch][32 ch + 8 pad] bf16 (80-B pixels): every
+//    ds_read_b128 A-fragment of conv2 is conflict-free without an XOR, so all
+//    reads are lane_base + compile-time immediates (searched exhaustively over
+//    the 4 lane groups x 9 taps x 4 chunks; tools/lds_layout_search.py).
+//  * conv1 epilogue: two quad DPP exchanges gather 4 channels of one pooled
+//    pixel per lane -> one ds_write_b64 (vs 4 ds_write_b16).
+//  * conv2 epilogue: the 2 horizontally adjacent pooled pixels are packed ->
+//    ds_write_b32 into a 136-B-pitch staging image (2-way instead of 32-way).
+// ---------------------------------------------------------------------------
+constexpr int V2_XW = 40;                                     // input row pitch (pixels)
+constexpr int V2_XIN_BYTES = 34 * V2_XW * 8;                  // 10880
+constexpr int V2_A1_OFF = V2_XIN_BYTES;                       // 10880 (16-B aligned)
+constexpr int V2_A1W = 24, V2_A1P = 80;                       // act1 pitch (pixels), pixel stride (bytes)
+constexpr int V2_A1_BYTES = 18 * V2_A1W * V2_A1P;             // 34560
+constexpr int V2_OB_OFF = V2_A1_OFF + V2_A1_BYTES;            // 45440
+constexpr int V2_OBP = 136;                                   // obuf channel pitch (bytes)
+constexpr int V2_LDS = V2_OB_OFF + 64 * V2_OBP;               // 54144
+
+__device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
+
+__global__ __launch_bounds__(256, 2) void cifar_stage0_v2_kernel(
+    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
+    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B) {
+  __shared__ __attribute__((aligned(16))) char smem[V2_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+
+  for (int i = tid; i < V2_OB_OFF / 16; i += 256) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+
+  // conv1 weights, B[k][oc] with k = ky*16 + kx*4 + c (48 = 3 k-steps)
+  bf16x8 w1f[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 48 + s * 16 + h * 8);
+  const float bias1 = b1[r32];
+  const int nt = wave & 1;
+  const int oc2 = nt * 32 + r32;
+  bf16x8 w2f[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
+  const float bias2 = b2[oc2];
+
+  // input prefetch: thread owns pixels p = tid + 256*i (i < 4), 3 channels each
+  float pf[4][3];
+  int img = blockIdx.x;
+  auto load_img = [&](int im) {
+    const float* xb = x + (size_t)im * 3072;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pf[i][c] = xb[c * 1024 + tid + 256 * i];
+  };
+  if (img < B) load_img(img);
+  __syncthreads();
+
+  // per-lane constant parts of the LDS addresses
+  const int c1_lane = ((r32 >> 3) * V2_XW + (r32 & 7) + 2 * h) * 8;              // conv1 A base (bytes)
+  const int c2_lane = V2_A1_OFF + ((r32 >> 3) * V2_A1W + (r32 & 7)) * V2_A1P + h * 16;  // conv2 A base
+  const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);  // pooled pixel this lane stores after the DPP gather
+  const int cb = r32 & ~3;
+
+  for (; img < B; img += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + 256 * i, yy = p >> 5, xx = p & 31;
+      uint2 v;
+      v.x = pack2bf(pf[i][0], pf[i][1]);
+      v.y = pack2bf(pf[i][2], 0.f);
+      *reinterpret_cast<uint2*>(smem + ((yy + 1) * V2_XW + xx + 1) * 8) = v;
+    }
+    __syncthreads();
+
+    // ---- conv1: 32 tiles of 4x8 output pixels, 3 k-steps each ----
+    for (int t = wave; t < 32; t += 4) {
+      const int ty = t >> 2, tx = t & 3;
+      const char* abase = smem + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
+        bf16x8 a;
+        a[0] = (short)(lo.x & 0xffff); a[1] = (short)(lo.x >> 16); a[2] = (short)(lo.y & 0xffff); a[3] = (short)(lo.y >> 16);
+        a[4] = (short)(hi.x & 0xffff); a[5] = (short)(hi.x >> 16); a[6] = (short)(hi.y & 0xffff); a[7] = (short)(hi.y >> 16);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
+      }
+      float v[4];
+#pragma unroll
+      for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+        for (int qx = 0; qx < 2; ++qx) {
+          const int g0 = (2 * qy) * 4 + 2 * qx;
+          v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
+        }
+      // gather 4 channels of one pooled pixel per lane (quad DPP exchanges)
+      const bool odd = r32 & 1;
+      const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
+      const float r0 = __int_as_float(dpp_xor1(s0)), r1 = __int_as_float(dpp_xor1(s1));
+      uint32_t u0, u1;
+      if (!odd) { u0 = pack2bf(v[0], r0); u1 = pack2bf(v[1], r1); }
+      else { u0 = pack2bf(r0, v[2]); u1 = pack2bf(r1, v[3]); }
+      const bool hi2 = r32 & 2;
+      const uint32_t snd = hi2 ? u0 : u1;
+      const uint32_t rcv = (uint32_t)dpp_xor2((int)snd);
+      const uint32_t mine = hi2 ? u1 : u0;
+      uint2 w;
+      w.x = hi2 ? rcv : mine;
+      w.y = hi2 ? mine : rcv;
+      const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
+      *reinterpret_cast<uint2*>(smem + V2_A1_OFF + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
+    }
+    __syncthreads();
+
+    const int nimg = img + gridDim.x;
+    if (nimg < B) load_img(nimg);
+
+    // ---- conv2 ----
+    {
+      f32x16 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
+      const int mt0 = (wave >> 1) * 4;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        const int kk = s >> 1, ky = kk / 3, kx = kk % 3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+          const int off = ((4 * ty2 + ky) * V2_A1W + 8 * tx2 + kx) * V2_A1P + (s & 1) * 32;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + c2_lane + off);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2f[s], acc[i], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+#pragma unroll
+        for (int qy = 0; qy < 2; ++qy) {
+          float pv[2];
+#pragma unroll
+          for (int qx = 0; qx < 2; ++qx) {
+            const int g0 = (2 * qy) * 4 + 2 * qx;
+            pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias2, 0.f);
+          }
+          const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;
+          *reinterpret_cast<uint32_t*>(smem + V2_OB_OFF + oc2 * V2_OBP + (PY * 8 + PX) * 2) = pack2bf(pv[0], pv[1]);
+        }
+      }
+    }
+    __syncthreads();
+    {
+      // 64 channel rows x 128 B -> global (coalesced 16-B stores; reads 2 x 8 B from the padded image)
+      int4* dst = reinterpret_cast<int4*>(out + (size_t)img * 4096);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u;            // 16-B chunk index 0..511
+        const int ch = e >> 3, j = e & 7;
+        const char* src = smem + V2_OB_OFF + ch * V2_OBP + j * 16;
+        const uint2 a = *reinterpret_cast<const uint2*>(src), b = *reinterpret_cast<const uint2*>(src + 8);
+        dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
+      }
+    }
+  }
+}
+
 }  // namespace dnn
 
 using namespace dnn;
+
+extern "C" int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                                   const float* b2, int B, int grid, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (grid <= 0) grid = 512;
+  if (grid > B) grid = B;
+  hipLaunchKernelGGL(cifar_stage0_v2_kernel, dim3(grid), dim3(256), 0, st, x, (bf16_t*)out, (const bf16_t*)w1p, b1,
+                     (const bf16_t*)w2p, b2, B);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
                                 const float* b2, int B, int grid, hipStream_t st) {

@@ -25,10 +25,14 @@ from .gemm import ACT_RELU, linear
 
 @dataclass
 class CifarStage0Weights:
-    w1p: torch.Tensor
+    w1p: torch.Tensor      # v1: [32][32], k = c*9+ky*3+kx
     b1: torch.Tensor
     w2p: torch.Tensor
     b2: torch.Tensor
+    w1p2: torch.Tensor = None  # v2: [32][48], k = ky*16 + kx*4 + c (kx<3, c<3 real)
+
+
+STAGE0_VARIANT = 2
 
 
 @dataclass
@@ -44,11 +48,14 @@ def pack_stage0(sd: Dict[str, torch.Tensor], device) -> CifarStage0Weights:
     w1p = torch.zeros(32, 32)
     w1p[:, :27] = w1
     w2 = sd["conv2.weight"].float().permute(0, 2, 3, 1).reshape(64, 288)  # (oc, ky, kx, c)
+    w1p2 = torch.zeros(32, 3, 4, 4)  # (oc, ky, kx, c) zero-padded kx=3, c=3
+    w1p2[:, :, :3, :3] = sd["conv1.weight"].float().permute(0, 2, 3, 1)
     return CifarStage0Weights(
         w1p=w1p.to(device=device, dtype=torch.bfloat16).contiguous(),
         b1=sd["conv1.bias"].float().to(device).contiguous(),
         w2p=w2.to(device=device, dtype=torch.bfloat16).contiguous(),
-        b2=sd["conv2.bias"].float().to(device).contiguous())
+        b2=sd["conv2.bias"].float().to(device).contiguous(),
+        w1p2=w1p2.reshape(32, 48).to(device=device, dtype=torch.bfloat16).contiguous())
 
 
 def pack_head(sd: Dict[str, torch.Tensor], device) -> CifarHeadWeights:
@@ -62,7 +69,7 @@ def pack_head(sd: Dict[str, torch.Tensor], device) -> CifarHeadWeights:
 
 
 def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.Tensor] = None,
-                   grid: int = 0) -> torch.Tensor:
+                   grid: int = 0, variant: Optional[int] = None) -> torch.Tensor:
     """x: (B,3,32,32) fp32 contiguous -> (B,4096) bf16."""
     if x.dtype != torch.float32 or not x.is_contiguous() or tuple(x.shape[1:]) != (3, 32, 32):
         raise ValueError(f"stage0: expected contiguous fp32 (B,3,32,32), got {x.dtype} {tuple(x.shape)}")
@@ -71,8 +78,12 @@ def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.T
         out = torch.empty((B, 4096), dtype=torch.bfloat16, device=x.device)
     if tuple(out.shape) != (B, 4096) or out.dtype != torch.bfloat16 or not out.is_contiguous():
         raise ValueError("stage0: bad output buffer")
-    check(lib().cifar_stage0(ptr(x), ptr(out), ptr(w.w1p), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
-                             stream_ptr()), "cifar_stage0")
+    if (variant or STAGE0_VARIANT) == 2:
+        check(lib().cifar_stage0_v2(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
+                                    stream_ptr()), "cifar_stage0_v2")
+    else:
+        check(lib().cifar_stage0(ptr(x), ptr(out), ptr(w.w1p), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
+                                 stream_ptr()), "cifar_stage0")
     return out
 
 

@@ -1,0 +1,5 @@
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1; echo rc=$?
+grep -oE "^\s*(SQ|TCC|TCP|TA|TD|GRBM|SQC)[A-Z0-9_]*" gpurun_out/pmc_list.txt | sort -u | head -5
+wc -l gpurun_out/pmc_list.txt
