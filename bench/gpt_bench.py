@@ -40,6 +40,7 @@ def parse(argv=None):
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--prefill_iters", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     return ap.parse_args(argv)
 
 
@@ -185,6 +186,67 @@ def main(args=None):
             lat.append(time.perf_counter() - ta)
 
     decode_round.started = [False] * M
+
+    # One HIP graph per microbatch for this group's decode compute (the P2P
+    # hops stay outside: blocking RCCL send/recv order the compute stream).
+    graphs = {}
+    if stages and not args.no_graph:
+        from distributed_neural_networks_amd.runtime.graph import GraphedStep
+        gout = {}
+
+        def body(m):
+            x = cur[m] if grp == 0 else dec_x[m]
+            y = run_group(x, m, 1)
+            pos[m].add_(1)
+            if isinstance(y, torch.Tensor):
+                gout[m] = y
+            else:
+                nid[m].copy_(y.pred)
+            return None
+
+        for m in range(M):
+            snap = pos[m].clone()
+            graphs[m] = GraphedStep(lambda m=m: body(m), dev, warmup=1)
+            pos[m].copy_(snap)
+        torch.cuda.synchronize()
+
+        class _Out:
+            def __init__(self, p):
+                self.pred = p
+
+    def group_step(x, m):
+        if graphs:
+            y = graphs[m]()
+            return gout[m] if m in gout else _Out(nid[m])
+        y = run_group(x, m, 1)
+        pos[m].add_(1)
+        return y
+
+    def decode_round():  # noqa: F811 (graph-aware version)
+        for m in range(M):
+            if not stages:
+                continue
+            ta = time.perf_counter()
+            if grp == 0:
+                if groups > 1 and back_from is not None and decode_round.started[m]:
+                    back_from.recv(nid[m])
+                    cur[m].copy_(nid[m].view(B, 1))
+                x = cur[m]
+            else:
+                x = dec_x[m]
+                prev.recv(x)
+            y = group_step(x, m)
+            if nxt is not None:
+                nxt.send(y)
+            else:
+                if groups > 1:
+                    back_to0.send(y.pred)
+                else:
+                    cur[m].copy_(y.pred.view(B, 1))
+            decode_round.started[m] = True
+            lat.append(time.perf_counter() - ta)
+
+    decode_round.started = [False] * M
     for _ in range(args.warmup):
         decode_round()
     t0 = sync()
@@ -197,6 +259,14 @@ def main(args=None):
     t1 = sync()
     decode_s = (t1 - t0) / args.steps
     dec_tok = B * M * replicas
+    # per-token latency of one decode step (single group only: a synced step)
+    tok_lat = []
+    if groups == 1 and stages:
+        for _ in range(16):
+            ta = sync()
+            decode_round()
+            tok_lat.append(sync() - ta)
+    lat[:] = tok_lat
 
     def mx(v):
         if N == 1:
@@ -217,7 +287,8 @@ def main(args=None):
             "data": "synthetic prompts, random-init weights",
             "prefill_tokens_per_s": round(prefill_tok / prefill_s, 1),
             "prefill_ms_per_round": round(prefill_s * 1e3, 3),
-            "decode_p50_step_ms_per_microbatch": round(statistics.median(lat) * 1e3, 4) if lat else None,
+            "decode_p50_token_latency_ms": round(statistics.median(lat) * 1e3, 4) if lat else None,
+            "hip_graph_decode": bool(graphs),
             "config": {"model": model, "stages": S, "gpu_groups": groups, "replicas": replicas,
                        "micro_batch": B, "microbatches": M, "prompt_len": T0, "seq_len": max_seq,
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},

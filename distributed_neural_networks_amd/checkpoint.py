@@ -150,30 +150,40 @@ def unexpected_keys(model: str, full_sd, start: int, end: int, first: bool, last
 
 
 def random_stage_state_dict(model: str, start: int, end: int, first: bool, last: bool,
-                            seed: int = 0) -> Dict[str, torch.Tensor]:
+                            seed: int = 0, device=None) -> Dict[str, torch.Tensor]:
     """Random-init weights for one stage, identical to slicing a random full model
-    generated with the same seed (layer-indexed seeding)."""
+    generated with the same seed (layer-indexed seeding).  ``device`` generates
+    directly on that device (billion-parameter stages without a host copy);
+    values then follow the device RNG, so compare only within one device."""
     info = model_info(model)
     if info.family == "cifar":
         return {k: v for k, v in cifar.random_state_dict(seed).items()
                 if k.split(".")[0] in {n for u in range(start, end + 1) for n in cifar.UNIT_KEYS[u]}}
-    from .models import build_golden_stage
-    stage = build_golden_stage(model, start, end, first, last)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    shapes = _stage_shapes(model, start, end, first, last)
     sd = {}
-    for local, t in stage.state_dict().items():
-        g = torch.Generator().manual_seed(_key_seed(seed, _global_key(model, local, start)))
+    for local, shape in shapes.items():
+        g = torch.Generator(device=dev).manual_seed(_key_seed(seed, _global_key(model, local, start)))
         if local.endswith("bias"):
-            sd[local] = torch.zeros_like(t)
+            sd[local] = torch.zeros(shape, device=dev)
         elif "ln" in local.split(".")[-2] or local.endswith("norm.weight") or "layernorm" in local:
-            sd[local] = torch.ones_like(t)
+            sd[local] = torch.ones(shape, device=dev)
         else:
-            sd[local] = torch.randn(t.shape, generator=g) * 0.02
+            sd[local] = torch.randn(shape, generator=g, device=dev) * 0.02
     if info.family == "gpt2" and last and first:
         sd["lm_head.weight"] = sd["wte.weight"]
     elif info.family == "gpt2" and last:
-        g = torch.Generator().manual_seed(_key_seed(seed, "transformer.wte.weight"))
-        sd["lm_head.weight"] = torch.randn(sd["lm_head.weight"].shape, generator=g) * 0.02
+        g = torch.Generator(device=dev).manual_seed(_key_seed(seed, "transformer.wte.weight"))
+        sd["lm_head.weight"] = torch.randn(sd["lm_head.weight"].shape, generator=g, device=dev) * 0.02
     return sd
+
+
+def _stage_shapes(model: str, start: int, end: int, first: bool, last: bool) -> Dict[str, Tuple[int, ...]]:
+    """Parameter shapes of a stage without materialising it (meta device)."""
+    from .models import build_golden_stage
+    with torch.device("meta"):
+        stage = build_golden_stage(model, start, end, first, last)
+    return {k: tuple(v.shape) for k, v in stage.state_dict().items()}
 
 
 def _global_key(model: str, local: str, start: int) -> str:

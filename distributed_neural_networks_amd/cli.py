@@ -47,6 +47,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--serve_seconds", type=float, default=None, help="non-initiating nodes exit after this long")
     p.add_argument("--device", default=None, help="override device: cpu | cuda | cuda:N")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--trace", default=None, help="write a Chrome trace (host + device spans) to this path")
+    p.add_argument("--metrics", action="store_true", help="print one METRICS json line per stage at exit")
     return p
 
 
@@ -102,14 +104,16 @@ def pick_device(ctx: NodeContext, override: Optional[str]) -> torch.device:
     return torch.device("cpu")
 
 
-def load_stage_weights(ctx: NodeContext, part: int, ranges, full_sd=None):
+def load_stage_weights(ctx: NodeContext, part: int, ranges, full_sd=None, device=None):
     """Per-stage weights; prints the reference's load messages (``node.py:294-317``)."""
     pipe = ctx.pipeline
     a, b = ranges[part]
     first, last = part == 0, part == pipe.num_parts - 1
     if ckpt.is_synthetic(pipe.model_weights):
         log(f"[{ctx.node_id}] Using synthetic random-init weights (seed {ckpt.synthetic_seed(pipe.model_weights)})")
-        return ckpt.random_stage_state_dict(pipe.model, a, b, first, last, ckpt.synthetic_seed(pipe.model_weights)), full_sd
+        gen_dev = device if (device is not None and device.type == "cuda" and model_info(pipe.model).family != "cifar") else None
+        return ckpt.random_stage_state_dict(pipe.model, a, b, first, last, ckpt.synthetic_seed(pipe.model_weights),
+                                            device=gen_dev), full_sd
     if full_sd is None:
         log(f"[{ctx.node_id}] Loading full state dict...")
         full_sd = ckpt.load_full_state_dict(pipe.model_weights)
@@ -129,7 +133,7 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
     pipe = ctx.pipeline
     a, b = ranges[part]
     first, last = part == 0, part == pipe.num_parts - 1
-    sd, full_sd = load_stage_weights(ctx, part, ranges, full_sd)
+    sd, full_sd = load_stage_weights(ctx, part, ranges, full_sd, device)
     fam = model_info(pipe.model).family
     if device.type == "cuda":
         if fam == "cifar":
@@ -167,7 +171,9 @@ async def run_grpc(ctx: NodeContext, args, stage) -> int:
     nid = ctx.node_id
     fam = model_info(ctx.pipeline.model).family
     fwd = _forward_fn(stage, fam)
-    servicer = NodeServicer(nid, fwd, ctx.is_last, ctx.next_address)
+    servicer = NodeServicer(nid, fwd, ctx.is_last, ctx.next_address, rpc_timeout_s=ctx.pipeline.rpc_timeout_s,
+                            stage=ctx.part_index)
+    args._servicer = servicer
     listen = f"[::]:{ctx.port}"
     try:
         server = await start_server(servicer, ctx.port)
@@ -217,7 +223,7 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
     # readiness barrier over every downstream stage (replaces the reference's sleep(2))
     for n in ctx.pipeline.stages[1:]:
         c = client if n.address == ctx.next_address else NodeClient(n.address)
-        ok = await c.wait_ready(120.0)
+        ok = await c.wait_ready(ctx.pipeline.health_timeout_s)
         if c is not client:
             await c.close()
         if not ok:
@@ -301,7 +307,7 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     if backend == "gloo":
         device = torch.device("cpu")
     s0 = pipe.stage(0)
-    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host,
+    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host, timeout_s=pipe.comm_timeout_s,
                      master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
     ranges = stage_ranges(ctx)
     stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device)
@@ -367,10 +373,23 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     return rc
 
 
+def _finish(args) -> None:
+    from .utils import trace
+    sv = getattr(args, "_servicer", None)
+    if sv is not None and args.metrics:
+        sv.metrics.emit(force=True)
+    p = trace.flush()
+    if p:
+        log(f"[{args.node_id}] trace written to {p}")
+
+
 def main(argv=None) -> int:
     log("Script started...")
     args = build_parser().parse_args(argv)
     set_quiet(args.quiet)
+    if args.trace:
+        from .utils import trace
+        trace.enable(args.trace)
     nid = args.node_id
     log(f"Parsed Node ID: {nid}")
     try:
@@ -403,3 +422,4 @@ def main(argv=None) -> int:
         return 0
     finally:
         log(f"[{nid}] Event loop closed. Exiting.")
+        _finish(args)

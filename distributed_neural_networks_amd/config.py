@@ -65,6 +65,9 @@ class PipelineConfig:
     seq_len: int = 64
     prompt_len: Optional[int] = None
     decode_steps: int = 0
+    rpc_timeout_s: Optional[float] = None     # per-hop SendTensor deadline (reference: none)
+    health_timeout_s: float = 120.0           # readiness barrier before stage 0 sends
+    comm_timeout_s: float = 300.0             # process-group (RCCL/gloo) watchdog timeout
     raw: Dict[str, Any] = field(default_factory=dict)
 
     def stage(self, part_index: int) -> NodeSpec:
@@ -157,7 +160,9 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"),
         transport=transport, micro_batch_size=int(cfg.get("micro_batch_size", 1)),
         num_microbatches=int(cfg.get("num_microbatches", 1)), seq_len=int(cfg.get("seq_len", 64)),
-        prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)), raw=cfg)
+        prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),
+        rpc_timeout_s=cfg.get("rpc_timeout_s"), health_timeout_s=float(cfg.get("health_timeout_s", 120.0)),
+        comm_timeout_s=float(cfg.get("comm_timeout_s", 300.0)), raw=cfg)
 
 
 def resolve_node(cfg: Dict[str, Any], node_id: str, path: str = "<config>") -> NodeContext:

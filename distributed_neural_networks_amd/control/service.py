@@ -21,7 +21,9 @@ reference servicer (``node.py:34-133``), all deliberate:
 from __future__ import annotations
 
 import asyncio
+import os
 import threading
+import time
 import traceback
 from typing import Callable, Optional
 
@@ -29,7 +31,9 @@ import grpc
 import numpy as np
 import torch
 
+from ..utils import trace
 from ..utils.log import log
+from ..utils.metrics import StageMetrics
 from ..wire import codec, proto
 
 UNLIMITED = [("grpc.max_send_message_length", -1), ("grpc.max_receive_message_length", -1)]
@@ -49,7 +53,10 @@ class NodeServicer:
     """
 
     def __init__(self, node_id: str, forward: Optional[Callable], is_last: bool,
-                 next_address: Optional[str] = None, wire_dtype: Optional[torch.dtype] = torch.float32):
+                 next_address: Optional[str] = None, wire_dtype: Optional[torch.dtype] = torch.float32,
+                 rpc_timeout_s: Optional[float] = None, stage: int = -1):
+        self.rpc_timeout_s = rpc_timeout_s
+        self.metrics = StageMetrics(node_id, stage)
         self.node_id = node_id
         self.forward = forward
         self.is_last = is_last
@@ -75,11 +82,13 @@ class NodeServicer:
         result = None
         status = f"[{nid}] Error processing tensor."
         try:
+            t0 = time.perf_counter()
             x = codec.decode(request.tensor)
             log(f"[{nid}] Deserialized input tensor shape: {x.shape}")
             loop = asyncio.get_running_loop()
-            with self._lock:
+            with self._lock, trace.span("SendTensor.forward", "compute", request=request.request_id):
                 out, pred = await loop.run_in_executor(None, self.forward, x)
+            self.metrics.record(time.perf_counter() - t0, int(x.shape[0]) if x.dim() else 1)
             out = out.detach().to("cpu")
             if self.wire_dtype is not None and out.is_floating_point():
                 out = out.to(self.wire_dtype)
@@ -96,7 +105,7 @@ class NodeServicer:
                 log(f"[{nid}] Forwarding tensor to next node: {self.next_address}")
                 nreq = proto.TensorRequest(request_id=request.request_id, tensor=codec.encode(out))
                 try:
-                    resp = await self._next_call()(nreq)
+                    resp = await self._next_call()(nreq, timeout=self.rpc_timeout_s)
                     log(f"[{nid}] Response from next node ({self.next_address}): {resp.status}")
                     status = f"[{nid}] Forwarded. Next node status: {resp.status}"
                     if resp.HasField("result_tensor"):

@@ -39,9 +39,21 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+DEBUG_SYNC = bool(os.environ.get("DNN_DEBUG_SYNC"))
+
+
 def check(rc: int, what: str) -> None:
+    """Raise on a rejected/failed launch.  With ``DNN_DEBUG_SYNC=1`` every kernel
+    is followed by a device sync so an asynchronous fault (bad address, hang)
+    is attributed to the launch that caused it (race/fault triage mode; the
+    GPU-side sanitizer is not available on this pool)."""
     if rc != 0:
         raise RuntimeError(f"{what}: HIP launch failed with code {rc}")
+    if DEBUG_SYNC:
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError(f"{what}: device fault after launch: {e}") from e
 
 
 def ptr(t) -> int:

@@ -21,6 +21,7 @@ from typing import Callable, List, Optional, Sequence
 import torch
 
 from ..parallel.links import P2PLink
+from ..utils import trace
 from .graph import GraphedStep
 from .stages import StageCompute, StageOutput
 
@@ -50,9 +51,10 @@ class ColocatedPipeline:
     def __call__(self, x: Optional[torch.Tensor] = None) -> StageOutput:
         if x is not None:
             self.x.copy_(x, non_blocking=True)
-        if self._graph is not None:
-            return self._graph()
-        return self._step()
+        with trace.span("pipeline_step", "compute", device=self.x.device, batch=self.batch):
+            if self._graph is not None:
+                return self._graph()
+            return self._step()
 
 
 def run_stage_stream(stage: StageCompute, M: int, batch: int, prev: Optional[P2PLink], nxt: Optional[P2PLink],
@@ -75,12 +77,15 @@ def run_stage_stream(stage: StageCompute, M: int, batch: int, prev: Optional[P2P
         if prev is None:
             x = source(i)
         else:
-            rwork[k].wait()
+            with trace.span("recv_wait", "p2p", mb=i):
+                rwork[k].wait()
             x = in_slots[k]
         if swork[k] is not None:
-            swork[k].wait()
+            with trace.span("slot_reuse_wait", "p2p", mb=i):
+                swork[k].wait()
             swork[k] = None
-        y = stage.forward(x, out_slots[k])
+        with trace.span("stage_forward", "compute", device=dev, mb=i):
+            y = stage.forward(x, out_slots[k])
         if prev is not None and i + depth < M:
             rwork[k] = prev.irecv(in_slots[k])  # ordered after this slot's compute (see module doc)
         if nxt is not None:
