@@ -37,6 +37,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("cifar_stage0_v2", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
     return dnn_cifar_stage0_v2(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
   });
+  m.def("cifar_stage0_v3", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
+    return dnn_cifar_stage0_v3(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
+  });
+  m.def("cifar_stage0_v3_stamps", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 stamps,
+                                     u64 st) {
+    return dnn_cifar_stage0_v3_stamps(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid,
+                                      reinterpret_cast<unsigned long long*>(static_cast<uintptr_t>(stamps)), ST(st));
+  });
   m.def("cifar_head_tail", [](u64 hid, u64 w2p, u64 b2, u64 probs, u64 pred, int B, u64 st) {
     return dnn_cifar_head_tail(CP(hid), CP(w2p), CFP(b2), FP(probs), IP(pred), B, ST(st));
   });

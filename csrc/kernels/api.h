@@ -11,6 +11,10 @@ int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1
                      int B, int grid, hipStream_t st);
 int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
+int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
+                        int B, int grid, hipStream_t st);
+int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                               const float* b2, int B, int grid, unsigned long long* stamps, hipStream_t st);
 int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
                         hipStream_t st);
 int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N, float eps,

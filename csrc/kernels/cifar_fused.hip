@@ -247,6 +247,64 @@ constexpr int V2_OB_OFF = V2_A1_OFF + V2_A1_BYTES;            // 45440
 constexpr int V2_OBP = 136;                                   // obuf channel pitch (bytes)
 constexpr int V2_LDS = V2_OB_OFF + 64 * V2_OBP;               // 54144
 
+// conv2 main loop for one wave: 4 M-tiles (mt0..mt0+3) x 18 k-steps of 16.
+// A fragments are software-pipelined one k-step ahead in registers and the
+// issue order is pinned (4 ds_read_b128 of step s+1, then the 4 MFMAs of step
+// s), so each MFMA's operand read is ~4 MFMAs (~128 cycles) old — enough to
+// cover the LDS latency that hipcc's own schedule (read 1 ahead) exposed.
+//
+// hipcc keeps scheduling each operand read one MFMA ahead whatever the source
+// order, so the reads are inline-asm ds_read_b128 (immediate offsets from one
+// base VGPR) issued a whole k-step ahead, with counted lgkmcnt waits fenced by
+// sched_barrier so no MFMA is hoisted above its wait (cdna_hip_programming.md
+// §5.7 form iii, rule 18). The caller must have no other LDS op in flight.
+template <int S, int I>
+__device__ __forceinline__ constexpr int c2_off() {
+  return ((4 * (I >> 1) + (S >> 1) / 3) * 24 + 8 * (I & 1) + (S >> 1) % 3) * 80 + (S & 1) * 32;
+}
+
+template <int S>
+__device__ __forceinline__ void c2_issue(uint32_t base, bf16x8 (&a)[4]) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[0]) : "v"(base), "i"(c2_off<S, 0>()));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[1]) : "v"(base), "i"(c2_off<S, 1>()));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[2]) : "v"(base), "i"(c2_off<S, 2>()));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[3]) : "v"(base), "i"(c2_off<S, 3>()));
+}
+
+template <int S>
+__device__ __forceinline__ void c2_step(uint32_t base, const bf16x8 (&w2f)[18], f32x16 (&acc)[4], bf16x8 (&cur)[4],
+                                        bf16x8 (&nxt)[4]) {
+  if constexpr (S + 1 < 18) {
+    c2_issue<S + 1>(base, nxt);
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // step S's 4 reads have landed
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[i], w2f[S], acc[i], 0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);  // keep step S+1's issue/wait below these MFMAs
+  if constexpr (S + 1 < 18) c2_step<S + 1>(base, w2f, acc, nxt, cur);
+}
+
+__device__ __forceinline__ void conv2_mainloop(const char* a1lane, const bf16x8 (&w2f)[18], f32x16 (&acc)[4],
+                                               int mt0) {
+  // M tiles mt0..mt0+3 = tile rows ty2 = mt0/2 + (i>>1): fold mt0 into the base address
+  const uint32_t base = (uint32_t)(uintptr_t)(a1lane + (mt0 >> 1) * 4 * 24 * 80);
+  bf16x8 a0[4], a1[4];
+  c2_issue<0>(base, a0);
+  c2_step<0>(base, w2f, acc, a0, a1);
+}
+
+// Force the loads of loop-invariant registers to complete at this point (an
+// empty asm that reads them makes hipcc place their s_waitcnt here).
+template <int N>
+__device__ __forceinline__ void resident_fence(const bf16x8 (&w)[N], float b) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(w[i]));
+  asm volatile("" ::"v"(b));
+}
+
 __device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
 
@@ -270,6 +328,8 @@ __global__ __launch_bounds__(256, 2) void cifar_stage0_v2_kernel(
 #pragma unroll
   for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
   const float bias2 = b2[oc2];
+  resident_fence(w1f, bias1);
+  resident_fence(w2f, bias2);
 
   // input prefetch: thread owns pixels p = tid + 256*i (i < 4), 3 channels each
   float pf[4][3];
@@ -351,17 +411,7 @@ __global__ __launch_bounds__(256, 2) void cifar_stage0_v2_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
       const int mt0 = (wave >> 1) * 4;
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const int kk = s >> 1, ky = kk / 3, kx = kk % 3;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
-          const int off = ((4 * ty2 + ky) * V2_A1W + 8 * tx2 + kx) * V2_A1P + (s & 1) * 32;
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + c2_lane + off);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2f[s], acc[i], 0, 0, 0);
-        }
-      }
+      conv2_mainloop(smem + c2_lane, w2f, acc, mt0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
@@ -394,9 +444,242 @@ __global__ __launch_bounds__(256, 2) void cifar_stage0_v2_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stage 0, v3: wave-specialised software pipeline (512 threads, 1 WG per CU).
+// Waves 0-3 ("P") stage the input and run conv1 for image k+1 while waves 4-7
+// ("C") run conv2 for image k, so every SIMD hosts one VALU/LDS-heavy wave and
+// one MFMA-heavy wave at the same time (separate pipes; MI355X_MICROARCH
+// "Execution model"). act1 and the output staging image are double-buffered;
+// two workgroup barriers per image. Same LDS layouts and lane maps as v2.
+//   iteration it:  A) P: input(it) regs -> xin         C: obuf[it-2] -> global
+//                  B) P: conv1(it) -> act1[it&1]       C: conv2(it-1) -> obuf[(it-1)&1]
+// ---------------------------------------------------------------------------
+constexpr int V3_A1_OFF = V2_XIN_BYTES;                                  // 10880
+constexpr int V3_OB_OFF = V3_A1_OFF + 2 * V2_A1_BYTES;                   // 80000
+constexpr int V3_OB_BYTES = 64 * V2_OBP;                                 // 8704
+constexpr int V3_LDS = V3_OB_OFF + 2 * V3_OB_BYTES;                      // 97408
+#ifndef DNN_V3_PT
+#define DNN_V3_PT 24
+#endif
+constexpr int V3_PT = DNN_V3_PT;  // conv1 tiles run by producer waves; the rest by consumers (balance, stamps)
+
+template <bool STAMPS>
+__global__ __launch_bounds__(512, 1) void cifar_stage0_v3_kernel(
+    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
+    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B,
+    unsigned long long* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) char smem[V3_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // diagnostic: cycles in [phase A, barrier 1, phase B, barrier 2] for wave 0 (P) and wave 4 (C)
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = 0;
+  auto stamp = [&](int slot) {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      if (slot >= 0) st_acc[slot] += t - st_t;
+      st_t = t;
+    }
+  };
+  const bool producer = wave < 4;
+  const int rw = wave & 3;            // wave index within its role
+  const int rt = tid & 255;           // thread index within its role
+  const int h = lane >> 5, r32 = lane & 31;
+  const int n = B > (int)blockIdx.x ? (B - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+
+  for (int i = tid; i < V3_OB_OFF / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+
+  // resident weights: every wave runs conv1 tiles (conv1 weights, 12 VGPRs);
+  // consumer waves also hold their conv2 N-tile (72 VGPRs)
+  bf16x8 w1f[3];
+  bf16x8 w2f[18];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 48 + s * 16 + h * 8);
+  const float bias1 = b1[r32];
+  float bias = 0.f;
+  int oc2 = 0;
+  if (!producer) {
+    oc2 = (rw & 1) * 32 + r32;
+#pragma unroll
+    for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
+    bias = b2[oc2];
+  }
+  // Retire the weight loads here, once: otherwise hipcc's waitcnt pass waits
+  // for them at their first use inside the loop with vmcnt(0), which also
+  // drains the in-flight input prefetch (HBM latency on every conv1 tile).
+  resident_fence(w1f, bias1);
+  if (!producer) resident_fence(w2f, bias);
+  float pf[4][3];
+  auto load_img = [&](int k) {
+    const float* xb = x + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 3072;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pf[i][c] = xb[c * 1024 + rt + 256 * i];
+  };
+  if (producer && n > 0) load_img(0);
+  __syncthreads();
+
+  const int c1_lane = ((r32 >> 3) * V2_XW + (r32 & 7) + 2 * h) * 8;
+  const int c2_lane = ((r32 >> 3) * V2_A1W + (r32 & 7)) * V2_A1P + h * 16;
+  const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
+  const int cb = r32 & ~3;
+
+  // one conv1 output tile (4x8 pixels x 32 channels) -> pooled 2x4 x 32 in act1 `a1`
+  auto conv1_tile = [&](int t, char* a1) {
+    const int ty = t >> 2, tx = t & 3;
+    const char* abase = smem + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
+    }
+    float v[4];
+#pragma unroll
+    for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+      for (int qx = 0; qx < 2; ++qx) {
+        const int g0 = (2 * qy) * 4 + 2 * qx;
+        v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
+      }
+    const bool odd = r32 & 1;
+    const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
+    const float r0 = __int_as_float(dpp_xor1(s0)), r1 = __int_as_float(dpp_xor1(s1));
+    uint32_t u0, u1;
+    if (!odd) { u0 = pack2bf(v[0], r0); u1 = pack2bf(v[1], r1); }
+    else { u0 = pack2bf(r0, v[2]); u1 = pack2bf(r1, v[3]); }
+    const bool hi2 = r32 & 2;
+    const uint32_t rcv = (uint32_t)dpp_xor2((int)(hi2 ? u0 : u1));
+    const uint32_t mine = hi2 ? u1 : u0;
+    uint2 w;
+    w.x = hi2 ? rcv : mine;
+    w.y = hi2 ? mine : rcv;
+    const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
+    *reinterpret_cast<uint2*>(a1 + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
+  };
+
+  for (int it = 0; it <= n; ++it) {
+    stamp(-1);
+    // ---------------- phase A ----------------
+    if (producer) {
+      if (it < n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = rt + 256 * i, yy = p >> 5, xx = p & 31;
+          uint2 v;
+          v.x = pack2bf(pf[i][0], pf[i][1]);
+          v.y = pack2bf(pf[i][2], 0.f);
+          *reinterpret_cast<uint2*>(smem + ((yy + 1) * V2_XW + xx + 1) * 8) = v;
+        }
+      }
+    } else if (it >= 2) {
+      const int k = it - 2;
+      int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
+      const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = rt + 256 * u, ch = e >> 3, j = e & 7;
+        const uint2 a = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16);
+        const uint2 b = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16 + 8);
+        dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
+      }
+    }
+    stamp(0);
+    __syncthreads();
+    stamp(1);
+    // ---------------- phase B ----------------
+    if (producer) {
+      if (it < n) {
+        // xin already holds image `it`: the prefetch registers are free, so the
+        // next image's HBM latency hides under conv1 (not in phase A).
+        if (it + 1 < n) load_img(it + 1);
+        char* a1 = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
+#pragma unroll 2
+        for (int t = rw; t < V3_PT; t += 4) conv1_tile(t, a1);
+      }
+    } else if (it >= 1) {
+      const int k = it - 1;
+      const char* a1 = smem + V3_A1_OFF + (k & 1) * V2_A1_BYTES + c2_lane;
+      char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
+      f32x16 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
+      const int mt0 = (rw >> 1) * 4;
+      conv2_mainloop(a1, w2f, acc, mt0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+#pragma unroll
+        for (int qy = 0; qy < 2; ++qy) {
+          float pv[2];
+#pragma unroll
+          for (int qx = 0; qx < 2; ++qx) {
+            const int g0 = (2 * qy) * 4 + 2 * qx;
+            pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
+          }
+          const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;
+          *reinterpret_cast<uint32_t*>(ob + oc2 * V2_OBP + (PY * 8 + PX) * 2) = pack2bf(pv[0], pv[1]);
+        }
+      }
+    }
+    if (!producer && it < n) {  // consumers take the last conv1 tiles of image `it` (load balance)
+      char* a1w = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
+      for (int t = V3_PT + rw; t < 32; t += 4) conv1_tile(t, a1w);
+    }
+    stamp(2);
+    __syncthreads();
+    stamp(3);
+  }
+  // drain: the last image's output staging
+  if (!producer && n >= 1) {
+    const int k = n - 1;
+    int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
+    const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = rt + 256 * u, ch = e >> 3, j = e & 7;
+      const uint2 a = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16);
+      const uint2 b = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16 + 8);
+      dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
+    }
+  }
+  if constexpr (STAMPS) {
+    if ((wave == 0 || wave == 4) && lane == 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) stamps[(blockIdx.x * 2 + (wave >> 2)) * 4 + s] = st_acc[s];
+    }
+  }
+}
+
 }  // namespace dnn
 
 using namespace dnn;
+
+extern "C" int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                                   const float* b2, int B, int grid, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (grid <= 0) grid = 256;
+  if (grid > B) grid = B;
+  hipLaunchKernelGGL((cifar_stage0_v3_kernel<false>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
+                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, nullptr);
+  return (int)hipGetLastError();
+}
+
+// Diagnostic build: per-WG [P, C] x [phaseA, barrier1, phaseB, barrier2] cycle sums (s_memtime).
+extern "C" int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                                          const float* b2, int B, int grid, unsigned long long* stamps, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (grid <= 0) grid = 256;
+  if (grid > B) grid = B;
+  hipLaunchKernelGGL((cifar_stage0_v3_kernel<true>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
+                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, stamps);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
                                    const float* b2, int B, int grid, hipStream_t st) {

@@ -25,6 +25,8 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 LIB_PATH = os.path.join(PKG, "_dnn_hip" + EXT_SUFFIX)
 
 TRANSFORMER_SRCS = ("norm_embed.hip", "attention.hip", "sampler.hip", "gemm_fp8.hip")
+# ReLU/max-pool epilogues: no NaN-canonicalising v_max before every fmaxf of an MFMA result
+PER_FILE_FLAGS = {"cifar_fused.hip": ["-ffast-math"]}
 
 
 def _hipcc() -> str:
@@ -41,6 +43,7 @@ def sources() -> List[str]:
 def _flags(src: str) -> List[str]:
     f = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + CSRC, "-Wno-unused-result",
          "-Wno-unused-command-line-argument"]
+    f += PER_FILE_FLAGS.get(os.path.basename(src), [])
     have_tf = all(os.path.exists(os.path.join(CSRC, "kernels", s)) for s in TRANSFORMER_SRCS)
     if have_tf:
         f.append("-DDNN_HAVE_TRANSFORMER")

@@ -32,7 +32,7 @@ class CifarStage0Weights:
     w1p2: torch.Tensor = None  # v2: [32][48], k = ky*16 + kx*4 + c (kx<3, c<3 real)
 
 
-STAGE0_VARIANT = 2
+STAGE0_VARIANT = 3
 
 
 @dataclass
@@ -78,7 +78,11 @@ def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.T
         out = torch.empty((B, 4096), dtype=torch.bfloat16, device=x.device)
     if tuple(out.shape) != (B, 4096) or out.dtype != torch.bfloat16 or not out.is_contiguous():
         raise ValueError("stage0: bad output buffer")
-    if (variant or STAGE0_VARIANT) == 2:
+    v = variant or STAGE0_VARIANT
+    if v == 3:
+        check(lib().cifar_stage0_v3(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
+                                    stream_ptr()), "cifar_stage0_v3")
+    elif v == 2:
         check(lib().cifar_stage0_v2(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
                                     stream_ptr()), "cifar_stage0_v2")
     else:

@@ -1,0 +1,2 @@
+export PYTHONPATH=$PWD
+timeout -k 10 120 python bench/cifar_stamps.py 65536 2>&1 | grep -v amdgpu.ids
