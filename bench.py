@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
+    ap.add_argument("--cut", default="auto", choices=["auto", "1", "2"],
+                    help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = cost model")
     return ap.parse_args()
 
 
@@ -66,15 +68,25 @@ def dist_setup(n, cpu=False):
     return info
 
 
-def stages_for(device):
+def stages_for(device, cut: int = 1):
+    """The two pipeline stages: units [0..cut] and [cut+1..3] (cut 1 = the reference's conv|fc split)."""
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import CifarHipStage, TorchStage
-    sd0 = ckpt.random_stage_state_dict("cifar10", 0, 1, True, False, 0)
-    sd1 = ckpt.random_stage_state_dict("cifar10", 2, 3, False, True, 0)
+    sd0 = ckpt.random_stage_state_dict("cifar10", 0, cut, True, False, 0)
+    sd1 = ckpt.random_stage_state_dict("cifar10", cut + 1, 3, False, True, 0)
     if device.type == "cpu":  # schedule-test mode only (never used for a reported number)
-        return (TorchStage("cifar10", sd0, 0, 1, True, False, device),
-                TorchStage("cifar10", sd1, 2, 3, False, True, device))
-    return CifarHipStage(sd0, 0, 1, device), CifarHipStage(sd1, 2, 3, device)
+        return (TorchStage("cifar10", sd0, 0, cut, True, False, device),
+                TorchStage("cifar10", sd1, cut + 1, 3, False, True, device))
+    return CifarHipStage(sd0, 0, cut, device), CifarHipStage(sd1, cut + 1, 3, device)
+
+
+def pick_cut(args, info) -> int:
+    from distributed_neural_networks_amd.parallel.partition import cifar_cut
+    if args.cut != "auto":
+        return int(args.cut)
+    if info.world == 1:
+        return 1  # colocated: no hop; keep the reference split
+    return cifar_cut(args.placement, info.world)
 
 
 def dsync(dev):
@@ -134,7 +146,7 @@ def bench_colocated(args, info):
 def bench_interleaved(args, info):
     import torch.distributed as dist
     dev, N, r = info.device, info.world, info.rank
-    s0, s1 = stages_for(dev)
+    s0, s1 = stages_for(dev, args._cut)
     M = max(1, args.microbatches)
     mb = args.batch // M
     per_peer = mb // (N - 1)
@@ -142,8 +154,9 @@ def bench_interleaved(args, info):
     g = torch.Generator(device=dev).manual_seed(1 + r)
     xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
     bdt = s0.out_spec(1)[1]
-    y0 = [torch.empty((mb, 4096), dtype=bdt, device=dev) for _ in range(M)]
-    rx = [torch.empty((mb, 4096), dtype=bdt, device=dev) for _ in range(M)]
+    bw = s0.out_spec(1)[0][1]  # boundary width: 4096 (cut 1) or 512 (cut 2)
+    y0 = [torch.empty((mb, bw), dtype=bdt, device=dev) for _ in range(M)]
+    rx = [torch.empty((mb, bw), dtype=bdt, device=dev) for _ in range(M)]
     probs = [torch.empty((mb, 10), device=dev) for _ in range(M)]
     splits = [0 if p == r else per_peer for p in range(N)]
 
@@ -166,7 +179,7 @@ def bench_interleaved(args, info):
     t1 = sync_time(info)
     # latency: one image per peer through stage0 -> all-to-all -> stage1
     lx = torch.randn((N - 1, 3, 32, 32), device=dev, generator=g)
-    ly = torch.empty((N - 1, 4096), dtype=bdt, device=dev)
+    ly = torch.empty((N - 1, bw), dtype=bdt, device=dev)
     lr = torch.empty_like(ly)
     lp = torch.empty((N - 1, 10), device=dev)
     one = [0 if p == r else 1 for p in range(N)]
@@ -188,7 +201,7 @@ def bench_linear(args, info):
     dev, N, r = info.device, info.world, info.rank
     if N % 2:
         raise SystemExit("linear placement needs an even number of GPUs")
-    s0, s1 = stages_for(dev)
+    s0, s1 = stages_for(dev, args._cut)
     stage_idx = r % 2
     st = s0 if stage_idx == 0 else s1
     M = max(1, args.microbatches)
@@ -218,6 +231,7 @@ def main():
         return gpt_bench.main(args)
     info = dist_setup(args.gpus, args.cpu)
     N = info.world
+    args._cut = pick_cut(args, info)
     if N == 1:
         el, imgs_per_gpu, p50, par = bench_colocated(args, info)
     elif args.placement == "interleaved":
@@ -236,7 +250,9 @@ def main():
             "p50_latency_ms": None if p50 != p50 else round(p50, 4),
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": imgs_per_gpu * N, "seq_len": None, "parallelism": par,
-                       "stages": 2, "microbatches": args.microbatches if N > 1 else 1},
+                       "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
+                       "stage_cut": {1: "conv|fc (reference split, 8 KiB/img hop)",
+                                     2: "conv+fc1|fc2 (1 KiB/img hop)"}[args._cut]},
         }
         print(json.dumps(out), flush=True)
     if N > 1:

@@ -58,14 +58,37 @@ def pack_stage0(sd: Dict[str, torch.Tensor], device) -> CifarStage0Weights:
         w1p2=w1p2.reshape(32, 48).to(device=device, dtype=torch.bfloat16).contiguous())
 
 
-def pack_head(sd: Dict[str, torch.Tensor], device) -> CifarHeadWeights:
-    w2 = torch.zeros(16, 512)
-    w2[:10] = sd["fc2.weight"].float()
-    return CifarHeadWeights(
-        w_fc1=sd["fc1.weight"].to(device=device, dtype=torch.bfloat16).contiguous(),
-        b_fc1=sd["fc1.bias"].float().to(device).contiguous(),
-        w_fc2p=w2.to(device=device, dtype=torch.bfloat16).contiguous(),
-        b_fc2=sd["fc2.bias"].float().to(device).contiguous())
+def pack_head(sd: Dict[str, torch.Tensor], device, fc1: bool = True, fc2: bool = True) -> CifarHeadWeights:
+    w_fc1 = b_fc1 = w2p = b_fc2 = None
+    if fc1:
+        w_fc1 = sd["fc1.weight"].to(device=device, dtype=torch.bfloat16).contiguous()
+        b_fc1 = sd["fc1.bias"].float().to(device).contiguous()
+    if fc2:
+        w2 = torch.zeros(16, 512)
+        w2[:10] = sd["fc2.weight"].float()
+        w2p = w2.to(device=device, dtype=torch.bfloat16).contiguous()
+        b_fc2 = sd["fc2.bias"].float().to(device).contiguous()
+    return CifarHeadWeights(w_fc1=w_fc1, b_fc1=b_fc1, w_fc2p=w2p, b_fc2=b_fc2)
+
+
+def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Unit 2: (B,4096) bf16 -> relu(fc1) (B,512) bf16 on the MFMA GEMM."""
+    if h.dtype != torch.bfloat16 or tuple(h.shape[1:]) != (4096,):
+        raise ValueError(f"fc1: expected bf16 (B,4096), got {h.dtype} {tuple(h.shape)}")
+    return linear(h, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
+
+
+def head_tail(hid: torch.Tensor, w: CifarHeadWeights, probs: Optional[torch.Tensor] = None,
+              pred: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Unit 3: (B,512) bf16 -> fc2 + softmax (B,10) fp32 + per-row argmax (B,) int32."""
+    if hid.dtype != torch.bfloat16 or tuple(hid.shape[1:]) != (512,) or not hid.is_contiguous():
+        raise ValueError(f"head_tail: expected contiguous bf16 (B,512), got {hid.dtype} {tuple(hid.shape)}")
+    B = hid.shape[0]
+    probs = probs if probs is not None else torch.empty((B, 10), dtype=torch.float32, device=hid.device)
+    pred = pred if pred is not None else torch.empty((B,), dtype=torch.int32, device=hid.device)
+    check(lib().cifar_head_tail(ptr(hid), ptr(w.w_fc2p), ptr(w.b_fc2), ptr(probs), ptr(pred), B, stream_ptr()),
+          "cifar_head_tail")
+    return probs, pred
 
 
 def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.Tensor] = None,

@@ -77,6 +77,45 @@ def validate_ranges(ranges: Sequence[Range], num_layers: int) -> None:
         raise ValueError(f"layer ranges {list(ranges)} do not cover 0..{num_layers - 1}")
 
 
+def choose_cut(unit_ns: Sequence[float], boundary_bytes: Sequence[int], cuts: Sequence[int], placement: str,
+               world: int, link_gbs: float) -> int:
+    """Pick the 2-stage cut (stage 0 = units [0..c], stage 1 = [c+1..]) that
+    minimises the per-item pipeline period under a compute + link cost model.
+
+    * ``linear`` (one stage per GPU): period = max(t_stage0, t_stage1, hop)
+      with the hop on ONE xGMI link;
+    * ``interleaved`` (every GPU hosts stage 0 of one pipeline and stage 1 of
+      the others, hop = all-to-all): compute is balanced by construction and
+      the hop is spread over the ``world-1`` links of the fully connected
+      board, overlapped with compute: period = max(sum(t), hop / (world-1)).
+    ``unit_ns`` = per-item compute of each unit; ``boundary_bytes[c]`` = bytes
+    per item crossing a cut after unit c; ``link_gbs`` = usable GB/s per link.
+    """
+    best, best_t = None, float("inf")
+    for c in cuts:
+        t0, t1 = sum(unit_ns[:c + 1]), sum(unit_ns[c + 1:])
+        hop = boundary_bytes[c] / link_gbs  # bytes / (GB/s) = ns
+        if placement == "linear":
+            t = max(t0, t1, hop)
+        else:
+            t = max(t0 + t1, hop / max(1, world - 1))
+        if t < best_t - 1e-9:
+            best, best_t = c, t
+    return best
+
+
+# Measured on 1x MI355X (profiles/r1_*): per-image ns of the CIFAR units with the
+# fused kernels (conv stage = units 0-1 together) and bf16 boundary sizes.
+CIFAR_UNIT_NS = (0.0, 10.8, 5.3, 0.3)
+CIFAR_BOUNDARY_BYTES = (32 * 16 * 16 * 2, 4096 * 2, 512 * 2, 10 * 4)
+XGMI_LINK_GBS = 50.0  # conservative usable P2P GB/s per direction per link (7 links x ~153 GB/s aggregate spec)
+
+
+def cifar_cut(placement: str, world: int, link_gbs: float = XGMI_LINK_GBS) -> int:
+    """Cut for the CIFAR 2-stage pipeline on MI355X: 1 (reference conv|fc) or 2 (after fc1)."""
+    return choose_cut(CIFAR_UNIT_NS, CIFAR_BOUNDARY_BYTES, (1, 2), placement, world, link_gbs)
+
+
 def resolve_ranges(num_layers: int, num_stages: int, given: Sequence[Optional[Range]],
                    first_extra: float = 0.0, last_extra: float = 0.0) -> List[Range]:
     """Use per-node ``layers`` if every node gives one, else compute a balanced split."""

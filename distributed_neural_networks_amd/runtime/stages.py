@@ -48,10 +48,17 @@ class StageCompute:
 
 
 class CifarHipStage(StageCompute):
-    """CIFAR units [start, end] on the fused HIP kernels. Supported splits:
-    (0,1) = reference part 0, (2,3) = reference part 1, (0,3) = whole model."""
+    """CIFAR units [start, end] on the fused HIP kernels.
 
-    SUPPORTED = {(0, 1), (2, 3), (0, 3)}
+    Units 0-1 always run together (the fused conv1/pool/conv2/pool kernel), so
+    the supported ranges are (0,1) = reference part 0, (2,3) = reference part 1,
+    (0,3) = whole model, and the fc1 cut (0,2) | (3,3) whose stage boundary is
+    the 512-wide hidden (1 KiB/img in bf16 instead of 8 KiB: what the
+    multi-GPU placement uses to cut xGMI traffic 8x, parallel/partition.py
+    ``cifar_cut``)."""
+
+    SUPPORTED = {(0, 1), (2, 3), (0, 3), (0, 2), (3, 3)}
+    _BOUNDARY = {1: (cifar.FLAT_DIM, torch.bfloat16), 2: (512, torch.bfloat16)}
 
     def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device):
         from ..ops import cifar as cops
@@ -61,21 +68,27 @@ class CifarHipStage(StageCompute):
         self.first, self.last = start == 0, end == cifar.NUM_UNITS - 1
         self._cops = cops
         self.w0 = cops.pack_stage0(sd, self.device) if start == 0 else None
-        self.wh = cops.pack_head(sd, self.device) if end == 3 else None
+        self.wh = cops.pack_head(sd, self.device, fc1=start <= 2 <= end, fc2=end == 3)
         self._scratch: Dict[int, Dict[str, torch.Tensor]] = {}
 
     def in_spec(self, batch):
-        return ((batch, 3, 32, 32), torch.float32) if self.first else ((batch, cifar.FLAT_DIM), torch.bfloat16)
+        if self.first:
+            return (batch, 3, 32, 32), torch.float32
+        w, dt = self._BOUNDARY[self.start - 1]
+        return (batch, w), dt
 
     def out_spec(self, batch):
-        return ((batch, 10), torch.float32) if self.last else ((batch, cifar.FLAT_DIM), torch.bfloat16)
+        if self.last:
+            return (batch, 10), torch.float32
+        w, dt = self._BOUNDARY[self.end]
+        return (batch, w), dt
 
     def _buf(self, batch):
         b = self._scratch.get(batch)
         if b is None:
             d = self.device
             b = {}
-            if self.first and self.last:
+            if self.first and self.end >= 2:
                 b["mid"] = torch.empty((batch, 4096), dtype=torch.bfloat16, device=d)
             if self.last:
                 b["hid"] = torch.empty((batch, 512), dtype=torch.bfloat16, device=d)
@@ -86,17 +99,18 @@ class CifarHipStage(StageCompute):
     def forward(self, x, out=None):
         B = x.shape[0]
         buf = self._buf(B)
+        h = x
         if self.first:
-            if x.dtype != torch.float32:
-                x = x.float()
-            x = x.contiguous()
-            mid = buf["mid"] if self.last else out
-            h = self._cops.stage0_forward(x, self.w0, mid)
-            if not self.last:
+            if h.dtype != torch.float32:
+                h = h.float()
+            h = self._cops.stage0_forward(h.contiguous(), self.w0, buf["mid"] if self.end >= 2 else out)
+            if self.end == 1:
                 return h
-        else:
-            h = x
-        probs, pred = self._cops.head_forward(h, self.wh, buf["hid"], out, buf["pred"])
+        if self.start <= 2 <= self.end:
+            h = self._cops.fc1_forward(h, self.wh, out if self.end == 2 else buf["hid"])
+            if self.end == 2:
+                return h
+        probs, pred = self._cops.head_tail(h, self.wh, out, buf["pred"])
         return StageOutput(probs, pred)
 
 

@@ -79,3 +79,39 @@ def test_cifar_stage0_and_head(B):
     assert agree > 0.9
     # argmax must be consistent with our own probabilities
     assert torch.equal(pred.cpu().long(), probs.cpu().argmax(1))
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_cifar_stage0_variants_agree(variant):
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork, CifarStage
+    from distributed_neural_networks_amd.ops import cifar as cops
+    torch.manual_seed(4)
+    sd = NeuralNetwork().state_dict()
+    w0 = cops.pack_stage0(sd, DEV)
+    for B in (1, 5, 300, 4099):
+        x = torch.randn(B, 3, 32, 32)
+        ref = CifarStage(0, 1)
+        ref.load_state_dict(sd, strict=False)
+        with torch.no_grad():
+            r = ref(x)
+        h = cops.stage0_forward(x.to(DEV), w0, variant=variant)
+        assert _rel(h.cpu(), r) < 1e-2, (variant, B)
+
+
+@pytest.mark.parametrize("cut", [1, 2])
+def test_cifar_stage_cuts(cut):
+    """Both 2-stage cuts (reference conv|fc and the fc1 cut) reproduce the full model."""
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
+    torch.manual_seed(5)
+    m = NeuralNetwork().eval()
+    sd = m.state_dict()
+    st = [CifarHipStage(sd, 0, cut, DEV), CifarHipStage(sd, cut + 1, 3, DEV)]
+    x = torch.randn(64, 3, 32, 32)
+    out = ColocatedPipeline(st, 64)(x.to(DEV))
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = m(x)
+    assert (out.probs.cpu() - ref).abs().max().item() < 2e-2
+    assert st[0].out_spec(8)[0] == (8, 4096 if cut == 1 else 512)
