@@ -92,7 +92,7 @@ def main(args=None):
     M = args.microbatches or groups
     B = args.batch
     T0 = args.prompt
-    total_steps = args.warmup + args.steps
+    total_steps = args.warmup + args.steps + 16 + 2  # + the 16 latency steps + graph-capture slack
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
     stages = _build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8) if stage_ids else []

@@ -44,6 +44,7 @@ __global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict
     r /= heads;
     const int t = (int)(r % T), b = (int)(r / T);
     const int p = (pos != nullptr ? pos[b] : 0) + t;
+    if (p >= S) continue;  // past the cache capacity: drop (never write out of bounds)
     const bf16_t* src = qkv + (size_t)(b * T + t) * ld + hh * hd;
     const int i0 = g * 8;
     const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(src + i0);
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const int q_abs = p0 + min(qrow, T - 1);
   const int wave_qmax = p0 + min(qrow0 + 31, T - 1);   // wave-uniform
   const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
-  const int kv_end = min(kv_len, blk_qmax + 1);
+  const int kv_end = min(min(kv_len, blk_qmax + 1), S);  // never read past the cache
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[qrow][ks*16 + 8h + j]
   bf16x8 qf[NKS];
@@ -241,13 +242,15 @@ template <int HD, int G>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                           const bf16_t* __restrict__ vc, float* __restrict__ ws, int H,
                                                           int Hkv, int S, const int* __restrict__ lens, float scale_log2,
-                                                          int chunk) {
+                                                          int chunk_cap, bf16_t* __restrict__ o_direct) {
   constexpr int LPK = HD / 8;           // lanes per key row (16 B each)
   constexpr int GPB = 256 / LPK;        // key groups per block
-  extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk] scores, then reduction scratch
+  extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk_cap] scores, then reduction scratch
   const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
   const int b = bk / Hkv, kvh = bk % Hkv;
-  const int len = lens[b];
+  const int len = min(lens[b], S);  // never read past the cache capacity
+  // splits share the *runtime* length evenly (one captured graph serves every step)
+  const int chunk = (len + NS - 1) / NS;
   const int k0 = split * chunk, k1 = min(len, k0 + chunk);
   const int tid = threadIdx.x, sub = tid % LPK, grp = tid / LPK;
   float* wsp = ws + ((size_t)bk * NS + split) * G * (HD + 2);
@@ -269,6 +272,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
+#pragma unroll 4
   for (int kk = grp; kk < n; kk += GPB) {
     const bf16x8 kr = *reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
     float kf[8];
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
 #pragma unroll
       for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      if (sub == 0) sc[g * chunk + kk] = d * scale_log2;
+      if (sub == 0) sc[g * chunk_cap + kk] = d * scale_log2;
     }
   }
   __syncthreads();
@@ -290,12 +294,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   const int wave = tid >> 6, lane = tid & 63;
   for (int g = wave; g < G; g += 4) {
     float mx = -INFINITY;
-    for (int i = lane; i < n; i += 64) mx = fmaxf(mx, sc[g * chunk + i]);
+    for (int i = lane; i < n; i += 64) mx = fmaxf(mx, sc[g * chunk_cap + i]);
     mx = wave_max(mx);
     float s = 0.f;
     for (int i = lane; i < n; i += 64) {
-      const float e = exp2f(sc[g * chunk + i] - mx);
-      sc[g * chunk + i] = e;
+      const float e = exp2f(sc[g * chunk_cap + i] - mx);
+      sc[g * chunk_cap + i] = e;
       s += e;
     }
     s = wave_sum(s);
@@ -308,6 +312,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+#pragma unroll 4
   for (int kk = grp; kk < n; kk += GPB) {
     const bf16x8 vr = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
     float vf[8];
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int j = 0; j < 8; ++j) vf[j] = bf2f_s(vr[j]);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float pw = sc[g * chunk + kk];
+      const float pw = sc[g * chunk_cap + kk];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[g][j] += pw * vf[j];
     }
@@ -331,9 +336,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     const int g = i / HD, d = i % HD;
     float s = 0.f;
     for (int r = 0; r < GPB; ++r) s += red[((size_t)r * G + g) * HD + d];
-    wsp[g * (HD + 2) + d] = s;
+    if (NS == 1) {  // single split: normalise and write the output directly (no combine pass)
+      o_direct[(size_t)b * H * HD + (kvh * G + g) * HD + d] = f2bf(s / lh[g]);
+    } else {
+      wsp[g * (HD + 2) + d] = s;
+    }
   }
-  if (tid < G) {
+  if (NS > 1 && tid < G) {
     wsp[tid * (HD + 2) + HD] = mh[tid];
     wsp[tid * (HD + 2) + HD + 1] = lh[tid];
   }
@@ -399,19 +408,20 @@ extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, vo
                                int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {
   const int G = H / Hkv;
   if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
-  const int chunk = (S + splits - 1) / splits;
+  const int chunk_cap = (S + splits - 1) / splits;
   const int gpb = 256 / (hd / 8);
-  size_t smem = sizeof(float) * (size_t)G * (size_t)(chunk > gpb * hd ? chunk : gpb * hd);
+  size_t smem = sizeof(float) * (size_t)G * (size_t)(chunk_cap > gpb * hd ? chunk_cap : gpb * hd);
   if (smem > 160 * 1024) return -3;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(B * Hkv, splits);
 #define DEC(HDV, GV)                                                                                               \
   if (hd == HDV && G == GV) {                                                                                      \
     hipLaunchKernelGGL((attn_decode_kernel<HDV, GV>), grid, dim3(256), smem, st, (const bf16_t*)q, (const bf16_t*)kc, \
-                       (const bf16_t*)vc, ws, H, Hkv, S, lens, sl2, chunk);                                        \
+                       (const bf16_t*)vc, ws, H, Hkv, S, lens, sl2, chunk_cap, (bf16_t*)o);                        \
   } else
   DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(128, 1) DEC(128, 2) DEC(128, 4) DEC(128, 8) { return -2; }
 #undef DEC
-  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
+  if (splits > 1)
+    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
   return (int)hipGetLastError();
 }

@@ -49,6 +49,100 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
   return *reinterpret_cast<const bf16x8*>(tile + row * 128 + ((chunk ^ swz_chunk(row)) << 4));
 }
 
+// Tile order: the XCD remap gives each XCD a contiguous run of logical ids;
+// inside it tiles go GROUP_M rows of M-tiles at a time, M fastest, so the ~32-64
+// tiles co-resident on one XCD share a few A and W panels in its L2.
+__device__ __forceinline__ void tile_coords(int logical, int ntm, int ntn, int& tm, int& tn) {
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * ntn;
+  const int grp = logical / per_group;
+  const int first = grp * GROUP_M;
+  const int gm = min(ntm - first, GROUP_M);
+  const int r = logical - grp * per_group;
+  tm = first + r % gm;
+  tn = r / gm;
+}
+
+// Epilogue on a TRANSPOSED accumulator: the MFMAs are issued as W.A^T, so a
+// lane holds 4 consecutive output columns n..n+3 of one row m (C/D map of the
+// 16x16 MFMA with the operands swapped) and writes them as one 8-B (bf16) or
+// 16-B (fp32) store instead of four scattered 2-B stores.
+// Vector epilogue stores need 4-column-aligned rows and 16-B aligned bases.
+__device__ __forceinline__ bool epi_vec_ok(const void* C, int ldc, const float* bias, const bf16_t* R, int ldr) {
+  const uintptr_t p = (uintptr_t)C | (uintptr_t)bias | (uintptr_t)R;
+  return ((ldc | (R != nullptr ? ldr : 0)) & 3) == 0 && (p & 15) == 0;
+}
+
+template <int ACT, bool OUT_F32>
+__device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void* __restrict__ Cv, int ldc,
+                                       const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
+                                       bool vec) {
+  if (m >= M) return;
+  if (vec && n + 3 < N) {
+    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (ACT == ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+      if (ACT == ACT_GELU) v[r] = gelu_erf(v[r]);
+    }
+    if (R != nullptr) {
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bf2f((bf16_t)rr[r]);
+    }
+    if (OUT_F32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + n) = v;
+    } else {
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + n) = pk;
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int nn = n + r;
+    if (nn < N) {
+      float x = v[r] + (bias != nullptr ? bias[nn] : 0.f);
+      if (ACT == ACT_RELU) x = fmaxf(x, 0.f);
+      if (ACT == ACT_GELU) x = gelu_erf(x);
+      if (R != nullptr) x += bf2f(R[(size_t)m * ldr + nn]);
+      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + nn] = x;
+      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + nn] = f2bf(x);
+    }
+  }
+}
+
+// SwiGLU epilogue on transposed accumulators: g = gate columns, u = the matching
+// up columns (packed gate|up weights, ops/gemm.py pack_gate_up); output columns
+// ncol..ncol+3 of a [M, N/2] result.
+template <bool OUT_F32>
+__device__ __forceinline__ void epi_silu_t4(const f32x4& g, const f32x4& u, int m, int ncol, int M, int NO,
+                                            void* __restrict__ Cv, int ldc, bool vec) {
+  if (m >= M) return;
+  f32x4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = silu(g[r]) * u[r];
+  if (vec && ncol + 3 < NO) {
+    if (OUT_F32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + ncol) = v;
+    } else {
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + ncol) = pk;
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (ncol + r < NO) {
+      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + ncol + r] = v[r];
+      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + ncol + r] = f2bf(v[r]);
+    }
+}
+
 template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
@@ -56,8 +150,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
   __shared__ __attribute__((aligned(16))) char smem[4 * G_TILE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + GB_N - 1) / GB_N, ntm = (M + GB_M - 1) / GB_M;
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = tile / ntn, tn = tile % ntn;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
   const int m0 = tm * GB_M, n0 = tn * GB_N;
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -93,54 +187,202 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // Epilogue: C/D map of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
+  // Epilogue (transposed accumulators): lane holds row m = .. + (lane&15), cols n..n+3.
+  const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (ACT == ACT_SILU_MUL) continue;
-    const float b = (bias != nullptr && n < N) ? bias[n] : 0.f;
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (ACT == ACT_SILU_MUL) {
+      // packed gate|up: n-tile j even = gate, j+1 = the matching up columns
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; j += 2)
+        epi_silu_t4<OUT_F32>(acc[i][j], acc[i][j + 1], m, (n0 + wn * 64 + j * 16) / 2 + (lane >> 4) * 4, M, N / 2,
+                             Cv, ldc, vec);
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) {
-          float v = acc[i][j][r] + b;
-          if (ACT == ACT_RELU) v = fmaxf(v, 0.f);
-          if (ACT == ACT_GELU) v = gelu_erf(v);
-          if (R != nullptr) v += bf2f(R[(size_t)m * ldr + n]);
-          if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + n] = v;
-          else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + n] = f2bf(v);
-        }
-      }
+      for (int j = 0; j < 4; ++j)
+        epi_t4<ACT, OUT_F32>(acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr, vec);
     }
   }
-  if (ACT == ACT_SILU_MUL) {
-    // Packed gate/up weights: within each 32-column group, columns 0..15 are
-    // gate rows and 16..31 the matching up rows (ops/gemm.py pack_gate_up), so a
-    // lane holds g (tile j even) and u (tile j+1) for the same output column.
+}
+
+// ---------------------------------------------------------------------------
+// Large-tile GEMM: 256x256x64, 8 waves (2 M x 4 N), ~1 block per CU, the
+// 4-phase-per-K-tile schedule of the guide's 256^2 template (§5 "8-phase"):
+//
+//   LDS = [2 buffers][A0 A1 B0 B1] half-tiles of 128 rows x 64 k (16 KiB each),
+//   one __shared__ array (trap 4(a)).  Half-tile h of A holds the rows of every
+//   wave's output quadrant-row h, so a wave's 128x64 output is 2x2 quadrants of
+//   64x32 and each phase is one quadrant x K=64 = 16 MFMAs:
+//
+//     ph1: read B0 (4 ds_read_b128), A0 (8)  | stage A1[t+1] -> buf^1 | C00
+//     ph2: read B1 (4)                       | stage B0[t+1] -> buf^1 | C01
+//     ph3: read A1 (8)                       | stage A0[t+2] -> buf   | C11
+//     ph4: read B0 (4)                       | stage B1[t+2] -> buf   | C10
+//          + s_waitcnt vmcnt(4)  (retires everything of tile t+1)
+//
+//   Every restage lands >= 2 phases after the last read of that half-tile
+//   (WAR), every read is >= 1 phase after the vmcnt+barrier that retired its
+//   DMA (RAW).  Each phase = [ds_reads + 2 glds] s_barrier [lgkmcnt(0),
+//   setprio(1), 16 MFMA] s_barrier; waves of M-row 1 run one barrier behind
+//   M-row 0, so on every SIMD one wave issues LDS reads while its partner
+//   issues MFMAs.  glds stays in flight across barriers (raw s_barrier, counted
+//   vmcnt, never __syncthreads in the loop).  Loads past the last K-tile are
+//   clamped to it (harmless refills of dead buffers) so the vmcnt count is
+//   uniform.
+// ---------------------------------------------------------------------------
+constexpr int BG_M = 256, BG_N = 256, BG_K = 64;
+constexpr int BG_HALF = 128 * BG_K * 2;  // 16 KiB
+
+// Stage one 128x64 half-tile: 2 glds per thread, 8 rows per wave-instruction.
+__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, int ld, int r0, int nrows, int k0,
+                                           char* dst, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      const int ncol = (n0 + wn * 64 + j * 16) / 2 + (lane & 15);
+  for (int i = 0; i < 2; ++i) {
+    const int piece = i * 8 + wave;
+    const int rl = piece * 8 + (lane >> 3);
+    const int cs = (lane & 7) ^ swz_chunk(rl);
+    int r = r0 + rl;
+    r = r < nrows ? r : nrows - 1;
+    glds16(src + (size_t)r * ld + k0 + cs * 8, dst + piece * 1024);
+  }
+}
+
+__device__ __forceinline__ void bg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int MI, int NJ>
+__device__ __forceinline__ void bg_mfma(f32x4 (&acc)[MI][NJ], const bf16x8 (&a)[MI][2], const bf16x8 (&b)[NJ][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int N>
+__device__ __forceinline__ void bg_read(bf16x8 (&f)[N][2], const char* half, int row0, int lane) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) f[i][s] = lds_frag(half, row0 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
+}
+
+template <int ACT, bool OUT_F32>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
+    const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
+    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
+  const int m0 = tm * BG_M, n0 = tn * BG_N;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nk = K / BG_K;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < M && ncol < N / 2) {
-            const float v = silu(acc[i][j][r]) * acc[i][j + 1][r];
-            if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + ncol] = v;
-            else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + ncol] = f2bf(v);
-          }
-        }
-    }
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile h of buffer u: A0=0, A1=1, B0=2, B1=3
+  auto half = [&](int u, int h) { return smem + (u * 4 + h) * BG_HALF; };
+  auto stA = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(A, lda, m0 + h * 128, M, t * BG_K, half(u, h), wave, lane);
+  };
+  auto stB = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
+  };
+
+  // prologue: tile 0 complete, A0/B1 of tile 1 in flight
+  stA(0, 0, 0);
+  stB(0, 1, 0);
+  stA(0, 1, 0);
+  stB(0, 0, 0);
+  stA(1, 0, 1);
+  stB(1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bg_barrier();
+  if (wr == 1) bg_barrier();
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 64, brow = wc * 32;
+  for (int t = 0; t < nk; ++t) {
+    const int u = t & 1;
+    // ph1
+    bg_read<2>(b0, half(u, 2), brow, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    bg_read<4>(af, half(u, 0), arow, lane);
+    stA(u ^ 1, 1, t + 1);
+    bg_barrier();
+    bg_mfma<4, 2>(acc[0][0], af, b0);
+    bg_barrier();
+    // ph2
+    bg_read<2>(b1, half(u, 3), brow, lane);
+    stB(u ^ 1, 0, t + 1);
+    bg_barrier();
+    bg_mfma<4, 2>(acc[0][1], af, b1);
+    bg_barrier();
+    // ph3
+    bg_read<4>(af, half(u, 1), arow, lane);
+    stA(u, 0, t + 2);
+    bg_barrier();
+    bg_mfma<4, 2>(acc[1][1], af, b1);
+    bg_barrier();
+    // ph4
+    bg_read<2>(b0, half(u, 2), brow, lane);
+    stB(u, 1, t + 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    bg_barrier();
+    bg_mfma<4, 2>(acc[1][0], af, b0);
+    bg_barrier();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wr == 0) bg_barrier();
+
+  // Epilogue (transposed accumulators):
+  //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
+  //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
+  const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
+        const int nb = n0 + nq * 128 + wc * 32;
+        if (ACT == ACT_SILU_MUL) {
+          epi_silu_t4<OUT_F32>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb / 2 + (lane >> 4) * 4, M, N / 2, Cv, ldc,
+                               vec);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            epi_t4<ACT, OUT_F32>(acc[mq][nq][i][j], m, nb + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr,
+                                 vec);
+        }
+      }
 }
 
 // ---------------------------------------------------------------------------
@@ -237,6 +479,16 @@ __global__ void silu_mul_packed_kernel(const bf16_t* __restrict__ gu, int ld_in,
 // ------------------------------- host API ----------------------------------
 using namespace dnn;
 
+// Large-GEMM tile selection: 0 = auto (256x256 when it still yields >= 256
+// blocks), 128 / 256 force a tile (A/B benchmarking, tests).
+static int g_gemm_tile = 0;
+
+extern "C" int dnn_gemm_set_tile(int tile) {
+  if (tile != 0 && tile != 128 && tile != 256) return -1;
+  g_gemm_tile = tile;
+  return 0;
+}
+
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                         const void* R, int ldr, int M, int N, int K, hipStream_t st) {
@@ -251,8 +503,23 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
 #undef SK
     return;
   }
-  const int tiles = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
-  hipLaunchKernelGGL((gemm_bf16_tn_kernel<ACT, F32>), dim3(tiles), dim3(256), 0, st, (const bf16_t*)A, lda,
+  // Auto choice by wave quantisation: the 256^2 kernel runs 1 block/CU (256
+  // slots) and is ~1.25x the 128^2 kernel (2 blocks/CU, 512 slots) per slot
+  // when both fill the chip (bench/gemm_bench.py, profiles/).
+  const int tiles256 = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+  const int tiles128 = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
+  auto fill = [](int tiles, int slots) {
+    const int waves = (tiles + slots - 1) / slots;
+    return (double)tiles / ((double)waves * slots);
+  };
+  const bool big = g_gemm_tile == 256 ||
+                   (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.25 * fill(tiles256, 256) > fill(tiles128, 512));
+  if (big) {
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
+                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_bf16_tn_kernel<ACT, F32>), dim3(tiles128), dim3(256), 0, st, (const bf16_t*)A, lda,
                      (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);
 }
 

@@ -53,6 +53,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
+def set_gemm_tile(tile: int = 0) -> None:
+    """Force the large-GEMM tile (128 or 256) or restore the auto choice (0)."""
+    check(lib().gemm_set_tile(int(tile)), "gemm_set_tile")
+
+
 def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     """Interleave gate/up rows in 16-row groups: [g0..g15, u0..u15, g16..g31, ...]
     so the GEMM epilogue sees matching gate/up columns in one lane (ACT_SILU_MUL)."""

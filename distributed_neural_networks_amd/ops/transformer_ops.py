@@ -76,10 +76,12 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
 
 
 def decode_splits(S: int, B: int, Hkv: int) -> int:
-    """Split-K factor for decode attention: enough workgroups to cover the CUs,
-    chunks of >= 256 keys."""
-    want = max(1, -(-512 // max(1, B * Hkv)))
-    return max(1, min(want, -(-S // 256)))
+    """Split-K factor for decode attention: enough workgroups to cover the 256
+    CUs, at most one split per 64 keys of cache capacity.  Each split takes
+    ``ceil(len/splits)`` of the *runtime* length, so short contexts stay
+    balanced; with one split the kernel writes the output itself (no combine)."""
+    want = max(1, -(-256 // max(1, B * Hkv)))
+    return max(1, min(want, -(-S // 64)))
 
 
 def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, H: int, Hkv: int,

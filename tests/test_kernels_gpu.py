@@ -31,6 +31,53 @@ def test_gemm_bf16(M, N, K, act):
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 4096), (300, 2304, 768), (1000, 520, 192),
+                                   (2048, 768, 3072), (65, 300, 128)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_gemm_bf16_256_tile(M, N, K, act):
+    """The 256x256 4-phase GEMM (forced), including edge tiles and odd K-tile counts."""
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
+    if act == 3 and N % 32:
+        pytest.skip("packed gate|up needs N % 32 == 0")
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV)
+    set_gemm_tile(256)
+    try:
+        if act == 3:
+            y = linear(x, w, act="silu_mul")
+        else:
+            r = torch.randn(M, N, device=DEV).bfloat16()
+            y = linear(x, w, b, act=act, residual=r)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_tile(0)
+    ref = x.float() @ w.float().t()
+    if act == 3:
+        g = ref.view(M, N // 32, 2, 16)
+        ref = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, N // 2)
+    else:
+        ref = ref + b
+        ref = torch.relu(ref) if act == 1 else torch.nn.functional.gelu(ref) if act == 2 else ref
+        ref = ref + r.float()
+    assert _rel(y, ref) < 1e-2
+
+
+def test_gemm_256_asymmetric_layout():
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
+    n = 512
+    x = torch.eye(n, device=DEV).bfloat16()
+    w = torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n).remainder(97).bfloat16()
+    set_gemm_tile(256)
+    try:
+        y = linear(x, w, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_tile(0)
+    assert torch.equal(y, w.float().t())
+
+
 def test_gemm_asymmetric_layout():
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     from distributed_neural_networks_amd.ops.gemm import linear
