@@ -51,7 +51,7 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8):
     out = []
     for s in stage_ids:
         a, b = ranges[s]
-        sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0)
+        sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0, device=dev)
         out.append(TransformerStage(model, sd, a, b, s == 0, s == S - 1, dev, max_batch=max_batch,
                                     max_seq=max_seq, fp8=fp8))
         del sd

@@ -28,6 +28,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
                         int K, int act, int out_f32, u64 st) {
     return dnn_gemm_bf16(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, out_f32, ST(st));
   });
+  m.def("gemm_skinny", [](u64 A, int lda, u64 sa, u64 W, int ldw, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr,
+                          int M, int N, int K, int act, int out_f32, int fp8, u64 st) {
+    return dnn_gemm_skinny(CP(A), lda, CFP(sa), CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act,
+                           out_f32, fp8, ST(st));
+  });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
   m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {
     return dnn_silu_mul_packed(CP(gu), ld_in, P(out), ld_out, M, F, ST(st));

@@ -237,6 +237,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
 // unnormalised partial (o, m, l) to ws; decode_combine merges the splits.
 // ---------------------------------------------------------------------------
 constexpr int DEC_MAXG = 8;
+constexpr int DEC_U = 8;  // key/value rows in flight per thread
 
 template <int HD, int G>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
@@ -272,20 +273,31 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
-#pragma unroll 4
-  for (int kk = grp; kk < n; kk += GPB) {
-    const bf16x8 kr = *reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
-    float kf[8];
+  // Scores: batches of DEC_U key rows per thread, all loads issued before the
+  // first use (memory-level parallelism is the whole game in decode).
+  for (int kb0 = 0; kb0 < n; kb0 += GPB * DEC_U) {
+    bf16x8 kr[DEC_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) kf[j] = bf2f_s(kr[j]);
+    for (int u = 0; u < DEC_U; ++u) {
+      const int kk = min(kb0 + u * GPB + grp, n - 1);
+      kr[u] = *reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float d = 0.f;
+    for (int u = 0; u < DEC_U; ++u) {
+      const int kk = kb0 + u * GPB + grp;
+      float kf[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
+      for (int j = 0; j < 8; ++j) kf[j] = bf2f_s(kr[u][j]);
 #pragma unroll
-      for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      if (sub == 0) sc[g * chunk_cap + kk] = d * scale_log2;
+      for (int g = 0; g < G; ++g) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
+#pragma unroll
+        for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0 && kk < n) sc[g * chunk_cap + kk] = d * scale_log2;
+      }
     }
   }
   __syncthreads();
@@ -312,17 +324,25 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-#pragma unroll 4
-  for (int kk = grp; kk < n; kk += GPB) {
-    const bf16x8 vr = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
-    float vf[8];
+  for (int kb0 = 0; kb0 < n; kb0 += GPB * DEC_U) {
+    bf16x8 vr[DEC_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vf[j] = bf2f_s(vr[j]);
+    for (int u = 0; u < DEC_U; ++u) {
+      const int kk = min(kb0 + u * GPB + grp, n - 1);
+      vr[u] = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float pw = sc[g * chunk_cap + kk];
+    for (int u = 0; u < DEC_U; ++u) {
+      const int kk = kb0 + u * GPB + grp;
+      if (kk < n) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[g][j] += pw * vf[j];
+        for (int g = 0; g < G; ++g) {
+          const float pw = sc[g * chunk_cap + kk];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[g][j] += pw * bf2f_s(vr[u][j]);
+        }
+      }
     }
   }
   __syncthreads();  // scores no longer needed: reuse dsm as [GPB][G][HD] reduction scratch

@@ -15,14 +15,11 @@
 // makes the ds_read_b128 fragment reads conflict-free (rule 21 / T2).
 // Block ids are remapped so tiles sharing A panels run on one XCD (T1).
 //
-// Small-M variant (decode, M <= 64): split-K 64xBN tiles reduce through fp32
-// atomics into a workspace is avoided; instead gemm_skinny streams W straight to
-// VGPRs (the 'GEMV / M <= 16' row of the guide) — see gemm_skinny below.
-#include "common.h"
+// Decode-sized M (<= 64) goes to the weight-streaming kernels of gemm_skinny.hip.
+#include "api.h"
+#include "gemm_epilogue.h"
 
 namespace dnn {
-
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU_MUL = 3 };
 
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int G_TILE_BYTES = GB_M * GB_K * 2;  // 16 KiB per operand tile
@@ -67,82 +64,6 @@ __device__ __forceinline__ void tile_coords(int logical, int ntm, int ntn, int& 
 // lane holds 4 consecutive output columns n..n+3 of one row m (C/D map of the
 // 16x16 MFMA with the operands swapped) and writes them as one 8-B (bf16) or
 // 16-B (fp32) store instead of four scattered 2-B stores.
-// Vector epilogue stores need 4-column-aligned rows and 16-B aligned bases.
-__device__ __forceinline__ bool epi_vec_ok(const void* C, int ldc, const float* bias, const bf16_t* R, int ldr) {
-  const uintptr_t p = (uintptr_t)C | (uintptr_t)bias | (uintptr_t)R;
-  return ((ldc | (R != nullptr ? ldr : 0)) & 3) == 0 && (p & 15) == 0;
-}
-
-template <int ACT, bool OUT_F32>
-__device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void* __restrict__ Cv, int ldc,
-                                       const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
-                                       bool vec) {
-  if (m >= M) return;
-  if (vec && n + 3 < N) {
-    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + n);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (ACT == ACT_RELU) v[r] = fmaxf(v[r], 0.f);
-      if (ACT == ACT_GELU) v[r] = gelu_erf(v[r]);
-    }
-    if (R != nullptr) {
-      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += bf2f((bf16_t)rr[r]);
-    }
-    if (OUT_F32) {
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + n) = v;
-    } else {
-      uint2 pk;
-      pk.x = pack2bf(v[0], v[1]);
-      pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + n) = pk;
-    }
-    return;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int nn = n + r;
-    if (nn < N) {
-      float x = v[r] + (bias != nullptr ? bias[nn] : 0.f);
-      if (ACT == ACT_RELU) x = fmaxf(x, 0.f);
-      if (ACT == ACT_GELU) x = gelu_erf(x);
-      if (R != nullptr) x += bf2f(R[(size_t)m * ldr + nn]);
-      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + nn] = x;
-      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + nn] = f2bf(x);
-    }
-  }
-}
-
-// SwiGLU epilogue on transposed accumulators: g = gate columns, u = the matching
-// up columns (packed gate|up weights, ops/gemm.py pack_gate_up); output columns
-// ncol..ncol+3 of a [M, N/2] result.
-template <bool OUT_F32>
-__device__ __forceinline__ void epi_silu_t4(const f32x4& g, const f32x4& u, int m, int ncol, int M, int NO,
-                                            void* __restrict__ Cv, int ldc, bool vec) {
-  if (m >= M) return;
-  f32x4 v;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = silu(g[r]) * u[r];
-  if (vec && ncol + 3 < NO) {
-    if (OUT_F32) {
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + ncol) = v;
-    } else {
-      uint2 pk;
-      pk.x = pack2bf(v[0], v[1]);
-      pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + ncol) = pk;
-    }
-    return;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (ncol + r < NO) {
-      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + ncol + r] = v[r];
-      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + ncol + r] = f2bf(v[r]);
-    }
-}
-
 template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
@@ -385,82 +306,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
       }
 }
 
-// ---------------------------------------------------------------------------
-// Skinny GEMM for decode-sized M (<= 16 rows): weight-streaming, one wave per
-// 16 output columns, split over K across the 4 waves of a workgroup, W loaded
-// straight to VGPRs (no LDS round trip: guide §5 table, GEMV row). A (tiny) is
-// read through L1/L2. Uses mfma_f32_16x16x32_bf16 with M padded to 16.
-// ---------------------------------------------------------------------------
-template <int ACT, bool OUT_F32, int MT>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(
-    const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
-    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K) {
-  // MT 16-row M tiles share every W fragment (M <= 16*MT rows).
-  __shared__ __attribute__((aligned(16))) f32x4 red[4][MT][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
-  const int n = n0 + (lane & 15);
-  const int nc = n < N ? n : N - 1;
-  const int kq = (lane >> 4) * 8;
-  f32x4 acc[MT];
-  const bf16_t* ap[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int mrow = t * 16 + (lane & 15);
-    ap[t] = A + (size_t)(mrow < M ? mrow : M - 1) * lda;
-  }
-  // K split into 4 contiguous quarters (one per wave), each a multiple of 32
-  const int kper = ((K / 32 + 3) / 4) * 32;
-  const int kbeg = wave * kper;
-  const int kend = min(K, kbeg + kper);
-  const bf16_t* wp = W + (size_t)nc * ldw;
-  int k = kbeg;
-  for (; k + 128 <= kend; k += 128) {
-    bf16x8 b[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const bf16x8*>(wp + k + u * 32 + kq);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      bf16x8 a[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(ap[t] + k + u * 32 + kq);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc[t], 0, 0, 0);
-    }
-  }
-  for (; k < kend; k += 32) {
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(wp + k + kq);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap[t] + k + kq);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < MT; ++t) red[wave][t][lane] = acc[t];
-  __syncthreads();
-  // reduction + epilogue: wave w handles M tiles t = w, w+4, ...
-  const float bb = (bias != nullptr && n < N) ? bias[n] : 0.f;
-  for (int t = wave; t < MT; t += 4) {
-    f32x4 s = red[0][t][lane];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) s += red[w][t][lane];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = t * 16 + (lane >> 4) * 4 + r;
-      if (m < M && n < N) {
-        float v = s[r] + bb;
-        if (ACT == ACT_RELU) v = fmaxf(v, 0.f);
-        if (ACT == ACT_GELU) v = gelu_erf(v);
-        if (R != nullptr) v += bf2f(R[(size_t)m * ldr + n]);
-        if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + n] = v;
-        else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + n] = f2bf(v);
-      }
-    }
-  }
-}
-
 // SwiGLU for the skinny path: h[m, j] = silu(g[m, j]) * u[m, j] where the skinny
 // GEMM produced the packed [M, 2F] fp32/bf16 output.
 __global__ void silu_mul_packed_kernel(const bf16_t* __restrict__ gu, int ld_in, bf16_t* __restrict__ out,
@@ -492,15 +337,8 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                         const void* R, int ldr, int M, int N, int K, hipStream_t st) {
-  if (M <= 64 && ACT != ACT_SILU_MUL) {
-    dim3 grid((N + 15) / 16);
-#define SK(MTV)                                                                                         \
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MTV>), grid, dim3(256), 0, st, (const bf16_t*)A, lda, \
-                     (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K)
-    if (M <= 16) SK(1);
-    else if (M <= 32) SK(2);
-    else SK(4);
-#undef SK
+  if (M <= 64) {  // decode-sized: weight-streaming skinny kernels (gemm_skinny.hip)
+    dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st);
     return;
   }
   // Auto choice by wave quantisation: the 256^2 kernel runs 1 block/CU (256

@@ -35,13 +35,13 @@ def kpad_of(k: int) -> int:
 
 
 def quantize_weight(w: torch.Tensor, device) -> Fp8Weight:
-    wf = w.float()
+    wf = w.to(device).float()  # quantise where the weight will live (fast on the GPU)
     N, K = wf.shape
     amax = wf.abs().amax(dim=1).clamp_min(1e-12)
     s = amax / FP8_MAX
-    q = torch.zeros((N, kpad_of(K)), dtype=torch.float8_e4m3fn)
+    q = torch.zeros((N, kpad_of(K)), dtype=torch.float8_e4m3fn, device=wf.device)
     q[:, :K] = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
-    return Fp8Weight(q.to(device).contiguous(), s.to(device=device, dtype=torch.float32).contiguous(), K)
+    return Fp8Weight(q.contiguous(), s.to(dtype=torch.float32).contiguous(), K)
 
 
 def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: Optional[int] = None):
@@ -70,6 +70,11 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     o2 = out.reshape(-1, out.shape[-1])
     r2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
+    if M <= 64:  # decode: fp8 weight streaming (half the bytes of bf16)
+        check(lib().gemm_skinny(ptr(qbuf), kp, ptr(sbuf), ptr(w.q), kp, ptr(w.scale), ptr(o2), o2.stride(0),
+                                ptr(bias), ptr(r2), 0 if r2 is None else r2.stride(0), M, N, kp, act, 0, 1,
+                                stream_ptr()), "gemm_skinny_fp8")
+        return out
     check(lib().gemm_fp8(ptr(qbuf), ptr(sbuf), ptr(w.q), ptr(w.scale), ptr(o2), o2.stride(0), ptr(bias), ptr(r2),
                          0 if r2 is None else r2.stride(0), M, N, kp, act, stream_ptr()), "gemm_fp8")
     return out

@@ -40,13 +40,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     r2 = None
     if residual is not None:
         r2 = residual.reshape(-1, residual.shape[-1]) if residual.dim() != 2 else residual
-    if a == ACT_SILU_MUL and M <= 64:
-        # skinny path: packed gate|up GEMM then the elementwise SwiGLU
-        tmp = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
-        check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(tmp), N, 0, 0, 0, M, N, K,
-                              ACT_NONE, 0, stream_ptr()), "gemm_bf16")
-        check(lib().silu_mul_packed(ptr(tmp), N, ptr(o2), o2.stride(0), M, Nout, stream_ptr()), "silu_mul")
-        return out
     check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
                           ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
                           1 if o2.dtype == torch.float32 else 0, stream_ptr()), "gemm_bf16")

@@ -76,11 +76,11 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
 
 
 def decode_splits(S: int, B: int, Hkv: int) -> int:
-    """Split-K factor for decode attention: enough workgroups to cover the 256
-    CUs, at most one split per 64 keys of cache capacity.  Each split takes
+    """Split-K factor for decode attention: enough workgroups for ~4 per CU
+    (1024), at most one split per 64 keys of cache capacity.  Each split takes
     ``ceil(len/splits)`` of the *runtime* length, so short contexts stay
     balanced; with one split the kernel writes the output itself (no combine)."""
-    want = max(1, -(-256 // max(1, B * Hkv)))
+    want = max(1, -(-1024 // max(1, B * Hkv)))
     return max(1, min(want, -(-S // 64)))
 
 

@@ -12,7 +12,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 768), (77, 200, 128), (4096, 512, 4096),
-                                   (1, 768, 768), (7, 3072, 768), (16, 50257, 768), (300, 2304, 768)])
+                                   (1, 768, 768), (7, 3072, 768), (16, 50257, 768), (300, 2304, 768),
+                                   (32, 4096, 14336), (64, 2304, 768), (40, 100, 128), (2, 28672, 4096)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_gemm_bf16(M, N, K, act):
     from distributed_neural_networks_amd.ops.gemm import linear
@@ -91,7 +92,7 @@ def test_gemm_asymmetric_layout():
 def test_gemm_silu_mul():
     from distributed_neural_networks_amd.ops.gemm import linear, pack_gate_up
     torch.manual_seed(1)
-    for M in (5, 200):
+    for M in (1, 5, 31, 64, 65, 200):
         x = torch.randn(M, 256, device=DEV).bfloat16()
         g = (torch.randn(512, 256, device=DEV) * 0.05).bfloat16()
         u = (torch.randn(512, 256, device=DEV) * 0.05).bfloat16()

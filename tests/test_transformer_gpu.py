@@ -160,7 +160,8 @@ def test_argmax_rows():
     assert torch.equal(out2.long().cpu(), xf.argmax(1).cpu())
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 512, 1024), (77, 4800, 1600), (3, 1600, 6400)])
+@pytest.mark.parametrize("M,N,K", [(256, 512, 1024), (77, 4800, 1600), (3, 1600, 6400), (64, 4800, 1600),
+                                   (33, 200, 1000), (1, 50257, 1600)])
 def test_fp8_gemm(M, N, K):
     from distributed_neural_networks_amd.ops.fp8 import linear_fp8, quantize_weight
     torch.manual_seed(3)
@@ -232,3 +233,25 @@ def test_fp8_stage_runs():
     with torch.no_grad():
         ref = g(ids)
     assert _rel(out.probs.view(2, 24, -1).cpu(), ref) < 0.15
+
+
+@pytest.mark.parametrize("M", [1, 16, 17, 48, 64])
+@pytest.mark.parametrize("act", [1, 2])
+def test_fp8_skinny_act_residual(M, act):
+    """Decode-size fp8 weight streaming with activation + residual epilogue."""
+    from distributed_neural_networks_amd.ops.fp8 import kpad_of, linear_fp8, quant_rows, quantize_weight
+    torch.manual_seed(7)
+    K, N = 1600, 6400
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K) * 0.05
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    wq = quantize_weight(w, DEV)
+    y = linear_fp8(x, wq, b, act=act, residual=r)
+    qb = torch.empty(M, kpad_of(K), dtype=torch.uint8, device=DEV)
+    sb = torch.empty(M, device=DEV)
+    quant_rows(x, qb, sb)
+    xq = qb[:, :K].view(torch.float8_e4m3fn).float() * sb[:, None]
+    ref = xq @ (wq.q[:, :K].float() * wq.scale[:, None]).t() + b
+    ref = torch.relu(ref) if act == 1 else torch.nn.functional.gelu(ref)
+    assert _rel(y, ref + r.float()) < 1e-2
