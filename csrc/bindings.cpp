@@ -74,6 +74,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
                           float scale, int splits, u64 ws, u64 st) {
     return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st));
   });
+  m.def("sample_topk", [](u64 x, int ld, int M, int N, u64 out, float temperature, int topk, unsigned seed, u64 step,
+                          u64 st) {
+    return dnn_sample_topk(CP(x), ld, M, N, reinterpret_cast<int*>(out), temperature, topk, seed,
+                           reinterpret_cast<const int*>(step), ST(st));
+  });
   m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st) {
     return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st));
   });

@@ -43,7 +43,7 @@ __device__ __forceinline__ f32x4 sk_mma(const i32x4& w, const i32x4& a, f32x4 ac
 }
 
 template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U>
-__global__ __launch_bounds__(1024) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
+__global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                            const float* __restrict__ sa, const uint8_t* __restrict__ W,
                                                            int ldw_b, const float* __restrict__ sw,
                                                            void* __restrict__ Cv, int ldc,
@@ -126,16 +126,19 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(const uint8_t* __rest
     const int m = t * 16 + (lane & 15);
     const float rs = (FP8 && m < M) ? sa[m] : 1.f;
     if constexpr (ACT == ACT_SILU_MUL) {
-      static_assert(NT == 2, "SwiGLU needs the gate and up tile");
-      if constexpr (FP8) {
-        const int ng = n0 + (lane >> 4) * 4, nu = ng + 16;
+      static_assert(NT % 2 == 0, "SwiGLU needs gate/up tile pairs");
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[0][r] *= rs * (ng + r < N ? sw[ng + r] : 0.f);
-          s[1][r] *= rs * (nu + r < N ? sw[nu + r] : 0.f);
+      for (int jp = 0; jp < NT; jp += 2) {
+        if constexpr (FP8) {
+          const int ng = n0 + jp * 16 + (lane >> 4) * 4, nu = ng + 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[jp][r] *= rs * (ng + r < N ? sw[ng + r] : 0.f);
+            s[jp + 1][r] *= rs * (nu + r < N ? sw[nu + r] : 0.f);
+          }
         }
+        epi_silu_t4<OUT_F32>(s[jp], s[jp + 1], m, (n0 + jp * 16) / 2 + (lane >> 4) * 4, M, N / 2, Cv, ldc, vec);
       }
-      epi_silu_t4<OUT_F32>(s[0], s[1], m, n0 / 2 + (lane >> 4) * 4, M, N / 2, Cv, ldc, vec);
     } else {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
@@ -152,39 +155,53 @@ using namespace dnn;
 // Waves per workgroup: enough workgroups x waves to cover the 256 CUs (x4 SIMDs)
 // while every wave keeps >= 2 chunks of K.
 static int skinny_ks(int groups, int nch) {
-  int ks = groups <= 64 ? 16 : groups <= 256 ? 8 : 4;
+  int ks = groups <= 256 ? 8 : 4;
   while (ks > 1 && nch / ks < 2) ks >>= 1;
   return ks;
 }
 
-template <int ACT, bool F32, bool FP8, int NT>
-static int launch_skinny_nt(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
-                            void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                            hipStream_t st) {
+// Per chunk a wave issues NT weight loads and MT activation loads (L2) for
+// NT x MT MFMAs: NT grows with MT so the activation re-reads stay <= the
+// weight bytes.  U = chunks in flight, sized for <= 256 VGPRs at 8 waves/WG.
+template <int ACT, bool F32, bool FP8, int MT, int NT, int U>
+static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
+                             void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
+                             hipStream_t st) {
   const int groups = (N + 16 * NT - 1) / (16 * NT);
   const int ks = skinny_ks(groups, kbytes / 64);
-  const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  const size_t smem = (size_t)ks * NT * mt * 64 * sizeof(f32x4);
-#define SKL(MTV, UV)                                                                                            \
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MTV, NT, FP8, UV>), dim3(groups), dim3(64 * ks), smem, st,  \
-                     (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R, \
-                     ldr, M, N, kbytes)
-  // U (chunks in flight per wave) sized to stay within 128 VGPRs at 16 waves/WG
-  if (mt == 1) SKL(1, (NT == 1 ? 8 : 4));
-  else if (mt == 2) SKL(2, 4);
-  else SKL(4, (NT == 1 ? 4 : 2));
-#undef SKL
+  const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U>), dim3(groups), dim3(64 * ks), smem, st,
+                     (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R, ldr,
+                     M, N, kbytes);
   return (int)hipGetLastError();
+}
+
+template <int ACT, bool F32, bool FP8, int MT, int U4>
+static int launch_skinny_mt(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
+                            void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
+                            hipStream_t st) {
+  // widest column tile that still leaves >= 128 workgroups (small N: latency-bound, keep the waves)
+  if (N >= 128 * 64)
+    return launch_skinny_cfg<ACT, F32, FP8, MT, 4, U4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes,
+                                                        st);
+  if (ACT == ACT_SILU_MUL || N >= 128 * 32)
+    return launch_skinny_cfg<ACT, F32, FP8, MT, 2, (MT >= 4 ? 4 : 8)>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias,
+                                                                              R, ldr, M, N, kbytes, st);
+  if constexpr (ACT != ACT_SILU_MUL)
+    return launch_skinny_cfg<ACT, F32, FP8, MT, 1, 8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes,
+                                                       st);
+  return -2;
 }
 
 template <int ACT, bool F32, bool FP8>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st) {
-  if constexpr (ACT == ACT_SILU_MUL)
-    return launch_skinny_nt<ACT, F32, FP8, 2>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
-  else
-    return launch_skinny_nt<ACT, F32, FP8, 1>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
+  if (M <= 16)
+    return launch_skinny_mt<ACT, F32, FP8, 1, 8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
+  if (M <= 32)
+    return launch_skinny_mt<ACT, F32, FP8, 2, 4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
+  return launch_skinny_mt<ACT, F32, FP8, 4, 4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
 }
 
 // bf16: K % 32 == 0 (64-B chunks), M <= 64.  fp8: K (bytes) % 64 == 0.
@@ -194,7 +211,7 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
   const int eb = fp8 ? 1 : 2;
   const int kbytes = K * eb;
   if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
-  if (act == ACT_SILU_MUL && N % 32 != 0) return -1;
+  if (act == ACT_SILU_MUL && N % 32 != 0) return -1;  // packed gate|up groups of 32
   if (fp8 && (sa == nullptr || sw == nullptr)) return -1;
   const int la = lda * eb, lw = ldw * eb;
 #define SKD(a)                                                                                              \

@@ -21,11 +21,23 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x,
   const bf16_t* xr = x + (size_t)row * ldx;
   float v[NC][8];
   float s = 0.f;
+  // gamma/beta are issued together with the row (one memory round trip before
+  // the reductions instead of a dependent second one after them)
+  constexpr bool PF = NC <= 8;
+  f32x4 wpf[PF ? NC : 1][2], bpf[PF ? NC : 1][2];
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = (lane + 64 * i) * 8;
     if (c < N) {
       const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+      if constexpr (PF) {
+        wpf[i][0] = *reinterpret_cast<const f32x4*>(w + c);
+        wpf[i][1] = *reinterpret_cast<const f32x4*>(w + c + 4);
+        if (!RMS && b != nullptr) {
+          bpf[i][0] = *reinterpret_cast<const f32x4*>(b + c);
+          bpf[i][1] = *reinterpret_cast<const f32x4*>(b + c + 4);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
     } else {
@@ -50,13 +62,21 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x,
   for (int i = 0; i < NC; ++i) {
     const int c = (lane + 64 * i) * 8;
     if (c < N) {
-      const float4 w0 = *reinterpret_cast<const float4*>(w + c), w1 = *reinterpret_cast<const float4*>(w + c + 4);
-      const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (!RMS && b != nullptr) {
-        const float4 b0 = *reinterpret_cast<const float4*>(b + c), b1 = *reinterpret_cast<const float4*>(b + c + 4);
-        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+      f32x4 w0, w1, b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+      if constexpr (PF) {
+        w0 = wpf[i][0];
+        w1 = wpf[i][1];
+        if (!RMS && b != nullptr) { b0 = bpf[i][0]; b1 = bpf[i][1]; }
+      } else {
+        w0 = *reinterpret_cast<const f32x4*>(w + c);
+        w1 = *reinterpret_cast<const f32x4*>(w + c + 4);
+        if (!RMS && b != nullptr) {
+          b0 = *reinterpret_cast<const f32x4*>(b + c);
+          b1 = *reinterpret_cast<const f32x4*>(b + c + 4);
+        }
       }
+      const float ww[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+      const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
       uint4 o;
       uint32_t* op = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll

@@ -51,9 +51,141 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const void* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stochastic sampler: temperature + top-k via the Gumbel-max trick
+//   token = argmax_{i in topk} ( x_i / T + G_i ),  G_i = -log(-log(U_i))
+// which draws exactly from softmax(x / T) restricted to the k largest logits.
+// One 1024-thread workgroup per row keeps the whole bf16 row in VGPRs (NV x 16 B
+// per lane: 128K-entry vocabularies fit), finds the k-th largest logit by a
+// 16-step bisection over the order-preserving 16-bit key (block-wide counts,
+// no atomics), then takes the Gumbel-max over the survivors.  U_i is a
+// counter-based hash of (seed, row, step[row], i): no RNG state, so one captured
+// HIP graph serves every decode step (step = the row's position, in device
+// memory) and the result is reproducible.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bf16_key(short v) {
+  const uint32_t u = (uint16_t)v;
+  return (u & 0x8000u) ? (~u & 0xFFFFu) : (u | 0x8000u);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float key_to_f(uint32_t k) {
+  const uint32_t u = (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu);
+  return __uint_as_float(u << 16);
+}
+
+template <int NV, int TH>
+__global__ __launch_bounds__(TH) void sample_topk_kernel(const bf16_t* __restrict__ x, int ld, int M, int N,
+                                                           int* __restrict__ out, float inv_temp, int topk,
+                                                           uint32_t seed, const int* __restrict__ step) {
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16_t* xr = x + (size_t)row * ld;
+  // the row lives in VGPRs as packed 16-bit order-preserving keys (2 per dword)
+  uint32_t kw[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i0 = (tid + TH * j) * 8;
+    bf16x8 p;
+    if (i0 + 8 <= N) {
+      p = *reinterpret_cast<const bf16x8*>(xr + i0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) p[e] = (short)(i0 + e < N ? xr[i0 + e] : (bf16_t)0xFF80u);  // -inf pad
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kw[j][e] = bf16_key(p[2 * e]) | (bf16_key(p[2 * e + 1]) << 16);
+  }
+  __shared__ int red[16];
+  __shared__ float bv[16];
+  __shared__ int bi_s[16];
+  uint32_t thr = 0;
+  if (topk > 0 && topk < N) {
+    for (int bit = 15; bit >= 0; --bit) {
+      const uint32_t cand = thr | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t w = kw[j][e];
+          asm volatile("" : "+v"(w));  // keep the unpack inside the loop (no hoisted 2x copy)
+          c += ((w & 0xFFFFu) >= cand ? 1 : 0) + ((w >> 16) >= cand ? 1 : 0);
+        }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0) red[wave] = c;
+      __syncthreads();
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < TH / 64; ++w) tot += red[w];
+      __syncthreads();
+      if (tot >= topk) thr = cand;
+    }
+  }
+  const uint32_t st = step != nullptr ? (uint32_t)step[row] : 0u;
+  const uint32_t base = mix32(seed ^ mix32((uint32_t)row * 0x9E3779B9u ^ mix32(st + 0x632BE5ABu)));
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = (tid + TH * j) * 8 + e;
+      const uint32_t k = (kw[j][e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+      if (i < N && k >= thr) {
+        const uint32_t h = mix32(base ^ (uint32_t)i * 0x85EBCA6Bu);
+        const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+        const float sc = key_to_f(k) * inv_temp - __logf(-__logf(u));
+        if (sc > best) { best = sc; bi = i; }
+      }
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if (lane == 0) { bv[wave] = best; bi_s[wave] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < TH / 64; ++w)
+      if (bv[w] > best || (bv[w] == best && bi_s[w] < bi)) { best = bv[w]; bi = bi_s[w]; }
+    out[row] = bi == 0x7fffffff ? 0 : bi;
+  }
+}
+
 }  // namespace dnn
 
 using namespace dnn;
+
+extern "C" int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float temperature, int topk,
+                               unsigned seed, const int* step, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (!(temperature > 0.f) || (ld % 8) != 0) return -1;
+  const int nv = (N + 8 * 1024 - 1) / (8 * 1024);
+  const float it = 1.f / temperature;
+#define SAMP(NVV, THV)                                                                                               \
+  {                                                                                                                  \
+    hipLaunchKernelGGL((sample_topk_kernel<NVV, THV>), dim3(M), dim3(THV), 0, st, (const bf16_t*)x, ld, M, N, out, it, \
+                       topk, (uint32_t)seed, step);                                                                  \
+    return (int)hipGetLastError();                                                                                   \
+  }
+  // <= 64K entries: 1024 threads, <= 8 vectors each; larger vocabularies (Llama-3
+  // 128K): 512 threads x 32 vectors (128 key VGPRs of a 256 budget)
+  if (nv <= 1) SAMP(1, 1024)
+  if (nv <= 2) SAMP(2, 1024)
+  if (nv <= 4) SAMP(4, 1024)
+  if (nv <= 8) SAMP(8, 1024)
+  if (nv <= 16) SAMP(32, 512)
+#undef SAMP
+  return -2;  // vocabulary > 128K entries
+}
 
 extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st) {
   if (M <= 0) return 0;

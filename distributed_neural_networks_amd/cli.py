@@ -140,9 +140,11 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
             st = CifarHipStage(sd, a, b, device)
         else:
             from .runtime.transformer import build_device_stage
-            st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype)
+            st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
+                                    temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed)
     else:
-        st = TorchStage(pipe.model, sd, a, b, first, last, device)
+        st = TorchStage(pipe.model, sd, a, b, first, last, device,
+                        sampling=(pipe.temperature, pipe.top_k, pipe.seed))
     log(f"[{ctx.node_id}] Successfully loaded weights into stage {part} (layers [{a},{b}]) on {device}.")
     return st, full_sd
 
@@ -282,9 +284,6 @@ def run_colocated(ctx: NodeContext, args, device) -> int:
     if fam != "cifar":
         from .runtime.transformer import run_generate_colocated
         return run_generate_colocated(ctx, args, stages, device)
-    if device.type == "cuda" and ctx.num_parts == 2:
-        # merge the reference split into one fused stage pair on the device
-        pass
     for r in range(args.num_requests):
         x = load_image(args.input_image, nid)
         pipe = ColocatedPipeline(stages, x.shape[0])

@@ -77,11 +77,11 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
 
 def decode_splits(S: int, B: int, Hkv: int) -> int:
     """Split-K factor for decode attention: enough workgroups for ~4 per CU
-    (1024), at most one split per 64 keys of cache capacity.  Each split takes
+    (1024), at most one split per 256 keys of cache capacity.  Each split takes
     ``ceil(len/splits)`` of the *runtime* length, so short contexts stay
     balanced; with one split the kernel writes the output itself (no combine)."""
     want = max(1, -(-1024 // max(1, B * Hkv)))
-    return max(1, min(want, -(-S // 64)))
+    return max(1, min(want, -(-S // 256)))  # >= 256 keys per split: short contexts skip the combine pass
 
 
 def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, H: int, Hkv: int,
@@ -102,4 +102,19 @@ def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> 
     N = n if n is not None else x.shape[1]
     check(lib().argmax_rows(ptr(x), x.stride(0), M, N, ptr(out), 1 if x.dtype == torch.float32 else 0,
                             stream_ptr()), "argmax_rows")
+    return out
+
+
+def sample_topk(logits: torch.Tensor, out: torch.Tensor, n: int, temperature: float, top_k: int = 0, seed: int = 0,
+                step: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Temperature / top-k sampling per row (Gumbel-max over the k largest
+    logits), bf16 logits only.  ``step`` (device int32 per row, e.g. the
+    sequence position) decorrelates successive decode steps inside one graph."""
+    if logits.dtype != torch.bfloat16:
+        raise TypeError("sample_topk: bf16 logits expected")
+    if not temperature > 0:
+        raise ValueError("sample_topk: temperature must be > 0 (use argmax_rows for greedy)")
+    M = logits.shape[0]
+    check(lib().sample_topk(ptr(logits), logits.stride(0), M, n, ptr(out), float(temperature), int(top_k),
+                            int(seed) & 0xFFFFFFFF, ptr(step), stream_ptr()), "sample_topk")
     return out

@@ -118,8 +118,9 @@ class TorchStage(StageCompute):
     """Golden torch module as a stage (CPU fp32 plumbing path / tests)."""
 
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
-                 device="cpu", dtype=torch.float32):
+                 device="cpu", dtype=torch.float32, sampling=(0.0, 0, 0)):
         from ..models import build_golden_stage
+        self.temperature, self.top_k, self.seed = float(sampling[0]), int(sampling[1]), int(sampling[2])
         self.model, self.start, self.end, self.first, self.last = model, start, end, first, last
         self.device = torch.device(device)
         self.family = model_info(model).family
@@ -173,8 +174,10 @@ class TorchStage(StageCompute):
             h = x.view(B, T, cfg.n_embd).to(self.dtype)
         y = self.module(h, self._kv, p, last_only=last_only)
         if self.last:
+            from .sampling import pick
             logits = y[:, -1, :] if last_only else y.reshape(B * T, -1)
-            return StageOutput(logits, y[:, -1, :].argmax(dim=-1).to(torch.int32))
+            step = pos if isinstance(pos, torch.Tensor) else torch.full((B,), p, dtype=torch.int32)
+            return StageOutput(logits, pick(y[:, -1, :], self.temperature, self.top_k, self.seed, step))
         return y.reshape(B * T, cfg.n_embd)
 
     @torch.no_grad()

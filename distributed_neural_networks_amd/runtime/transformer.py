@@ -60,8 +60,11 @@ class LayerW:
 class TransformerStage(StageCompute):
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
                  device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
-                 fp8: bool = False):
+                 fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0):
         info = model_info(model)
+        # sampling (last stage): temperature 0 = greedy argmax; otherwise
+        # Gumbel-max over the top_k logits (0 = all), seeded per (row, position)
+        self.temperature, self.top_k, self.seed = float(temperature), int(top_k), int(seed)
         self.model, self.family, self.cfg = model, info.family, info.cfg
         self.start, self.end, self.first, self.last = start, end, first, last
         self.device = dev = torch.device(device)
@@ -229,7 +232,10 @@ class TransformerStage(StageCompute):
         else:
             linear(lnf, self.w_head, None, out=logits[:, :self.V])
         nxt = self.next_ids[:rows]
-        T_.argmax_rows(logits, nxt, n=self.V)
+        if self.temperature > 0 and last_only:
+            T_.sample_topk(logits, nxt, self.V, self.temperature, self.top_k, self.seed, step=pos)
+        else:
+            T_.argmax_rows(logits, nxt, n=self.V)
         if last_only and out is not None:
             out.copy_(nxt)
         return StageOutput(logits[:, :self.V], nxt)
@@ -244,11 +250,13 @@ class TransformerStage(StageCompute):
 
 
 def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
-                       max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None):
+                       max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
+                       temperature: float = 0.0, top_k: int = 0, seed: int = 0):
     fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
     info = model_info(model)
     max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))
-    return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8)
+    return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8,
+                            temperature, top_k, seed)
 
 
 # ---------------------------------------------------------------------- drivers
