@@ -33,6 +33,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_skinny(CP(A), lda, CFP(sa), CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act,
                            out_f32, fp8, ST(st));
   });
+  m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, int M, int N, int K, int nt, int u,
+                                int ks, int pipe, u64 st) {
+    return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, P(C), ldc, M, N, K, nt, u, ks, pipe, ST(st));
+  });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
   m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {
     return dnn_silu_mul_packed(CP(gu), ld_in, P(out), ld_out, M, F, ST(st));

@@ -294,8 +294,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
-#pragma unroll
-        for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        d = group_sum<LPK>(d);  // DPP row reduction over the LPK lanes of this key
         if (sub == 0 && kk < n) sc[g * chunk_cap + kk] = d * scale_log2;
       }
     }

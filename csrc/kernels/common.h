@@ -31,16 +31,40 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// DPP lane moves (VALU, no LDS round trip — __shfl_xor lowers to
+// ds_bpermute_b32 on gfx950): quad_perm xor1 / xor2, row_half_mirror (lane i
+// <-> 7-i within 8), row_mirror (i <-> 15-i within 16).  For a reduction any
+// pairing of the two halves works, so these four steps reduce a 16-lane row.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum / max over aligned groups of L lanes (L = 1..64); every lane of the group
+// gets the result.
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (L >= 2) v += dpp_f<0xB1>(v);
+  if constexpr (L >= 4) v += dpp_f<0x4E>(v);
+  if constexpr (L >= 8) v += dpp_f<0x141>(v);
+  if constexpr (L >= 16) v += dpp_f<0x140>(v);
+  if constexpr (L >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (L >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+template <int L>
+__device__ __forceinline__ float group_max(float v) {
+  if constexpr (L >= 2) v = fmaxf(v, dpp_f<0xB1>(v));
+  if constexpr (L >= 4) v = fmaxf(v, dpp_f<0x4E>(v));
+  if constexpr (L >= 8) v = fmaxf(v, dpp_f<0x141>(v));
+  if constexpr (L >= 16) v = fmaxf(v, dpp_f<0x140>(v));
+  if constexpr (L >= 32) v = fmaxf(v, __shfl_xor(v, 16, 64));
+  if constexpr (L >= 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
+
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+__device__ __forceinline__ float wave_max(float v) { return group_max<64>(v); }
 
 // 16-byte async global->LDS copy. `lds_wave_base` must be wave-uniform: lane i
 // lands at lds_wave_base + 16*i (glds semantics, cdna_hip_programming.md §5).

@@ -120,11 +120,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     if (ACT == ACT_SILU_MUL) {
-      // packed gate|up: n-tile j even = gate, j+1 = the matching up columns
 #pragma unroll
-      for (int j = 0; j < 4; j += 2)
-        epi_silu_t4<OUT_F32>(acc[i][j], acc[i][j + 1], m, (n0 + wn * 64 + j * 16) / 2 + (lane >> 4) * 4, M, N / 2,
-                             Cv, ldc, vec);
+      for (int j = 0; j < 4; ++j)
+        epi_silu_t4<OUT_F32>(acc[i][j], m, (n0 + wn * 64 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -295,8 +293,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
         const int nb = n0 + nq * 128 + wc * 32;
         if (ACT == ACT_SILU_MUL) {
-          epi_silu_t4<OUT_F32>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb / 2 + (lane >> 4) * 4, M, N / 2, Cv, ldc,
-                               vec);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            epi_silu_t4<OUT_F32>(acc[mq][nq][i][j], m, (nb + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
         } else {
 #pragma unroll
           for (int j = 0; j < 2; ++j)

@@ -61,16 +61,23 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
   }
 }
 
-// SwiGLU epilogue on transposed accumulators: g = gate columns, u = the matching
-// up columns (packed gate|up weights, ops/gemm.py pack_gate_up); output columns
-// ncol..ncol+3 of a [M, N/2] result.
+// SwiGLU epilogue on a transposed accumulator tile of the packed gate|up
+// weight (ops/gemm.py pack_gate_up: 8 gate rows, then the 8 matching up rows):
+// lanes 0-31 hold gate columns, lanes 32-63 the up columns of the same outputs,
+// so one xor-32 shuffle pairs them; lanes 0-31 write output columns
+// ncol0 + 4*(lane>>4) .. +3 of the [M, N/2] result.  Every lane must call this
+// (the shuffle), whatever its row.
 template <bool OUT_F32>
-__device__ __forceinline__ void epi_silu_t4(const f32x4& g, const f32x4& u, int m, int ncol, int M, int NO,
-                                            void* __restrict__ Cv, int ldc, bool vec) {
-  if (m >= M) return;
+__device__ __forceinline__ void epi_silu_t4(const f32x4& acc, int m, int ncol0, int M, int NO, void* __restrict__ Cv,
+                                            int ldc, bool vec, int lane) {
+  f32x4 other;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) other[r] = __shfl_xor(acc[r], 32, 64);
+  if (lane >= 32 || m >= M) return;
+  const int ncol = ncol0 + (lane >> 4) * 4;
   f32x4 v;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = silu(g[r]) * u[r];
+  for (int r = 0; r < 4; ++r) v[r] = silu(acc[r]) * other[r];
   if (vec && ncol + 3 < NO) {
     if (OUT_F32) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + ncol) = v;

@@ -42,7 +42,7 @@ __device__ __forceinline__ f32x4 sk_mma(const i32x4& w, const i32x4& a, f32x4 ac
   }
 }
 
-template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U>
+template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                            const float* __restrict__ sa, const uint8_t* __restrict__ W,
                                                            int ldw_b, const float* __restrict__ sw,
@@ -78,34 +78,62 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   const int nch = kbytes >> 6;
   const int per = (nch + KS - 1) / KS;
   const int c0 = wave * per, c1 = min(nch, c0 + per);
-  int c = c0;
-  for (; c + U <= c1; c += U) {
-    i32x4 wv[NT][U], av[MT][U];
+  // Batches of U chunks; the last batch of a wave is partial: its loads are
+  // clamped in-bounds and the surplus chunks' weights zeroed, so every batch
+  // (including short K slices) issues all of its loads at once.
+  auto load = [&](int cc, i32x4(&wv)[NT][U], i32x4(&av)[MT][U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      const int ci = min(cc + u, c1 - 1);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) wv[j][u] = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)(c + u) * 64);
+      for (int j = 0; j < NT; ++j) wv[j][u] = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)ci * 64);
+    }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      const int ci = min(cc + u, c1 - 1);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) av[t][u] = *reinterpret_cast<const i32x4*>(ap[t] + (size_t)(c + u) * 64);
-    // keep every load of the batch ahead of the first MFMA (the scheduler would
-    // otherwise interleave them and wait vmcnt(0) per chunk: 1-2 loads in flight)
+      for (int t = 0; t < MT; ++t) av[t][u] = *reinterpret_cast<const i32x4*>(ap[t] + (size_t)ci * 64);
+    }
+    // keep every load of the batch ahead of the MFMAs that follow (the scheduler
+    // would otherwise interleave them and wait vmcnt(0) per chunk)
     __builtin_amdgcn_sched_barrier(0);
+  };
+  auto comp = [&](int cc, i32x4(&wv)[NT][U], const i32x4(&av)[MT][U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      if (cc + u >= c1) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wv[j][u] = i32x4{0, 0, 0, 0};
+      }
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[j][t] = sk_mma<FP8>(wv[j][u], av[t][u], acc[j][t]);
-  }
-  for (; c < c1; ++c) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const i32x4 w = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)c * 64);
-#pragma unroll
-      for (int t = 0; t < MT; ++t)
-        acc[j][t] = sk_mma<FP8>(w, *reinterpret_cast<const i32x4*>(ap[t] + (size_t)c * 64), acc[j][t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int nb = c1 > c0 ? (c1 - c0 + U - 1) / U : 0;
+  int c = c0;
+  if constexpr (PIPE) {
+    // software pipeline: the next batch is in flight while this one computes
+    if (nb > 0) {
+      i32x4 w0[NT][U], a0[MT][U], w1[NT][U], a1[MT][U];
+      load(c, w0, a0);
+      int b = 0;
+      for (; b + 2 <= nb; b += 2) {
+        load(c + U, w1, a1);
+        comp(c, w0, a0);
+        if (b + 2 < nb) load(c + 2 * U, w0, a0);
+        comp(c + U, w1, a1);
+        c += 2 * U;
+      }
+      if (b < nb) comp(c, w0, a0);
+    }
+  } else {
+    for (int b = 0; b < nb; ++b, c += U) {
+      i32x4 wv[NT][U], av[MT][U];
+      load(c, wv, av);
+      comp(c, wv, av);
     }
   }
 #pragma unroll
@@ -126,18 +154,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     const int m = t * 16 + (lane & 15);
     const float rs = (FP8 && m < M) ? sa[m] : 1.f;
     if constexpr (ACT == ACT_SILU_MUL) {
-      static_assert(NT % 2 == 0, "SwiGLU needs gate/up tile pairs");
 #pragma unroll
-      for (int jp = 0; jp < NT; jp += 2) {
+      for (int j = 0; j < NT; ++j) {
         if constexpr (FP8) {
-          const int ng = n0 + jp * 16 + (lane >> 4) * 4, nu = ng + 16;
+          const int n = n0 + j * 16 + (lane >> 4) * 4;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[jp][r] *= rs * (ng + r < N ? sw[ng + r] : 0.f);
-            s[jp + 1][r] *= rs * (nu + r < N ? sw[nu + r] : 0.f);
-          }
+          for (int r = 0; r < 4; ++r) s[j][r] *= rs * (n + r < N ? sw[n + r] : 0.f);
         }
-        epi_silu_t4<OUT_F32>(s[jp], s[jp + 1], m, (n0 + jp * 16) / 2 + (lane >> 4) * 4, M, N / 2, Cv, ldc, vec);
+        epi_silu_t4<OUT_F32>(s[j], m, (n0 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
       }
     } else {
 #pragma unroll
@@ -152,56 +176,51 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 
 using namespace dnn;
 
-// Waves per workgroup: enough workgroups x waves to cover the 256 CUs (x4 SIMDs)
-// while every wave keeps >= 2 chunks of K.
-static int skinny_ks(int groups, int nch) {
-  int ks = groups <= 256 ? 8 : 4;
-  while (ks > 1 && nch / ks < 2) ks >>= 1;
-  return ks;
-}
-
 // Per chunk a wave issues NT weight loads and MT activation loads (L2) for
-// NT x MT MFMAs: NT grows with MT so the activation re-reads stay <= the
-// weight bytes.  U = chunks in flight, sized for <= 256 VGPRs at 8 waves/WG.
-template <int ACT, bool F32, bool FP8, int MT, int NT, int U>
+// NT x MT MFMAs.  The configuration table below is fitted to
+// bench/skinny_sweep.py on MI355X (profiles/r1_skinny_sweep.jsonl, weights
+// rotated past the 256 MB MALL):
+//   M <= 8     : 1 tile, 4 chunks in flight, 8 waves/WG (within 3% of the best
+//                config on every Llama-3 / GPT-2 XL shape)
+//   M <= 64    : wide N (>= 16K, the FFN and the LM head): 4 tiles x 2 chunks,
+//                2 waves; K >= 8K: 1 tile x 8 chunks, 2 waves; otherwise 2 tiles
+//                x 2 chunks, 4 waves (activation re-reads dominate as M grows)
+template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                             hipStream_t st) {
+                             int ks, hipStream_t st) {
   const int groups = (N + 16 * NT - 1) / (16 * NT);
-  const int ks = skinny_ks(groups, kbytes / 64);
+  while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
   const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U>), dim3(groups), dim3(64 * ks), smem, st,
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE>), dim3(groups), dim3(64 * ks), smem, st,
                      (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R, ldr,
                      M, N, kbytes);
   return (int)hipGetLastError();
-}
-
-template <int ACT, bool F32, bool FP8, int MT, int U4>
-static int launch_skinny_mt(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
-                            void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                            hipStream_t st) {
-  // widest column tile that still leaves >= 128 workgroups (small N: latency-bound, keep the waves)
-  if (N >= 128 * 64)
-    return launch_skinny_cfg<ACT, F32, FP8, MT, 4, U4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes,
-                                                        st);
-  if (ACT == ACT_SILU_MUL || N >= 128 * 32)
-    return launch_skinny_cfg<ACT, F32, FP8, MT, 2, (MT >= 4 ? 4 : 8)>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias,
-                                                                              R, ldr, M, N, kbytes, st);
-  if constexpr (ACT != ACT_SILU_MUL)
-    return launch_skinny_cfg<ACT, F32, FP8, MT, 1, 8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes,
-                                                       st);
-  return -2;
 }
 
 template <int ACT, bool F32, bool FP8>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st) {
-  if (M <= 16)
-    return launch_skinny_mt<ACT, F32, FP8, 1, 8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
-  if (M <= 32)
-    return launch_skinny_mt<ACT, F32, FP8, 2, 4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
-  return launch_skinny_mt<ACT, F32, FP8, 4, 4>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);
+  const bool wide = N >= 16384;
+  const bool deep = kbytes >= 16384;  // K >= 8K bf16
+#define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
+  return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, \
+                                                             kbytes, KSV, st)
+  if (M <= 8) CFG(1, 1, 4, false, 8);
+  if (M <= 16) {
+    if (wide) CFG(1, 4, 2, false, 2);
+    CFG(1, 2, 2, true, 4);
+  }
+  if (M <= 32) {
+    if (wide) CFG(2, 4, 2, false, 2);
+    if (deep) CFG(2, 1, 8, false, 2);
+    CFG(2, 2, 2, false, 4);
+  }
+  if (wide) CFG(4, 4, 2, false, 2);
+  if (deep) CFG(4, 1, 8, false, 2);
+  CFG(4, 2, 2, false, 4);
+#undef CFG
 }
 
 // bf16: K % 32 == 0 (64-B chunks), M <= 64.  fp8: K (bytes) % 64 == 0.
@@ -211,7 +230,7 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
   const int eb = fp8 ? 1 : 2;
   const int kbytes = K * eb;
   if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
-  if (act == ACT_SILU_MUL && N % 32 != 0) return -1;  // packed gate|up groups of 32
+  if (act == ACT_SILU_MUL && N % 16 != 0) return -1;  // packed gate|up groups of 8+8
   if (fp8 && (sa == nullptr || sw == nullptr)) return -1;
   const int la = lda * eb, lw = ldw * eb;
 #define SKD(a)                                                                                              \
@@ -229,4 +248,37 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
   SKD(ACT_SILU_MUL)
 #undef SKD
   return -2;
+}
+
+// Configuration sweep for bench/gemm_bench.py --skinny (bf16, no epilogue ops):
+// nt in {1,2,4}, u in {2,4,8}, pipe in {0,1}; ks = waves per workgroup.
+template <int MT, int NT, int U, bool PIPE>
+static int skinny_sweep_launch(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                               int ks, hipStream_t st) {
+  const int groups = (N + 16 * NT - 1) / (16 * NT);
+  const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE>), dim3(groups), dim3(64 * ks), smem,
+                     st, (const uint8_t*)A, lda * 2, nullptr, (const uint8_t*)W, ldw * 2, nullptr, C, ldc, nullptr,
+                     nullptr, 0, M, N, K * 2);
+  return (int)hipGetLastError();
+}
+
+template <int MT>
+static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                           int nt, int u, int ks, int pipe, hipStream_t st) {
+#define SW(NTV, UV)                                                                                     \
+  if (nt == NTV && u == UV)                                                                             \
+    return pipe ? skinny_sweep_launch<MT, NTV, UV, true>(A, lda, W, ldw, C, ldc, M, N, K, ks, st)      \
+                : skinny_sweep_launch<MT, NTV, UV, false>(A, lda, W, ldw, C, ldc, M, N, K, ks, st);
+  SW(1, 2) SW(1, 4) SW(1, 8) SW(2, 2) SW(2, 4) SW(2, 8) SW(4, 2) SW(4, 4)
+#undef SW
+  return -2;
+}
+
+extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N,
+                                     int K, int nt, int u, int ks, int pipe, hipStream_t st) {
+  if (M <= 0 || M > 64 || (K * 2) % 64 != 0 || ks < 1 || ks > 8) return -1;
+  if (M <= 16) return skinny_sweep_mt<1>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+  if (M <= 32) return skinny_sweep_mt<2>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+  return skinny_sweep_mt<4>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
 }

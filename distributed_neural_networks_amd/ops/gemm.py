@@ -52,11 +52,13 @@ def set_gemm_tile(tile: int = 0) -> None:
 
 
 def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
-    """Interleave gate/up rows in 16-row groups: [g0..g15, u0..u15, g16..g31, ...]
-    so the GEMM epilogue sees matching gate/up columns in one lane (ACT_SILU_MUL)."""
+    """Interleave gate/up rows in 8-row groups: [g0..g7, u0..u7, g8..g15, ...]
+    so every 16-column MFMA tile holds 8 gate and the 8 matching up columns
+    (lane groups 0-1 vs 2-3 of the transposed accumulator): the ACT_SILU_MUL
+    epilogue pairs them with one cross-half lane shuffle, at any tile width."""
     F, K = gate.shape
-    if F % 16:
-        raise ValueError("ffn dim must be a multiple of 16")
-    g = gate.reshape(F // 16, 16, K)
-    u = up.reshape(F // 16, 16, K)
+    if F % 8:
+        raise ValueError("ffn dim must be a multiple of 8")
+    g = gate.reshape(F // 8, 8, K)
+    u = up.reshape(F // 8, 8, K)
     return torch.stack([g, u], dim=1).reshape(2 * F, K).contiguous()
