@@ -33,6 +33,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_skinny(CP(A), lda, CFP(sa), CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act,
                            out_f32, fp8, ST(st));
   });
+  m.def("gemm_skinny_norm", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M,
+                               int N, int K, int act, int norm, u64 colsum, float eps, u64 st) {
+    return dnn_gemm_skinny_norm(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, norm,
+                                CFP(colsum), eps, ST(st));
+  });
   m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, int M, int N, int K, int nt, int u,
                                 int ks, int pipe, u64 st) {
     return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, P(C), ldc, M, N, K, nt, u, ks, pipe, ST(st));
@@ -77,6 +82,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("attn_decode", [](u64 q, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S, u64 lens,
                           float scale, int splits, u64 ws, u64 st) {
     return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st));
+  });
+  m.def("attn_decode_qkv", [](u64 qkv, int ldqkv, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S,
+                              u64 pos, u64 cos, u64 sin, float scale, int splits, u64 ws, u64 st) {
+    return dnn_attn_decode_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, H, Hkv, hd, S, CIP(pos), CFP(cos), CFP(sin),
+                               scale, splits, FP(ws), ST(st));
   });
   m.def("sample_topk", [](u64 x, int ld, int M, int N, u64 out, float temperature, int topk, unsigned seed, u64 step,
                           u64 st) {

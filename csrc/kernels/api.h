@@ -9,6 +9,9 @@ int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int l
 int dnn_gemm_set_tile(int tile);
 int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K, int nt,
                           int u, int ks, int pipe, hipStream_t st);
+int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
+                         const void* R, int ldr, int M, int N, int K, int act, int norm, const float* colsum, float eps,
+                         hipStream_t st);
 int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw, void* C, int ldc,
                     const float* bias, const void* R, int ldr, int M, int N, int K, int act, int out_f32, int fp8,
                     hipStream_t st);
@@ -31,6 +34,9 @@ int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, in
                   const int* pos, const float* cos, const float* sin, int rope, hipStream_t st);
 int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv, int hd, int S,
                    const int* pos, float scale, hipStream_t st);
+int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd, int S,
+                        const int* pos, const float* cosT, const float* sinT, float scale, int splits, float* ws,
+                        hipStream_t st);
 int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd, int S,
                     const int* lens, float scale, int splits, float* ws, hipStream_t st);
 int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float temperature, int topk, unsigned seed,

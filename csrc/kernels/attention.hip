@@ -239,17 +239,53 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
 constexpr int DEC_MAXG = 8;
 constexpr int DEC_U = 8;  // key/value rows in flight per thread
 
-template <int HD, int G>
-__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
-                                                          const bf16_t* __restrict__ vc, float* __restrict__ ws, int H,
-                                                          int Hkv, int S, const int* __restrict__ lens, float scale_log2,
+// 8 consecutive head-dim elements [8*sub, 8*sub+8) of one head row, RoPE'd
+// (rotate-half: element i pairs with i +- hd/2) when cosT != nullptr, and
+// rounded to bf16 exactly as qkv_split stores them.
+template <int HD>
+__device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int sub, const float* __restrict__ cosT,
+                                           const float* __restrict__ sinT, int p, float out[8]) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(row + sub * 8);
+  if (cosT == nullptr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = bf2f_s(x[j]);
+    return;
+  }
+  constexpr int HALFC = HD / 16;  // 16-B chunks per half row
+  const bool lo = sub < HALFC;
+  const int psub = lo ? sub + HALFC : sub - HALFC;
+  const bf16x8 y = *reinterpret_cast<const bf16x8*>(row + psub * 8);
+  const int i0 = (lo ? sub : psub) * 8;
+  const float* cr = cosT + (size_t)p * (HD / 2) + i0;
+  const float* sr = sinT + (size_t)p * (HD / 2) + i0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float a = bf2f_s(x[j]), c = bf2f_s(y[j]);
+    const float r = lo ? a * cr[j] - c * sr[j] : a * cr[j] + c * sr[j];
+    out[j] = bf2f(f2bf(r));
+  }
+}
+
+// FUSED (decode steps): q, the new key (RoPE'd) and value are read straight
+// from the QKV projection row of each sequence, the key count is pos[b] + 1,
+// and the workgroup whose split holds the new position writes it into the
+// cache; its own scores use the register copy, so no other split touches that
+// row and there is no qkv_split launch.  Otherwise q is head-major (B,H,hd)
+// and lens[b] keys are cached.
+template <int HD, int G, bool FUSED>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                          bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                          float* __restrict__ ws, int H, int Hkv, int S,
+                                                          const int* __restrict__ lens, const float* __restrict__ cosT,
+                                                          const float* __restrict__ sinT, float scale_log2,
                                                           int chunk_cap, bf16_t* __restrict__ o_direct) {
   constexpr int LPK = HD / 8;           // lanes per key row (16 B each)
   constexpr int GPB = 256 / LPK;        // key groups per block
   extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk_cap] scores, then reduction scratch
   const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
   const int b = bk / Hkv, kvh = bk % Hkv;
-  const int len = min(lens[b], S);  // never read past the cache capacity
+  const int p_new = FUSED ? lens[b] : 0;  // FUSED: lens = positions already cached
+  const int len = FUSED ? min(p_new + 1, S) : min(lens[b], S);  // never read past the cache capacity
   // splits share the *runtime* length evenly (one captured graph serves every step)
   const int chunk = (len + NS - 1) / NS;
   const int k0 = split * chunk, k1 = min(len, k0 + chunk);
@@ -262,15 +298,42 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     }
     return;
   }
-  const bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD;
-  const bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD;
+  bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD;
+  bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD;
   float qv[G][8];
+  float nk[8], nv[8];
+  // FUSED: is the new key inside this split (and inside the cache)?
+  const bool own_new = FUSED && p_new < S && p_new >= k0 && p_new < k1;
+  if constexpr (FUSED) {
+    const bf16_t* row = q + (size_t)b * ldq;
+    const int pr = min(p_new, S - 1);  // RoPE table row (overflow is dropped, never read out of bounds)
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const bf16x8 p = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
+    for (int g = 0; g < G; ++g) load_head8<HD>(row + (kvh * G + g) * HD, sub, cosT, sinT, pr, qv[g]);
+    if (own_new) {
+      load_head8<HD>(row + (H + kvh) * HD, sub, cosT, sinT, pr, nk);
+      load_head8<HD>(row + (H + Hkv + kvh) * HD, sub, nullptr, nullptr, 0, nv);
+      if (grp == 0) {
+        uint4 wk, wv;
+        uint32_t* pk = reinterpret_cast<uint32_t*>(&wk);
+        uint32_t* pv = reinterpret_cast<uint32_t*>(&wv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) qv[g][j] = bf2f_s(p[j]);
+        for (int j = 0; j < 4; ++j) {
+          pk[j] = pack2bf(nk[2 * j], nk[2 * j + 1]);
+          pv[j] = pack2bf(nv[2 * j], nv[2 * j + 1]);
+        }
+        *reinterpret_cast<uint4*>(kb + (size_t)p_new * HD + sub * 8) = wk;
+        *reinterpret_cast<uint4*>(vb + (size_t)p_new * HD + sub * 8) = wv;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[g][j] = bf2f_s(pq[j]);
+    }
   }
+  const int knew = own_new ? p_new - k0 : -1;  // split-relative index of the register-held key
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
   // Scores: batches of DEC_U key rows per thread, all loads issued before the
@@ -289,6 +352,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       float kf[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) kf[j] = bf2f_s(kr[u][j]);
+      if (FUSED && kk == knew) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[j] = nk[j];
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
@@ -335,11 +402,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int u = 0; u < DEC_U; ++u) {
       const int kk = kb0 + u * GPB + grp;
       if (kk < n) {
+        float vf[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vf[j] = bf2f_s(vr[u][j]);
+        if (FUSED && kk == knew) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vf[j] = nv[j];
+        }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           const float pw = sc[g * chunk_cap + kk];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[g][j] += pw * bf2f_s(vr[u][j]);
+          for (int j = 0; j < 8; ++j) acc[g][j] += pw * vf[j];
         }
       }
     }
@@ -423,8 +497,9 @@ extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, voi
   return (int)hipGetLastError();
 }
 
-extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd,
-                               int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {
+static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd,
+                              int S, const int* lens, const float* cosT, const float* sinT, float scale, int splits,
+                              float* ws, bool fused, hipStream_t st) {
   const int G = H / Hkv;
   if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
   const int chunk_cap = (S + splits - 1) / splits;
@@ -433,14 +508,35 @@ extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, vo
   if (smem > 160 * 1024) return -3;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(B * Hkv, splits);
-#define DEC(HDV, GV)                                                                                               \
-  if (hd == HDV && G == GV) {                                                                                      \
-    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV>), grid, dim3(256), smem, st, (const bf16_t*)q, (const bf16_t*)kc, \
-                       (const bf16_t*)vc, ws, H, Hkv, S, lens, sl2, chunk_cap, (bf16_t*)o);                        \
+#define DEC(HDV, GV)                                                                                                  \
+  if (hd == HDV && G == GV) {                                                                                         \
+    if (fused)                                                                                                        \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, true>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,       \
+                         (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, chunk_cap, (bf16_t*)o);      \
+    else                                                                                                              \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, false>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,      \
+                         (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2, chunk_cap, (bf16_t*)o); \
   } else
   DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(128, 1) DEC(128, 2) DEC(128, 4) DEC(128, 8) { return -2; }
 #undef DEC
   if (splits > 1)
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
   return (int)hipGetLastError();
+}
+
+extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd,
+                               int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {
+  return attn_decode_launch(q, H * hd, const_cast<void*>(kc), const_cast<void*>(vc), o, B, H, Hkv, hd, S, lens,
+                            nullptr, nullptr, scale, splits, ws, false, st);
+}
+
+// Decode step straight from the QKV projection: qkv rows (B, ldqkv) laid out
+// [q H*hd | k Hkv*hd | v Hkv*hd]; pos[b] = tokens already cached.  RoPE when
+// cos/sin are given.  Writes the new k/v into the cache and the attention
+// output (B, H*hd).
+extern "C" int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int H, int Hkv,
+                                   int hd, int S, const int* pos, const float* cosT, const float* sinT, float scale,
+                                   int splits, float* ws, hipStream_t st) {
+  if (ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
+  return attn_decode_launch(qkv, ldqkv, kc, vc, o, B, H, Hkv, hd, S, pos, cosT, sinT, scale, splits, ws, true, st);
 }

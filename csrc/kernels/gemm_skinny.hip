@@ -15,6 +15,13 @@
 // transposed-accumulator one (gemm_epilogue.h): bias / act / residual / SwiGLU
 // (NT = 2: gate and up tile of the packed gate|up weight in one workgroup).
 //
+// Fused pre-norm (NORM = NORM_RMS / NORM_LN, bf16 only): the producing
+// LayerNorm/RMSNorm is folded into the weights on the host (ops/gemm.py
+// fold_norm: W' = W diag(gamma), bias' = W beta + bias, colsum[n] = sum_k W'[n,k])
+// and the row statistics are accumulated from the A fragments this kernel
+// streams anyway, so the norm kernel and its activation round trip disappear:
+//   y = rstd[m] * (A W'^T - mean[m] colsum) + bias'   (LN; RMS: no mean term).
+//
 // bf16: one v_mfma_f32_16x16x32_bf16 per 16-B chunk.  fp8 (OCP e4m3fn weights
 // and per-token-quantised activations, ops/fp8.py): two
 // v_mfma_f32_16x16x32_fp8_fp8 per chunk (the k order inside a chunk is the same
@@ -42,15 +49,29 @@ __device__ __forceinline__ f32x4 sk_mma(const i32x4& w, const i32x4& a, f32x4 ac
   }
 }
 
-template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false>
+enum SkNorm { NORM_NONE = 0, NORM_RMS = 1, NORM_LN = 2 };
+
+// Sum and sum of squares of the 8 bf16 of one A fragment.
+__device__ __forceinline__ void sk_stats(const i32x4& a, float& s1, float& s2) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float((uint32_t)a[i] << 16), hi = __uint_as_float((uint32_t)a[i] & 0xffff0000u);
+    s1 += lo + hi;
+    s2 = fmaf(lo, lo, fmaf(hi, hi, s2));
+  }
+}
+
+template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false, int NORM = NORM_NONE>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                            const float* __restrict__ sa, const uint8_t* __restrict__ W,
                                                            int ldw_b, const float* __restrict__ sw,
                                                            void* __restrict__ Cv, int ldc,
                                                            const float* __restrict__ bias,
                                                            const bf16_t* __restrict__ R, int ldr, int M, int N,
-                                                           int kbytes) {
-  extern __shared__ __attribute__((aligned(16))) f32x4 sk_red[];  // [KS][NT*MT][64]
+                                                           int kbytes, const float* __restrict__ colsum = nullptr,
+                                                           float eps = 0.f) {
+  static_assert(NORM == NORM_NONE || !FP8, "fused norm is bf16-only");
+  extern __shared__ __attribute__((aligned(16))) f32x4 sk_red[];  // [KS][NT*MT][64], then [KS][MT][16] x2 stats
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, KS = blockDim.x >> 6;
   const int n0 = blockIdx.x * (16 * NT);
   const int lg = (lane >> 4) * 16;  // byte offset of this lane group inside a 64-B chunk
@@ -74,6 +95,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float st1[MT], st2[MT];  // row statistics of this lane's A fragments (NORM)
+#pragma unroll
+  for (int t = 0; t < MT; ++t) st1[t] = st2[t] = 0.f;
 
   const int nch = kbytes >> 6;
   const int per = (nch + KS - 1) / KS;
@@ -104,6 +128,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
       if (cc + u >= c1) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) wv[j][u] = i32x4{0, 0, 0, 0};
+      } else if constexpr (NORM != NORM_NONE) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) sk_stats(av[t][u], st1[t], st2[t]);
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j)
@@ -140,6 +167,22 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int t = 0; t < MT; ++t) sk_red[(wave * NT * MT + j * MT + t) * 64 + lane] = acc[j][t];
+  float* sk_st = reinterpret_cast<float*>(sk_red + KS * NT * MT * 64);  // [KS][MT][2][16]
+  if constexpr (NORM != NORM_NONE) {
+    // the 4 lane groups hold disjoint 16-B pieces of the same 16 rows
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      float a = st1[t], q = st2[t];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        sk_st[((wave * MT + t) * 2 + 0) * 16 + lane] = a;
+        sk_st[((wave * MT + t) * 2 + 1) * 16 + lane] = q;
+      }
+    }
+  }
   __syncthreads();
 
   // reduction over the KS waves + epilogue: wave w finishes M tiles t = w, w+KS, ...
@@ -153,6 +196,27 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     }
     const int m = t * 16 + (lane & 15);
     const float rs = (FP8 && m < M) ? sa[m] : 1.f;
+    if constexpr (NORM != NORM_NONE) {
+      float a = 0.f, q = 0.f;
+      for (int w = 0; w < KS; ++w) {
+        a += sk_st[((w * MT + t) * 2 + 0) * 16 + (lane & 15)];
+        q += sk_st[((w * MT + t) * 2 + 1) * 16 + (lane & 15)];
+      }
+      const float invk = 1.f / (float)(kbytes >> 1);
+      const float mean = NORM == NORM_LN ? a * invk : 0.f;
+      const float var = fmaxf(q * invk - mean * mean, 0.f);
+      const float rstd = rsqrtf(var + eps);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        if constexpr (NORM == NORM_LN) {
+          const int n = n0 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[j][r] = rstd * (s[j][r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+        } else {
+          s[j] *= rstd;
+        }
+      }
+    }
     if constexpr (ACT == ACT_SILU_MUL) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -185,28 +249,29 @@ using namespace dnn;
 //   M <= 64    : wide N (>= 16K, the FFN and the LM head): 4 tiles x 2 chunks,
 //                2 waves; K >= 8K: 1 tile x 8 chunks, 2 waves; otherwise 2 tiles
 //                x 2 chunks, 4 waves (activation re-reads dominate as M grows)
-template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE>
+template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                             int ks, hipStream_t st) {
+                             int ks, const float* colsum, float eps, hipStream_t st) {
   const int groups = (N + 16 * NT - 1) / (16 * NT);
   while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
-  const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE>), dim3(groups), dim3(64 * ks), smem, st,
-                     (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R, ldr,
-                     M, N, kbytes);
+  size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
+  if (NORM != NORM_NONE) smem += (size_t)ks * MT * 2 * 16 * sizeof(float);
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM>), dim3(groups), dim3(64 * ks), smem,
+                     st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
+                     ldr, M, N, kbytes, colsum, eps);
   return (int)hipGetLastError();
 }
 
-template <int ACT, bool F32, bool FP8>
+template <int ACT, bool F32, bool FP8, int NORM = NORM_NONE>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                         hipStream_t st) {
+                         hipStream_t st, const float* colsum = nullptr, float eps = 0.f) {
   const bool wide = N >= 16384;
   const bool deep = kbytes >= 16384;  // K >= 8K bf16
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
-  return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, M, N, \
-                                                             kbytes, KSV, st)
+  return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, \
+                                                                   M, N, kbytes, KSV, colsum, eps, st)
   if (M <= 8) CFG(1, 1, 4, false, 8);
   if (M <= 16) {
     if (wide) CFG(1, 4, 2, false, 2);
@@ -247,6 +312,29 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
   SKD(ACT_GELU)
   SKD(ACT_SILU_MUL)
 #undef SKD
+  return -2;
+}
+
+// Pre-norm fused skinny GEMM (bf16): y = act(rstd (A W'^T - mean colsum) + bias) (+ R),
+// norm = 1 RMSNorm, 2 LayerNorm (colsum required); W', bias', colsum from
+// ops/gemm.py fold_norm.  act: NONE / GELU / SILU_MUL.
+extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
+                                    const void* R, int ldr, int M, int N, int K, int act, int norm,
+                                    const float* colsum, float eps, hipStream_t st) {
+  const int kbytes = K * 2;
+  if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
+  if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
+  if (norm == NORM_LN && colsum == nullptr) return -1;
+  const int la = lda * 2, lw = ldw * 2;
+#define SKN(a, nm)                                                                                                   \
+  if (act == a && norm == nm)                                                                                        \
+    return launch_skinny<a, false, false, nm>(A, la, nullptr, W, lw, nullptr, C, ldc, bias, R, ldr, M, N, kbytes, st, \
+                                              colsum, eps);
+  SKN(ACT_NONE, NORM_RMS)
+  SKN(ACT_SILU_MUL, NORM_RMS)
+  SKN(ACT_NONE, NORM_LN)
+  SKN(ACT_GELU, NORM_LN)
+#undef SKN
   return -2;
 }
 

@@ -62,3 +62,71 @@ def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     g = gate.reshape(F // 8, 8, K)
     u = up.reshape(F // 8, 8, K)
     return torch.stack([g, u], dim=1).reshape(2 * F, K).contiguous()
+
+
+NORM_RMS, NORM_LN = 1, 2
+
+
+class FoldedLinear:
+    """A linear layer with the preceding LayerNorm/RMSNorm folded in
+    (``fold_norm``): ``w`` = W diag(gamma) (bf16), ``bias`` = W beta + b
+    (fp32 or None), ``colsum`` = row sums of the bf16 ``w`` (LayerNorm only)."""
+
+    __slots__ = ("w", "bias", "colsum", "norm", "eps")
+
+    def __init__(self, w, bias, colsum, norm, eps):
+        self.w, self.bias, self.colsum, self.norm, self.eps = w, bias, colsum, norm, eps
+
+
+def fold_norm(w: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+              rms: bool, eps: float, device) -> FoldedLinear:
+    """Fold ``norm(x) @ w.T + bias`` into ``rstd * (x @ w'.T - mean * colsum) + bias'``.
+
+    norm(x) = (x - mean) * rstd * gamma + beta (LayerNorm; RMSNorm: mean = 0,
+    no beta), so  norm(x) @ w.T = rstd * (x @ (w * gamma).T - mean * sum_k
+    (w * gamma)[n, k]) + w @ beta.  Exact in real arithmetic; colsum is taken
+    from the bf16-rounded folded weight actually used by the kernel."""
+    w32 = w.to(device=device, dtype=torch.float32)
+    wf = (w32 * gamma.to(device=device, dtype=torch.float32)[None, :]).to(torch.bfloat16).contiguous()
+    b = None
+    if beta is not None and not rms:
+        b = w32 @ beta.to(device=device, dtype=torch.float32)
+    if bias is not None:
+        b = bias.to(device=device, dtype=torch.float32) if b is None else b + bias.to(device=device,
+                                                                                        dtype=torch.float32)
+    colsum = None if rms else wf.float().sum(dim=1).contiguous()
+    return FoldedLinear(wf, None if b is None else b.contiguous(), colsum, NORM_RMS if rms else NORM_LN, float(eps))
+
+
+def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, std_buf: Optional[torch.Tensor] = None,
+                ones: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  Decode-sized M (<= 64):
+    one skinny-GEMM launch that accumulates the row statistics from the A
+    fragments it streams.  Larger M: the norm kernel standardises x into
+    ``std_buf`` (gamma = ``ones``, no beta), then the plain GEMM with the folded
+    weight and bias."""
+    a = _ACTS[act] if not isinstance(act, int) else act
+    M, K = x.shape
+    N = f.w.shape[0]
+    if f.w.shape[1] != K or x.dtype != torch.bfloat16 or x.stride(1) != 1:
+        raise ValueError(f"linear_norm: x {tuple(x.shape)} {x.dtype} vs w {tuple(f.w.shape)}")
+    if M > 64:
+        from .transformer_ops import layernorm
+        if std_buf is None or ones is None:
+            raise ValueError("linear_norm: M > 64 needs std_buf and ones")
+        xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+        return linear(xs[:M], f.w, f.bias, a, residual, out)
+    if K % 32:
+        raise ValueError(f"linear_norm: K={K} must be a multiple of 32")
+    Nout = N // 2 if a == ACT_SILU_MUL else N
+    if out is None:
+        out = torch.empty((M, Nout), dtype=torch.bfloat16, device=x.device)
+    if out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.shape[0] < M or out.shape[1] < Nout:
+        raise ValueError("linear_norm: bad output buffer")
+    if residual is not None and (residual.shape[0] < M or residual.stride(1) != 1):
+        raise ValueError("linear_norm: bad residual")
+    check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0), ptr(f.bias),
+                                 ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, a, f.norm,
+                                 ptr(f.colsum), f.eps, stream_ptr()), "gemm_skinny_norm")
+    return out

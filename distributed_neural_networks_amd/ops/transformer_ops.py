@@ -97,6 +97,32 @@ def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.
     return out
 
 
+def attn_decode_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, H: int,
+                    Hkv: int, hd: int, pos: torch.Tensor, ws: torch.Tensor, splits: int,
+                    cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None,
+                    scale: Optional[float] = None) -> torch.Tensor:
+    """One decode step straight from the QKV projection rows (B, (H+2Hkv)*hd):
+    RoPE (when cos/sin), the new k/v written into the cache at ``pos[b]`` and
+    attention over ``pos[b]+1`` keys, in one launch (no qkv_split)."""
+    S = kc.shape[2]
+    if kc.shape[:2] != (B, Hkv) or kc.shape[3] != hd or vc.shape != kc.shape:
+        raise ValueError(f"attn_decode_qkv: cache {tuple(kc.shape)} does not match B={B} Hkv={Hkv} hd={hd}")
+    if qkv.dim() != 2 or qkv.shape[0] < B or qkv.shape[1] < (H + 2 * Hkv) * hd or qkv.stride(1) != 1:
+        raise ValueError(f"attn_decode_qkv: qkv {tuple(qkv.shape)} too small")
+    if out.numel() < B * H * hd or pos.numel() < B or pos.dtype != torch.int32:
+        raise ValueError("attn_decode_qkv: bad out/pos")
+    if cos is not None and (cos.shape[0] < S or cos.shape[1] != hd // 2):
+        raise ValueError("attn_decode_qkv: RoPE table does not cover the cache")
+    G = H // Hkv
+    need = B * Hkv * splits * G * (hd + 2)
+    if ws.numel() < need or ws.dtype != torch.float32:
+        raise ValueError(f"attn_decode_qkv: workspace needs {need} fp32")
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    check(lib().attn_decode_qkv(ptr(qkv), qkv.stride(0), ptr(kc), ptr(vc), ptr(out), B, H, Hkv, hd, S, ptr(pos),
+                                ptr(cos), ptr(sin), scale, splits, ptr(ws), stream_ptr()), "attn_decode_qkv")
+    return out
+
+
 def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
     M = x.shape[0]
     N = n if n is not None else x.shape[1]

@@ -12,7 +12,10 @@ reference's all-position logits).
 
 Per layer (GPT-2): LN -> QKV GEMM(+bias) -> split(+cache write) -> attention ->
 O-proj GEMM(+bias, +residual in the epilogue) -> LN -> FC GEMM(+bias, GELU in
-the epilogue) -> proj GEMM(+bias, +residual).  Llama: RMSNorm, RoPE in the
+the epilogue) -> proj GEMM(+bias, +residual).  In bf16 the LNs (ln_1, ln_2,
+ln_f) are folded into the following projection (ops/gemm.py fold_norm): at
+decode sizes the skinny GEMM computes the row statistics itself, so a layer
+is five launches (QKV, attention, O, FC, proj).  Llama: RMSNorm, RoPE in the
 split kernel, GQA, gate|up packed so SiLU(g)*u happens in the GEMM epilogue.
 With ``fp8=True`` every projection uses e4m3 weights (per-channel scales) and
 per-token-quantised activations on the scaled MFMA (GPT-2 XL config).
@@ -29,7 +32,7 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import transformer_ops as T_
-from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, linear, pack_gate_up
+from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up
 from .stages import StageCompute, StageOutput
 
 
@@ -69,6 +72,7 @@ class TransformerStage(StageCompute):
         self.start, self.end, self.first, self.last = start, end, first, last
         self.device = dev = torch.device(device)
         self.fp8 = fp8
+        self.fuse_norm = not fp8  # fold pre-norms into the projections (bf16 path)
         c = self.cfg
         self.d = c.n_embd
         self.H = c.n_head
@@ -80,6 +84,7 @@ class TransformerStage(StageCompute):
         self.rms = self.family == "llama3"
         self.max_batch, self.max_seq = max_batch, max_seq
         self.max_tokens = max_tokens or max_batch * max_seq
+        self.ones = torch.ones((self.d,), dtype=torch.float32, device=dev)
         self.layers: List[LayerW] = [self._pack_layer(sd, j) for j in range(end - start + 1)]
         if first:
             if self.family == "gpt2":
@@ -91,7 +96,10 @@ class TransformerStage(StageCompute):
                 self.lnf_w, self.lnf_b = _f32(sd["ln_f.weight"], dev), _f32(sd["ln_f.bias"], dev)
             else:
                 self.lnf_w, self.lnf_b = _f32(sd["norm.weight"], dev), None
-            self.w_head = self._w(sd["lm_head.weight"])
+            if self.fuse_norm:
+                self.w_head = fold_norm(sd["lm_head.weight"], self.lnf_w, self.lnf_b, None, self.rms, self.eps, dev)
+            else:
+                self.w_head = self._w(sd["lm_head.weight"])
         # RoPE tables (Llama)
         self.cos = self.sin = None
         if self.family == "llama3":
@@ -114,11 +122,18 @@ class TransformerStage(StageCompute):
         dev = self.device
         if self.family == "gpt2":
             p = f"h.{j}."
-            return LayerW(_f32(sd[p + "ln_1.weight"], dev), _f32(sd[p + "ln_1.bias"], dev),
-                          self._w(sd[p + "attn.c_attn.weight"]), _f32(sd[p + "attn.c_attn.bias"], dev),
+            ln1_w, ln1_b = _f32(sd[p + "ln_1.weight"], dev), _f32(sd[p + "ln_1.bias"], dev)
+            ln2_w, ln2_b = _f32(sd[p + "ln_2.weight"], dev), _f32(sd[p + "ln_2.bias"], dev)
+            w_qkv, b_qkv = sd[p + "attn.c_attn.weight"], sd[p + "attn.c_attn.bias"]
+            w_up, b_up = sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"]
+            if self.fuse_norm:
+                return LayerW(None, None, fold_norm(w_qkv, ln1_w, ln1_b, b_qkv, False, self.eps, dev), None,
+                              self._w(sd[p + "attn.c_proj.weight"]), _f32(sd[p + "attn.c_proj.bias"], dev),
+                              None, None, fold_norm(w_up, ln2_w, ln2_b, b_up, False, self.eps, dev), None,
+                              self._w(sd[p + "mlp.c_proj.weight"]), _f32(sd[p + "mlp.c_proj.bias"], dev))
+            return LayerW(ln1_w, ln1_b, self._w(w_qkv), _f32(b_qkv, dev),
                           self._w(sd[p + "attn.c_proj.weight"]), _f32(sd[p + "attn.c_proj.bias"], dev),
-                          _f32(sd[p + "ln_2.weight"], dev), _f32(sd[p + "ln_2.bias"], dev),
-                          self._w(sd[p + "mlp.c_fc.weight"]), _f32(sd[p + "mlp.c_fc.bias"], dev),
+                          ln2_w, ln2_b, self._w(w_up), _f32(b_up, dev),
                           self._w(sd[p + "mlp.c_proj.weight"]), _f32(sd[p + "mlp.c_proj.bias"], dev))
         p = f"layers.{j}."
         qkv = torch.cat([sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"],
@@ -126,10 +141,15 @@ class TransformerStage(StageCompute):
         if self.fp8:
             raise NotImplementedError("fp8 path is implemented for GPT-2 family")
         gu = pack_gate_up(sd[p + "mlp.gate_proj.weight"].float(), sd[p + "mlp.up_proj.weight"].float())
-        return LayerW(_f32(sd[p + "input_layernorm.weight"], dev), None, self._w(qkv), None,
-                      self._w(sd[p + "self_attn.o_proj.weight"]), None,
-                      _f32(sd[p + "post_attention_layernorm.weight"], dev), None,
-                      self._w(gu), None, self._w(sd[p + "mlp.down_proj.weight"]), None)
+        ln1_w = _f32(sd[p + "input_layernorm.weight"], dev)
+        ln2_w = _f32(sd[p + "post_attention_layernorm.weight"], dev)
+        if self.fuse_norm:
+            return LayerW(None, None, fold_norm(qkv, ln1_w, None, None, True, self.eps, dev), None,
+                          self._w(sd[p + "self_attn.o_proj.weight"]), None, None, None,
+                          fold_norm(gu, ln2_w, None, None, True, self.eps, dev), None,
+                          self._w(sd[p + "mlp.down_proj.weight"]), None)
+        return LayerW(ln1_w, None, self._w(qkv), None, self._w(sd[p + "self_attn.o_proj.weight"]), None,
+                      ln2_w, None, self._w(gu), None, self._w(sd[p + "mlp.down_proj.weight"]), None)
 
     def _alloc(self, ntok: int):
         dev, c = self.device, self.cfg
@@ -194,25 +214,27 @@ class TransformerStage(StageCompute):
             h_in = x.reshape(ntok, d)
         h = self.buf_h[:ntok]
         a = self.buf_a[:ntok]
-        if T == 1:
-            torch.add(pos, 1, out=self.lens[:B])
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
-            T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
-            qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[:ntok])
-            T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
-            att = self.buf_att[:ntok]
-            if T == 1:
-                T_.attn_decode(self.buf_q, kc, vc, att, B, self.H, self.Hkv, self.hd, self.lens[:B], self.ws,
-                               self.splits)
+            if self.fuse_norm:
+                qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[:ntok], std_buf=a, ones=self.ones)
             else:
+                T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
+                qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[:ntok])
+            att = self.buf_att[:ntok]
+            if T == 1:  # decode: split/RoPE/cache write fused into the attention launch
+                T_.attn_decode_qkv(qkv, kc, vc, att, B, self.H, self.Hkv, self.hd, pos, self.ws, self.splits,
+                                   self.cos, self.sin)
+            else:
+                T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
             self._lin(att, L.w_o, L.b_o, residual=h_in, out=h)
-            T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
-            if self.family == "gpt2":
-                f = self._lin(a, L.w_up, L.b_up, act=ACT_GELU, out=self.buf_f[:ntok])
+            up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
+            if self.fuse_norm:
+                f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[:ntok], std_buf=a, ones=self.ones)
             else:
-                f = self._lin(a, L.w_up, None, act=ACT_SILU_MUL, out=self.buf_f[:ntok])
+                T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
+                f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[:ntok])
             self._lin(f, L.w_down, L.b_down, residual=h, out=h)
             h_in = h
         if not self.last:
@@ -224,13 +246,17 @@ class TransformerStage(StageCompute):
             rows, src, ldx = B, h[T - 1:], T * d
         else:
             rows, src, ldx = ntok, h, d
-        lnf = self.buf_lnf[:rows]
-        T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)
         logits = self.logits[:rows]
-        if self.fp8:
-            self._head_fp8(lnf, logits)
+        if self.fuse_norm:
+            x_last = torch.as_strided(src, (rows, d), (ldx, 1))
+            linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf, ones=self.ones)
         else:
-            linear(lnf, self.w_head, None, out=logits[:, :self.V])
+            lnf = self.buf_lnf[:rows]
+            T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)
+            if self.fp8:
+                self._head_fp8(lnf, logits)
+            else:
+                linear(lnf, self.w_head, None, out=logits[:, :self.V])
         nxt = self.next_ids[:rows]
         if self.temperature > 0 and last_only:
             T_.sample_topk(logits, nxt, self.V, self.temperature, self.top_k, self.seed, step=pos)

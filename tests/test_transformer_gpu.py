@@ -255,3 +255,110 @@ def test_fp8_skinny_act_residual(M, act):
     ref = xq @ (wq.q[:, :K].float() * wq.scale[:, None]).t() + b
     ref = torch.relu(ref) if act == 1 else torch.nn.functional.gelu(ref)
     assert _rel(y, ref + r.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
+@pytest.mark.parametrize("rms,act", [(True, "none"), (True, "silu_mul"), (False, "none"), (False, "gelu")])
+def test_linear_norm_fused(M, rms, act):
+    """Pre-norm folded into the skinny GEMM (row stats from the streamed A
+    fragments) and, for M > 64, standardise + plain GEMM: vs fp32 norm + linear."""
+    from distributed_neural_networks_amd.ops.gemm import fold_norm, linear_norm, pack_gate_up
+    torch.manual_seed(5)
+    K, N = 768, 1024
+    x = (torch.randn(M, K, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = None if rms else torch.randn(K, device=DEV) * 0.1
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = None if rms else torch.randn(N, device=DEV) * 0.1
+    R = torch.randn(M, N // 2 if act == "silu_mul" else N, device=DEV).bfloat16() if act == "none" else None
+    xf = x.float()
+    xn = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma if rms
+          else F.layer_norm(xf, (K,), gamma, beta, 1e-5))
+    if act == "silu_mul":
+        g, u = W[: N // 2], W[N // 2:]
+        Wk = pack_gate_up(g, u)
+        ref = F.silu(xn @ g.t()) * (xn @ u.t())
+    else:
+        Wk = W
+        ref = xn @ W.t() + (bias if bias is not None else 0)
+        if act == "gelu":
+            ref = F.gelu(ref)
+    if R is not None:
+        ref = ref + R.float()
+    f = fold_norm(Wk, gamma, beta, bias, rms, 1e-5, DEV)
+    out = torch.empty(ref.shape, device=DEV, dtype=torch.bfloat16)
+    std = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    ones = torch.ones(K, device=DEV)
+    linear_norm(x, f, act=act, residual=R, out=out, std_buf=std, ones=ones)
+    assert _rel(out, ref) < 1.5e-2, _rel(out, ref)
+
+
+def test_linear_norm_strided_rows():
+    """The last-position head: rows T-1, 2T-1, ... of the hidden states."""
+    from distributed_neural_networks_amd.ops.gemm import fold_norm, linear_norm
+    torch.manual_seed(6)
+    B, Tn, K, N = 4, 9, 512, 640
+    h = torch.randn(B * Tn, K, device=DEV).bfloat16()
+    gamma, beta = torch.rand(K, device=DEV) + 0.5, torch.randn(K, device=DEV) * 0.1
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    f = fold_norm(W, gamma, beta, None, False, 1e-5, DEV)
+    x_last = torch.as_strided(h[Tn - 1:], (B, K), (Tn * K, 1))
+    out = torch.empty(B, N, device=DEV, dtype=torch.bfloat16)
+    linear_norm(x_last, f, out=out)
+    ref = F.layer_norm(h.float().view(B, Tn, K)[:, -1], (K,), gamma, beta, 1e-5) @ W.t()
+    assert _rel(out, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("B,H,Hkv,hd,S,pos,rope,splits", [
+    (1, 32, 8, 128, 200, [150], True, 1), (3, 12, 12, 64, 300, [0, 17, 299], False, 2),
+    (2, 8, 2, 128, 1024, [700, 1023], True, 4), (2, 4, 4, 64, 64, [63, 64], False, 1)])
+def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits):
+    """Fused decode step (split + RoPE + cache write + attention) == qkv_split
+    then attn_decode, and the cache row it wrote matches; pos >= S (overflow)
+    writes nothing and attends to the S cached keys."""
+    from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(9)
+    kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv = torch.randn(B, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    p = torch.tensor(pos, device=DEV, dtype=torch.int32)
+    cos = sin = None
+    if rope:
+        cfg = LLAMA_CONFIGS["llama3-tiny"]
+        import dataclasses
+        cos, sin = rope_tables(dataclasses.replace(cfg, n_embd=hd * cfg.n_head), S)
+        cos, sin = cos.to(DEV), sin.to(DEV)
+        assert cos.shape[1] == hd // 2
+    G = H // Hkv
+    ws = torch.empty(B * Hkv * splits * G * (hd + 2), device=DEV)
+    out = torch.empty(B, H * hd, device=DEV, dtype=torch.bfloat16)
+    T.attn_decode_qkv(qkv, kc, vc, out, B, H, Hkv, hd, p, ws, splits, cos, sin)
+    # unfused reference path on the copies
+    q = torch.empty(B * H * hd, device=DEV, dtype=torch.bfloat16)
+    T.qkv_split(qkv, q, kc2, vc2, B, 1, H, Hkv, hd, p, cos, sin)
+    lens = torch.clamp(p + 1, max=S)
+    out2 = torch.empty_like(out)
+    T.attn_decode(q, kc2, vc2, out2, B, H, Hkv, hd, lens.to(torch.int32), ws, splits)
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    qr = qkv[:, :H * hd].view(B, H, hd).float()
+    if rope:
+        from distributed_neural_networks_amd.models.llama3 import apply_rope
+        pc = torch.clamp(p, max=S - 1).long()
+        c, s_ = cos[pc], sin[pc]  # (B, hd/2)
+        h2 = hd // 2
+        x1, x2 = qr[..., :h2], qr[..., h2:]
+        qr = torch.cat([x1 * c[:, None] - x2 * s_[:, None], x2 * c[:, None] + x1 * s_[:, None]], -1)
+    qr = qr.bfloat16().float()
+    for b in range(B):
+        if pos[b] < S:  # overflow rows: qkv_split drops q too, so only the torch reference applies
+            assert _rel(out[b], out2[b]) < 5e-3, b
+        n = min(pos[b] + 1, S)
+        k = kc[b, :, :n].float().repeat_interleave(G, 0)
+        v = vc[b, :, :n].float().repeat_interleave(G, 0)
+        qb = qr[b]
+        s = torch.einsum("hd,hkd->hk", qb, k) / math.sqrt(hd)
+        ref = torch.einsum("hk,hkd->hd", s.softmax(-1), v).reshape(-1)
+        assert _rel(out[b], ref) < 2e-2, b
