@@ -283,7 +283,8 @@ def main(args=None):
             "metric": f"tokens/sec {model} {S}-stage greedy decode", "value": round(value, 1), "unit": "tokens/s",
             "n_gpus": N, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(decode_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp8-e4m3 weights/acts, bf16 elsewhere" if fp8 else "bf16",
+            "dtype": ("fp8-e4m3 weights (decode: W8A16 on bf16 MFMA; prefill: W8A8 on fp8 MFMA), bf16 activations"
+                      if fp8 else "bf16"),
             "data": "synthetic prompts, random-init weights",
             "prefill_tokens_per_s": round(prefill_tok / prefill_s, 1),
             "prefill_ms_per_round": round(prefill_s * 1e3, 3),

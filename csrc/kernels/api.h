@@ -12,6 +12,9 @@ int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, void* 
 int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                          const void* R, int ldr, int M, int N, int K, int act, int norm, const float* colsum, float eps,
                          hipStream_t st);
+int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
+                       const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
+                       const float* colsum, float eps, hipStream_t st);
 int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw, void* C, int ldc,
                     const float* bias, const void* R, int ldr, int M, int N, int K, int act, int out_f32, int fp8,
                     hipStream_t st);

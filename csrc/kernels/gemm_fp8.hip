@@ -101,7 +101,14 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(const uint8_t* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) {
+        if constexpr (ACT == 3) {
+          // SwiGLU on the packed gate|up weight (ops/gemm.py pack_gate_up): in each
+          // 16-column tile lanes (l & 15) < 8 hold gate, the lane ^ 8 partner its up
+          const float v = m < M ? acc[i][j][r] * sa[m] * swn + b : 0.f;
+          const float u = __shfl_xor(v, 8, 64);
+          if ((lane & 8) == 0 && m < M && n < N)
+            C[(size_t)m * ldc + (n0 + wn * 64 + j * 16) / 2 + (lane & 7)] = f2bf(silu(v) * u);
+        } else if (m < M && n < N) {
           float v = acc[i][j][r] * sa[m] * swn + b;
           if (ACT == 1) v = fmaxf(v, 0.f);
           if (ACT == 2) v = gelu_erf(v);
@@ -149,6 +156,7 @@ using namespace dnn;
 extern "C" int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc,
                             const float* bias, const void* R, int ldr, int M, int N, int K, int act, hipStream_t st) {
   if (K % F8_BK != 0) return -1;
+  if (act == 3 && N % 16 != 0) return -1;  // packed gate|up groups of 8+8
   const int tiles = ((M + F8_BM - 1) / F8_BM) * ((N + F8_BN - 1) / F8_BN);
 #define F8(a)                                                                                                        \
   if (act == a) {                                                                                                    \
@@ -156,7 +164,7 @@ extern "C" int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const
                        sw, (bf16_t*)C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);                                   \
     return (int)hipGetLastError();                                                                                   \
   }
-  F8(0) F8(1) F8(2)
+  F8(0) F8(1) F8(2) F8(3)
 #undef F8
   return -2;
 }

@@ -51,6 +51,23 @@ __device__ __forceinline__ f32x4 sk_mma(const i32x4& w, const i32x4& a, f32x4 ac
 
 enum SkNorm { NORM_NONE = 0, NORM_RMS = 1, NORM_LN = 2 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// 16 OCP e4m3 weight bytes -> 16 bf16 (exact: every e4m3 value is a bf16
+// value; the hardware converter yields fp32 and bf16 is its upper half).
+__device__ __forceinline__ void w8_to_bf16(const i32x4& w, bf16x8& lo, bf16x8& hi) {
+  uint32_t o[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(w[i], false);
+    const f32x2 b = __builtin_amdgcn_cvt_pk_f32_fp8(w[i], true);
+    o[2 * i] = (__float_as_uint(a[0]) >> 16) | (__float_as_uint(a[1]) & 0xffff0000u);
+    o[2 * i + 1] = (__float_as_uint(b[0]) >> 16) | (__float_as_uint(b[1]) & 0xffff0000u);
+  }
+  __builtin_memcpy(&lo, &o[0], 16);
+  __builtin_memcpy(&hi, &o[4], 16);
+}
+
 // Sum and sum of squares of the 8 bf16 of one A fragment.
 __device__ __forceinline__ void sk_stats(const i32x4& a, float& s1, float& s2) {
 #pragma unroll
@@ -61,7 +78,8 @@ __device__ __forceinline__ void sk_stats(const i32x4& a, float& s1, float& s2) {
   }
 }
 
-template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false, int NORM = NORM_NONE>
+template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false, int NORM = NORM_NONE,
+          bool W8 = false>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                            const float* __restrict__ sa, const uint8_t* __restrict__ W,
                                                            int ldw_b, const float* __restrict__ sw,
@@ -70,7 +88,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
                                                            const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                            int kbytes, const float* __restrict__ colsum = nullptr,
                                                            float eps = 0.f) {
-  static_assert(NORM == NORM_NONE || !FP8, "fused norm is bf16-only");
+  static_assert(NORM == NORM_NONE || !FP8, "fused norm needs bf16 activations");
+  static_assert(!(FP8 && W8), "W8 = fp8 weights with bf16 activations; FP8 = both fp8");
+  constexpr int AU = W8 ? 2 : 1;        // 16-B A loads per chunk per M tile (W8: a chunk is 64 k = 128 B of A)
+  constexpr int ACH = W8 ? 128 : 64;    // A bytes per row per chunk
   extern __shared__ __attribute__((aligned(16))) f32x4 sk_red[];  // [KS][NT*MT][64], then [KS][MT][16] x2 stats
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, KS = blockDim.x >> 6;
   const int n0 = blockIdx.x * (16 * NT);
@@ -88,7 +109,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   for (int t = 0; t < MT; ++t) {
     int m = t * 16 + (lane & 15);
     m = m < M ? m : M - 1;
-    ap[t] = A + (size_t)m * lda_b + lg;
+    ap[t] = A + (size_t)m * lda_b + lg * AU;
   }
   f32x4 acc[NT][MT];
 #pragma unroll
@@ -105,7 +126,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   // Batches of U chunks; the last batch of a wave is partial: its loads are
   // clamped in-bounds and the surplus chunks' weights zeroed, so every batch
   // (including short K slices) issues all of its loads at once.
-  auto load = [&](int cc, i32x4(&wv)[NT][U], i32x4(&av)[MT][U]) {
+  auto load = [&](int cc, i32x4(&wv)[NT][U], i32x4(&av)[MT][U * AU]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int ci = min(cc + u, c1 - 1);
@@ -116,13 +137,16 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     for (int u = 0; u < U; ++u) {
       const int ci = min(cc + u, c1 - 1);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) av[t][u] = *reinterpret_cast<const i32x4*>(ap[t] + (size_t)ci * 64);
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int h = 0; h < AU; ++h)
+          av[t][u * AU + h] = *reinterpret_cast<const i32x4*>(ap[t] + (size_t)ci * ACH + 16 * h);
     }
     // keep every load of the batch ahead of the MFMAs that follow (the scheduler
     // would otherwise interleave them and wait vmcnt(0) per chunk)
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto comp = [&](int cc, i32x4(&wv)[NT][U], const i32x4(&av)[MT][U]) {
+  auto comp = [&](int cc, i32x4(&wv)[NT][U], const i32x4(&av)[MT][U * AU]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (cc + u >= c1) {
@@ -130,12 +154,32 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
         for (int j = 0; j < NT; ++j) wv[j][u] = i32x4{0, 0, 0, 0};
       } else if constexpr (NORM != NORM_NONE) {
 #pragma unroll
-        for (int t = 0; t < MT; ++t) sk_stats(av[t][u], st1[t], st2[t]);
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int h = 0; h < AU; ++h) sk_stats(av[t][u * AU + h], st1[t], st2[t]);
       }
+      if constexpr (W8) {
+        // the lane's 16 weight bytes are k = 16g..16g+15 of the chunk; its two A
+        // pieces hold the same k, so MFMA #h pairs W bytes 8h..8h+7 with A piece h
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 wlo, whi;
+          w8_to_bf16(wv[j][u], wlo, whi);
 #pragma unroll
-        for (int t = 0; t < MT; ++t) acc[j][t] = sk_mma<FP8>(wv[j][u], av[t][u], acc[j][t]);
+          for (int t = 0; t < MT; ++t) {
+            bf16x8 a0, a1;
+            __builtin_memcpy(&a0, &av[t][2 * u], 16);
+            __builtin_memcpy(&a1, &av[t][2 * u + 1], 16);
+            acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, a0, acc[j][t], 0, 0, 0);
+            acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi, a1, acc[j][t], 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[j][t] = sk_mma<FP8>(wv[j][u], av[t][u], acc[j][t]);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -144,7 +188,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   if constexpr (PIPE) {
     // software pipeline: the next batch is in flight while this one computes
     if (nb > 0) {
-      i32x4 w0[NT][U], a0[MT][U], w1[NT][U], a1[MT][U];
+      i32x4 w0[NT][U], a0[MT][U * AU], w1[NT][U], a1[MT][U * AU];
       load(c, w0, a0);
       int b = 0;
       for (; b + 2 <= nb; b += 2) {
@@ -158,7 +202,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     }
   } else {
     for (int b = 0; b < nb; ++b, c += U) {
-      i32x4 wv[NT][U], av[MT][U];
+      i32x4 wv[NT][U], av[MT][U * AU];
       load(c, wv, av);
       comp(c, wv, av);
     }
@@ -196,13 +240,21 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     }
     const int m = t * 16 + (lane & 15);
     const float rs = (FP8 && m < M) ? sa[m] : 1.f;
+    if constexpr (W8) {  // per-output-channel weight scale, before the norm terms (colsum is of the dequantised W)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[j][r] *= n + r < N ? sw[n + r] : 0.f;
+      }
+    }
     if constexpr (NORM != NORM_NONE) {
       float a = 0.f, q = 0.f;
       for (int w = 0; w < KS; ++w) {
         a += sk_st[((w * MT + t) * 2 + 0) * 16 + (lane & 15)];
         q += sk_st[((w * MT + t) * 2 + 1) * 16 + (lane & 15)];
       }
-      const float invk = 1.f / (float)(kbytes >> 1);
+      const float invk = 1.f / (float)(W8 ? kbytes : kbytes >> 1);
       const float mean = NORM == NORM_LN ? a * invk : 0.f;
       const float var = fmaxf(q * invk - mean * mean, 0.f);
       const float rstd = rsqrtf(var + eps);
@@ -249,7 +301,7 @@ using namespace dnn;
 //   M <= 64    : wide N (>= 16K, the FFN and the LM head): 4 tiles x 2 chunks,
 //                2 waves; K >= 8K: 1 tile x 8 chunks, 2 waves; otherwise 2 tiles
 //                x 2 chunks, 4 waves (activation re-reads dominate as M grows)
-template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM>
+template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                              int ks, const float* colsum, float eps, hipStream_t st) {
@@ -257,21 +309,21 @@ static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const vo
   while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
   size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
   if (NORM != NORM_NONE) smem += (size_t)ks * MT * 2 * 16 * sizeof(float);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM>), dim3(groups), dim3(64 * ks), smem,
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8>), dim3(groups), dim3(64 * ks), smem,
                      st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
                      ldr, M, N, kbytes, colsum, eps);
   return (int)hipGetLastError();
 }
 
-template <int ACT, bool F32, bool FP8, int NORM = NORM_NONE>
+template <int ACT, bool F32, bool FP8, int NORM = NORM_NONE, bool W8 = false>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st, const float* colsum = nullptr, float eps = 0.f) {
   const bool wide = N >= 16384;
   const bool deep = kbytes >= 16384;  // K >= 8K bf16
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
-  return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R, ldr, \
-                                                                   M, N, kbytes, KSV, colsum, eps, st)
+  return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
+                                                                       ldr, M, N, kbytes, KSV, colsum, eps, st)
   if (M <= 8) CFG(1, 1, 4, false, 8);
   if (M <= 16) {
     if (wide) CFG(1, 4, 2, false, 2);
@@ -335,6 +387,30 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
   SKN(ACT_NONE, NORM_LN)
   SKN(ACT_GELU, NORM_LN)
 #undef SKN
+  return -2;
+}
+
+// Weight-only fp8 (W8A16) skinny GEMM: W OCP e4m3 [N, ldw bytes] with per-channel
+// scales sw, A bf16, bf16 MFMA on the exactly-converted weights; half the
+// weight bytes of bf16 with the bf16 pipeline's epilogues and fused pre-norm
+// (norm 0 = none).  K % 64 == 0 (logical K; the weight rows may be padded).
+extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
+                                  const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
+                                  const float* colsum, float eps, hipStream_t st) {
+  if (M <= 0 || M > 64 || N <= 0 || K % 64 != 0 || ldw < K || sw == nullptr) return -1;
+  if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
+  if (norm == NORM_LN && colsum == nullptr) return -1;
+  const int la = lda * 2;
+#define SKW(a, nm)                                                                                                    \
+  if (act == a && norm == nm)                                                                                         \
+    return launch_skinny<a, false, false, nm, true>(A, la, nullptr, W, ldw, sw, C, ldc, bias, R, ldr, M, N, K, st,     \
+                                                    colsum, eps);
+  SKW(ACT_NONE, NORM_NONE)
+  SKW(ACT_NONE, NORM_RMS)
+  SKW(ACT_SILU_MUL, NORM_RMS)
+  SKW(ACT_NONE, NORM_LN)
+  SKW(ACT_GELU, NORM_LN)
+#undef SKW
   return -2;
 }
 

@@ -6,6 +6,12 @@ Activations: per-token absmax scale, quantised on device by
 ``quant_fp8_rows`` right before each GEMM (fused into the GEMM's producer is a
 later optimisation).  ``linear_fp8`` = ``quant -> gemm_fp8`` with the bf16
 epilogue (bias / act / residual) of the bf16 GEMM.
+
+Decode-sized M (<= 64) is weight-bandwidth bound, so there the activations
+stay bf16 (``linear_w8``: W8A16): the skinny kernel converts the streamed
+e4m3 weights to bf16 in registers (exact) and applies the channel scales in
+its epilogue — half the bytes of bf16 weights, no activation-quantise launch,
+and the fused pre-norm of the bf16 path (ops/gemm.py ``linear_norm``).
 """
 from __future__ import annotations
 
@@ -67,7 +73,7 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
     sbuf = sbuf if sbuf is not None else torch.empty((M,), dtype=torch.float32, device=x.device)
     quant_rows(x2, qbuf, sbuf, M)
     if out is None:
-        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+        out = torch.empty((M, N // 2 if act == 3 else N), dtype=torch.bfloat16, device=x.device)
     o2 = out.reshape(-1, out.shape[-1])
     r2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
     if M <= 64:  # decode: fp8 weight streaming (half the bytes of bf16)
@@ -77,4 +83,26 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
         return out
     check(lib().gemm_fp8(ptr(qbuf), ptr(sbuf), ptr(w.q), ptr(w.scale), ptr(o2), o2.stride(0), ptr(bias), ptr(r2),
                          0 if r2 is None else r2.stride(0), M, N, kp, act, stream_ptr()), "gemm_fp8")
+    return out
+
+
+def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
+              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, norm: int = 0,
+              colsum: Optional[torch.Tensor] = None, eps: float = 0.0) -> torch.Tensor:
+    """Weight-only fp8 GEMM for M <= 64: bf16 x (M, K) times e4m3 w, bf16 out.
+    ``norm`` (1 RMS / 2 LN, with ``colsum`` for LN) fuses a folded pre-norm."""
+    M, K = x.shape
+    N, kp = w.q.shape
+    if M > 64 or (w.k and w.k != K) or kp < K or K % 64:
+        raise ValueError(f"linear_w8: x {tuple(x.shape)} vs weight {tuple(w.q.shape)} (k={w.k})")
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1:
+        raise TypeError("linear_w8: bf16 activations with a contiguous last dim")
+    Nout = N // 2 if act == 3 else N
+    if out is None:
+        out = torch.empty((M, Nout), dtype=torch.bfloat16, device=x.device)
+    if out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.shape[0] < M or out.shape[1] < Nout:
+        raise ValueError("linear_w8: bad output buffer")
+    check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0), ptr(bias),
+                               ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, act, norm,
+                               ptr(colsum), eps, stream_ptr()), "gemm_skinny_w8")
     return out

@@ -79,44 +79,61 @@ class FoldedLinear:
 
 
 def fold_norm(w: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor], bias: Optional[torch.Tensor],
-              rms: bool, eps: float, device) -> FoldedLinear:
+              rms: bool, eps: float, device, fp8: bool = False) -> FoldedLinear:
     """Fold ``norm(x) @ w.T + bias`` into ``rstd * (x @ w'.T - mean * colsum) + bias'``.
 
     norm(x) = (x - mean) * rstd * gamma + beta (LayerNorm; RMSNorm: mean = 0,
     no beta), so  norm(x) @ w.T = rstd * (x @ (w * gamma).T - mean * sum_k
     (w * gamma)[n, k]) + w @ beta.  Exact in real arithmetic; colsum is taken
-    from the bf16-rounded folded weight actually used by the kernel."""
+    from the rounded folded weight actually used by the kernel (bf16, or the
+    dequantised e4m3 weight with ``fp8=True``)."""
     w32 = w.to(device=device, dtype=torch.float32)
-    wf = (w32 * gamma.to(device=device, dtype=torch.float32)[None, :]).to(torch.bfloat16).contiguous()
+    wf32 = w32 * gamma.to(device=device, dtype=torch.float32)[None, :]
+    if fp8:
+        from .fp8 import quantize_weight
+        wf = quantize_weight(wf32, device)
+        wdq = wf.q[:, :wf32.shape[1]].float() * wf.scale[:, None]
+    else:
+        wf = wf32.to(torch.bfloat16).contiguous()
+        wdq = wf.float()
+    del wf32
     b = None
     if beta is not None and not rms:
         b = w32 @ beta.to(device=device, dtype=torch.float32)
     if bias is not None:
         b = bias.to(device=device, dtype=torch.float32) if b is None else b + bias.to(device=device,
                                                                                         dtype=torch.float32)
-    colsum = None if rms else wf.float().sum(dim=1).contiguous()
+    colsum = None if rms else wdq.sum(dim=1).contiguous()
     return FoldedLinear(wf, None if b is None else b.contiguous(), colsum, NORM_RMS if rms else NORM_LN, float(eps))
 
 
 def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, std_buf: Optional[torch.Tensor] = None,
-                ones: Optional[torch.Tensor] = None) -> torch.Tensor:
+                ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
+                s8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  Decode-sized M (<= 64):
     one skinny-GEMM launch that accumulates the row statistics from the A
-    fragments it streams.  Larger M: the norm kernel standardises x into
-    ``std_buf`` (gamma = ``ones``, no beta), then the plain GEMM with the folded
-    weight and bias."""
+    fragments it streams (bf16 weights, or e4m3 weights converted in registers).
+    Larger M: the norm kernel standardises x into ``std_buf`` (gamma = ``ones``,
+    no beta), then the plain GEMM with the folded weight and bias (bf16, or the
+    W8A8 fp8 GEMM with the ``q8``/``s8`` activation-quantisation buffers)."""
+    from .fp8 import Fp8Weight, linear_fp8, linear_w8
     a = _ACTS[act] if not isinstance(act, int) else act
     M, K = x.shape
+    w8 = isinstance(f.w, Fp8Weight)
     N = f.w.shape[0]
-    if f.w.shape[1] != K or x.dtype != torch.bfloat16 or x.stride(1) != 1:
+    if (not w8 and f.w.shape[1] != K) or x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise ValueError(f"linear_norm: x {tuple(x.shape)} {x.dtype} vs w {tuple(f.w.shape)}")
     if M > 64:
         from .transformer_ops import layernorm
         if std_buf is None or ones is None:
             raise ValueError("linear_norm: M > 64 needs std_buf and ones")
         xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+        if w8:
+            return linear_fp8(xs[:M], f.w, f.bias, a, residual, out, q8, s8)
         return linear(xs[:M], f.w, f.bias, a, residual, out)
+    if w8:
+        return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps)
     if K % 32:
         raise ValueError(f"linear_norm: K={K} must be a multiple of 32")
     Nout = N // 2 if a == ACT_SILU_MUL else N

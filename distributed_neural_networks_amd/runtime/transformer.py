@@ -17,8 +17,10 @@ ln_f) are folded into the following projection (ops/gemm.py fold_norm): at
 decode sizes the skinny GEMM computes the row statistics itself, so a layer
 is five launches (QKV, attention, O, FC, proj).  Llama: RMSNorm, RoPE in the
 split kernel, GQA, gate|up packed so SiLU(g)*u happens in the GEMM epilogue.
-With ``fp8=True`` every projection uses e4m3 weights (per-channel scales) and
-per-token-quantised activations on the scaled MFMA (GPT-2 XL config).
+With ``fp8=True`` every projection uses e4m3 weights (per-channel scales): in
+prefill with per-token-quantised activations on the scaled fp8 MFMA (W8A8), in
+decode as weight-only fp8 (W8A16, the weight bytes halve and the fused
+pre-norm stays) — GPT-2 XL config, and Llama-3 8B with ``dtype: fp8``.
 All positions/lengths live in device memory so a decode step is one graph.
 """
 from __future__ import annotations
@@ -72,7 +74,7 @@ class TransformerStage(StageCompute):
         self.start, self.end, self.first, self.last = start, end, first, last
         self.device = dev = torch.device(device)
         self.fp8 = fp8
-        self.fuse_norm = not fp8  # fold pre-norms into the projections (bf16 path)
+        self.fuse_norm = True  # fold pre-norms into the projections (ops/gemm.py fold_norm)
         c = self.cfg
         self.d = c.n_embd
         self.H = c.n_head
@@ -97,7 +99,8 @@ class TransformerStage(StageCompute):
             else:
                 self.lnf_w, self.lnf_b = _f32(sd["norm.weight"], dev), None
             if self.fuse_norm:
-                self.w_head = fold_norm(sd["lm_head.weight"], self.lnf_w, self.lnf_b, None, self.rms, self.eps, dev)
+                self.w_head = fold_norm(sd["lm_head.weight"], self.lnf_w, self.lnf_b, None, self.rms, self.eps, dev,
+                                        self.fp8)
             else:
                 self.w_head = self._w(sd["lm_head.weight"])
         # RoPE tables (Llama)
@@ -127,9 +130,11 @@ class TransformerStage(StageCompute):
             w_qkv, b_qkv = sd[p + "attn.c_attn.weight"], sd[p + "attn.c_attn.bias"]
             w_up, b_up = sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"]
             if self.fuse_norm:
-                return LayerW(None, None, fold_norm(w_qkv, ln1_w, ln1_b, b_qkv, False, self.eps, dev), None,
+                qkv_f = fold_norm(w_qkv, ln1_w, ln1_b, b_qkv, False, self.eps, dev, self.fp8)
+                up_f = fold_norm(w_up, ln2_w, ln2_b, b_up, False, self.eps, dev, self.fp8)
+                return LayerW(None, None, qkv_f, None,
                               self._w(sd[p + "attn.c_proj.weight"]), _f32(sd[p + "attn.c_proj.bias"], dev),
-                              None, None, fold_norm(w_up, ln2_w, ln2_b, b_up, False, self.eps, dev), None,
+                              None, None, up_f, None,
                               self._w(sd[p + "mlp.c_proj.weight"]), _f32(sd[p + "mlp.c_proj.bias"], dev))
             return LayerW(ln1_w, ln1_b, self._w(w_qkv), _f32(b_qkv, dev),
                           self._w(sd[p + "attn.c_proj.weight"]), _f32(sd[p + "attn.c_proj.bias"], dev),
@@ -138,15 +143,13 @@ class TransformerStage(StageCompute):
         p = f"layers.{j}."
         qkv = torch.cat([sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"],
                          sd[p + "self_attn.v_proj.weight"]], dim=0)
-        if self.fp8:
-            raise NotImplementedError("fp8 path is implemented for GPT-2 family")
         gu = pack_gate_up(sd[p + "mlp.gate_proj.weight"].float(), sd[p + "mlp.up_proj.weight"].float())
         ln1_w = _f32(sd[p + "input_layernorm.weight"], dev)
         ln2_w = _f32(sd[p + "post_attention_layernorm.weight"], dev)
         if self.fuse_norm:
-            return LayerW(None, None, fold_norm(qkv, ln1_w, None, None, True, self.eps, dev), None,
+            return LayerW(None, None, fold_norm(qkv, ln1_w, None, None, True, self.eps, dev, self.fp8), None,
                           self._w(sd[p + "self_attn.o_proj.weight"]), None, None, None,
-                          fold_norm(gu, ln2_w, None, None, True, self.eps, dev), None,
+                          fold_norm(gu, ln2_w, None, None, True, self.eps, dev, self.fp8), None,
                           self._w(sd[p + "mlp.down_proj.weight"]), None)
         return LayerW(ln1_w, None, self._w(qkv), None, self._w(sd[p + "self_attn.o_proj.weight"]), None,
                       ln2_w, None, self._w(gu), None, self._w(sd[p + "mlp.down_proj.weight"]), None)
@@ -166,6 +169,7 @@ class TransformerStage(StageCompute):
         self.splits = T_.decode_splits(self.max_seq, self.max_batch, Hkv)
         G = H // Hkv
         self.ws = torch.empty((self.max_batch * Hkv * self.splits * G * (hd + 2),), dtype=torch.float32, device=dev)
+        self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
             kmax = max(kpad_of(d), kpad_of(ffn))
@@ -178,7 +182,9 @@ class TransformerStage(StageCompute):
 
     def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None):
         if self.fp8:
-            from ..ops.fp8 import linear_fp8
+            from ..ops.fp8 import linear_fp8, linear_w8
+            if x.shape[0] <= 64:  # decode: weight-only fp8 (bf16 activations, no quantise launch)
+                return linear_w8(x, w, b, act, residual, out)
             return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
         return linear(x, w, b, act, residual, out)
 
@@ -217,7 +223,8 @@ class TransformerStage(StageCompute):
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
             if self.fuse_norm:
-                qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[:ntok], std_buf=a, ones=self.ones)
+                qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[:ntok], std_buf=a, ones=self.ones, q8=self.q8,
+                                  s8=self.s8)
             else:
                 T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
                 qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[:ntok])
@@ -231,7 +238,8 @@ class TransformerStage(StageCompute):
             self._lin(att, L.w_o, L.b_o, residual=h_in, out=h)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
             if self.fuse_norm:
-                f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[:ntok], std_buf=a, ones=self.ones)
+                f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[:ntok], std_buf=a, ones=self.ones, q8=self.q8,
+                                s8=self.s8)
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
                 f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[:ntok])
@@ -249,7 +257,8 @@ class TransformerStage(StageCompute):
         logits = self.logits[:rows]
         if self.fuse_norm:
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
-            linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf, ones=self.ones)
+            linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf, ones=self.ones,
+                        q8=self.q8, s8=self.s8)
         else:
             lnf = self.buf_lnf[:rows]
             T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)

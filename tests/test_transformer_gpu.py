@@ -218,21 +218,81 @@ def test_gpt2_stage_logits_close():
     assert _rel(out.probs.view(2, 40, -1).cpu(), ref) < 3e-2
 
 
-def test_fp8_stage_runs():
+@pytest.mark.parametrize("model", ["gpt2-tiny", "llama3-tiny"])
+@pytest.mark.parametrize("Tn", [24, 40])
+def test_fp8_stage_runs(model, Tn):
+    """fp8 weights: 2 x 24 tokens take the weight-only W8A16 skinny path (fused
+    pre-norm), 2 x 40 the standardise + quantise + W8A8 fp8-MFMA path."""
     from distributed_neural_networks_amd import checkpoint as ckpt
-    from distributed_neural_networks_amd.models import build_golden_stage
+    from distributed_neural_networks_amd.models import build_golden_stage, model_info
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
-    model = "gpt2-tiny"
-    sd = ckpt.random_stage_state_dict(model, 0, 3, True, True, 5)
-    st = TransformerStage(model, sd, 0, 3, True, True, DEV, max_batch=2, max_seq=128, fp8=True)
-    g = build_golden_stage(model, 0, 3, True, True)
+    n = model_info(model).num_layers
+    sd = ckpt.random_stage_state_dict(model, 0, n - 1, True, True, 5)
+    st = TransformerStage(model, sd, 0, n - 1, True, True, DEV, max_batch=2, max_seq=128, fp8=True)
+    g = build_golden_stage(model, 0, n - 1, True, True)
     g.load_state_dict(sd)
-    ids = torch.randint(0, 512, (2, 24))
+    ids = torch.randint(0, 512, (2, Tn))
     pos = torch.zeros(2, dtype=torch.int32, device=DEV)
-    out = st.step(ids.to(DEV, torch.int32), pos, 2, 24, last_only=False)
+    out = st.step(ids.to(DEV, torch.int32), pos, 2, Tn, last_only=False)
     with torch.no_grad():
         ref = g(ids)
-    assert _rel(out.probs.view(2, 24, -1).cpu(), ref) < 0.15
+    assert _rel(out.probs.view(2, Tn, -1).cpu(), ref) < 0.15
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("norm,act", [(0, 0), (1, 0), (1, 3), (2, 0), (2, 2)])
+def test_linear_w8(M, norm, act):
+    """Weight-only fp8 skinny GEMM (e4m3 weights converted in registers, bf16
+    activations): vs the same algebra in fp32 on the dequantised weight (tight),
+    and vs fp32 norm + linear on the unquantised weight (fp8 tolerance).  K=1600
+    exercises the zero-padded weight rows (kpad 1664)."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8
+    from distributed_neural_networks_amd.ops.gemm import fold_norm, pack_gate_up
+    torch.manual_seed(11)
+    K, N = 1600, 2048
+    x = (torch.randn(M, K, device=DEV) + 0.3).bfloat16()
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    Wk = pack_gate_up(W[: N // 2], W[N // 2:]) if act == 3 else W
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = torch.randn(K, device=DEV) * 0.1 if norm == 2 else None
+    bias = torch.randn(N, device=DEV) * 0.1 if act != 3 else None
+    f = fold_norm(Wk, gamma if norm else torch.ones(K, device=DEV), beta, bias, norm == 1, 1e-5, DEV, fp8=True)
+    Nout = N // 2 if act == 3 else N
+    R = torch.randn(M, Nout, device=DEV).bfloat16() if act == 0 else None
+    out = torch.empty(M, Nout, device=DEV, dtype=torch.bfloat16)
+    linear_w8(x, f.w, f.bias, act, R, out, norm, f.colsum if norm else None, 1e-5)
+    xf = x.float()
+    wdq = f.w.q[:, :K].float() * f.w.scale[:, None]
+    if norm == 0:
+        y = xf @ wdq.t()
+    else:
+        mean = xf.mean(1, keepdim=True) if norm == 2 else torch.zeros_like(xf[:, :1])
+        var = xf.pow(2).mean(1, keepdim=True) - mean ** 2
+        y = xf @ wdq.t()
+        if norm == 2:
+            y = y - mean * f.colsum[None, :]
+        y = torch.rsqrt(var + 1e-5) * y
+    if f.bias is not None:
+        y = y + f.bias
+    # true reference: norm(x) @ W (no quantisation)
+    if norm == 0:
+        xn = xf
+    elif norm == 1:
+        xn = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma
+    else:
+        xn = F.layer_norm(xf, (K,), gamma, beta, 1e-5)
+    t = xn @ Wk.t() + (bias if bias is not None else 0)
+    if act == 3:
+        g_idx = torch.arange(N, device=DEV).view(-1, 16)[:, :8].reshape(-1)
+        u_idx = torch.arange(N, device=DEV).view(-1, 16)[:, 8:].reshape(-1)
+        y = F.silu(y[:, g_idx]) * y[:, u_idx]
+        t = F.silu(t[:, g_idx]) * t[:, u_idx]
+    elif act == 2:
+        y, t = F.gelu(y), F.gelu(t)
+    if R is not None:
+        y, t = y + R.float(), t + R.float()
+    assert _rel(out, y) < 1e-2, _rel(out, y)
+    assert _rel(out, t) < 6e-2, _rel(out, t)
 
 
 @pytest.mark.parametrize("M", [1, 16, 17, 48, 64])
