@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
 """Decode-GEMM (M <= 64) configuration sweep: achieved weight-stream GB/s per
 (column tiles NT, chunks in flight U, waves/WG KS, software pipeline) on the
-Llama-3 8B / GPT-2 shapes.  Weight copies are rotated so >= 1 GiB is streamed
-between reuses (the 256 MB MALL would otherwise serve repeats).
+Llama-3 8B / GPT-2 / GPT-2 XL projection shapes, for bf16 weights and for
+weight-only fp8 (``--w8``: e4m3 weights, bf16 activations).  Weight copies are
+rotated so >= 1 GiB is streamed between reuses (the 256 MB MALL would
+otherwise serve repeats, which a decode step never does).
 
-    python bench/skinny_sweep.py [--m 1,32] [--iters 20]
+    python bench/skinny_sweep.py [--m 1,32] [--w8 0,1] [--shapes llama,gpt2,gpt2xl] [--iters 20]
+
+One JSON line per (shape, M, w8): the auto-dispatch time and the best config;
+``csrc/kernels/gemm_skinny.hip`` launch_skinny's table is fitted to these.
 """
 from __future__ import annotations
 
@@ -18,27 +23,46 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096), (4800, 1600), (6400, 1600),
-          (1600, 6400), (50304, 1600)]
+SHAPES = {
+    "llama": [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)],
+    "gpt2": [(2304, 768), (768, 768), (3072, 768), (768, 3072)],
+    "gpt2xl": [(4800, 1600), (1600, 1600), (6400, 1600), (1600, 6400), (50304, 1600)],
+}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", default="1,32")
+    ap.add_argument("--w8", default="0")
+    ap.add_argument("--shapes", default="llama,gpt2xl")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import linear
     dev = torch.device("cuda", 0)
     L = lib()
-    for (N, K), M in itertools.product(SHAPES, [int(v) for v in args.m.split(",")]):
-        wbytes = N * K * 2
+    shapes = [s for k in args.shapes.split(",") for s in SHAPES[k]]
+    for (N, K), M, w8 in itertools.product(shapes, [int(v) for v in args.m.split(",")],
+                                           [int(v) for v in args.w8.split(",")]):
+        wbytes = N * K * (1 if w8 else 2)
         copies = max(2, min(64, (1 << 30) // wbytes + 1))
-        ws = [torch.randn(N, K, device=dev).bfloat16() for _ in range(copies)]
+        if w8:
+            ws = [quantize_weight(torch.randn(N, K, device=dev), dev) for _ in range(copies)]
+            sw = ws[0].scale
+            ldw = ws[0].q.shape[1]
+            wref = ws[0].q[:, :K].float() * ws[0].scale[:, None]
+        else:
+            ws = [torch.randn(N, K, device=dev).bfloat16() for _ in range(copies)]
+            sw, ldw = None, K
+            wref = ws[0].float()
         x = torch.randn(M, K, device=dev).bfloat16()
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ref = (x.float() @ ws[0].float().t())
-        res = {"M": M, "N": N, "K": K}
+        ref = x.float() @ wref.t()
+        res = {"M": M, "N": N, "K": K, "w8": w8}
+
+        def wptr(w):
+            return ptr(w.q) if w8 else ptr(w)
 
         def timed(fn):
             for i in range(3):
@@ -52,23 +76,29 @@ def main():
             torch.cuda.synchronize()
             return a.elapsed_time(b) / args.iters * 1e3  # us
 
-        us = timed(lambda w: linear(x, w, out=out))
+        if w8:
+            us = timed(lambda w: linear_w8(x, w, out=out))
+        else:
+            us = timed(lambda w: linear(x, w, out=out))
         res["auto_us"] = round(us, 2)
         res["auto_GBs"] = round(wbytes / us / 1e3, 1)
         best = None
         for nt, u, ks, pipe in itertools.product((1, 2, 4), (2, 4, 8), (2, 4, 8), (0, 1)):
             if nt == 4 and u == 8:
                 continue
-            rc = L.gemm_skinny_sweep(ptr(x), K, ptr(ws[0]), K, ptr(out), N, M, N, K, nt, u, ks, pipe, stream_ptr())
-            if rc != 0:
+
+            def run(w):
+                return L.gemm_skinny_sweep(ptr(x), K, wptr(w), ldw, ptr(sw if not w8 else w.scale), ptr(out), N, M,
+                                           N, K, nt, u, ks, pipe, w8, stream_ptr())
+
+            if run(ws[0]) != 0:
                 continue
             torch.cuda.synchronize()
             err = ((out.float() - ref).norm() / ref.norm()).item()
             if err > 2e-2:
                 res[f"bad_{nt}_{u}_{ks}_{pipe}"] = err
                 continue
-            us = timed(lambda w: L.gemm_skinny_sweep(ptr(x), K, ptr(w), K, ptr(out), N, M, N, K, nt, u, ks, pipe,
-                                                     stream_ptr()))
+            us = timed(run)
             res.setdefault("all", {})[f"{nt}/{u}/{ks}/{pipe}"] = round(us, 2)
             if best is None or us < best[0]:
                 best = (us, nt, u, ks, pipe)

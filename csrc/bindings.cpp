@@ -43,9 +43,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_skinny_w8(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, norm,
                               CFP(colsum), eps, ST(st));
   });
-  m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, int M, int N, int K, int nt, int u,
-                                int ks, int pipe, u64 st) {
-    return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, P(C), ldc, M, N, K, nt, u, ks, pipe, ST(st));
+  m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 sw, u64 C, int ldc, int M, int N, int K, int nt,
+                                int u, int ks, int pipe, int w8, u64 st) {
+    return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, M, N, K, nt, u, ks, pipe, w8, ST(st));
   });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
   m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {

@@ -7,8 +7,8 @@ extern "C" {
 int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias, const void* R,
                   int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st);
 int dnn_gemm_set_tile(int tile);
-int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K, int nt,
-                          int u, int ks, int pipe, hipStream_t st);
+int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc, int M,
+                          int N, int K, int nt, int u, int ks, int pipe, int w8, hipStream_t st);
 int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                          const void* R, int ldr, int M, int N, int K, int act, int norm, const float* colsum, float eps,
                          hipStream_t st);

@@ -298,9 +298,11 @@ using namespace dnn;
 // rotated past the 256 MB MALL):
 //   M <= 8     : 1 tile, 4 chunks in flight, 8 waves/WG (within 3% of the best
 //                config on every Llama-3 / GPT-2 XL shape)
-//   M <= 64    : wide N (>= 16K, the FFN and the LM head): 4 tiles x 2 chunks,
-//                2 waves; K >= 8K: 1 tile x 8 chunks, 2 waves; otherwise 2 tiles
-//                x 2 chunks, 4 waves (activation re-reads dominate as M grows)
+//   M <= 16    : wide N (>= 16K): 4 tiles x 2 chunks, 2 waves; else 2 tiles x 2
+//                chunks pipelined, 4 waves
+//   M <= 64    : by N class (wide >= 16K / mid / narrow <= 4K): 4 / 2 / 1 column
+//                tiles x 2 chunks, 4 waves (activation re-reads dominate as M
+//                grows, so narrow N keeps one column tile for more workgroups)
 template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
@@ -320,7 +322,6 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st, const float* colsum = nullptr, float eps = 0.f) {
   const bool wide = N >= 16384;
-  const bool deep = kbytes >= 16384;  // K >= 8K bf16
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
   return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
                                                                        ldr, M, N, kbytes, KSV, colsum, eps, st)
@@ -329,13 +330,21 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     if (wide) CFG(1, 4, 2, false, 2);
     CFG(1, 2, 2, true, 4);
   }
+  // M in (16, 64]: profiles/r1_skinny_sweep.jsonl + r1_skinny_sweep_m32_m64.jsonl
+  // (bf16 and W8 on the GPT-2 / GPT-2 XL / Llama-3 shapes), checked in the decode
+  // pipeline: wide N streams 4 column tiles on 2 waves, deep K (bf16 >= 8K) 1 tile
+  // x 8 chunks on 2 waves, narrow N one column tile on 4 waves (more workgroups)
+  const bool deep = kbytes >= 16384;
+  const bool narrow = N <= 4096;
   if (M <= 32) {
     if (wide) CFG(2, 4, 2, false, 2);
     if (deep) CFG(2, 1, 8, false, 2);
-    CFG(2, 2, 2, false, 4);
+    if (narrow) CFG(2, 1, 2, false, 4);
+    CFG(2, 2, 2, true, 4);
   }
   if (wide) CFG(4, 4, 2, false, 2);
   if (deep) CFG(4, 1, 8, false, 2);
+  if (narrow) CFG(4, 1, 2, false, 4);
   CFG(4, 2, 2, false, 4);
 #undef CFG
 }
@@ -414,35 +423,41 @@ extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw
   return -2;
 }
 
-// Configuration sweep for bench/gemm_bench.py --skinny (bf16, no epilogue ops):
-// nt in {1,2,4}, u in {2,4,8}, pipe in {0,1}; ks = waves per workgroup.
-template <int MT, int NT, int U, bool PIPE>
-static int skinny_sweep_launch(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
-                               int ks, hipStream_t st) {
+// Configuration sweep for bench/skinny_sweep.py (no epilogue ops): nt in
+// {1,2,4}, u in {2,4,8}, pipe in {0,1}; ks = waves per workgroup; w8 = fp8
+// weights (W8A16, sw = channel scales) instead of bf16.
+template <int MT, int NT, int U, bool PIPE, bool W8>
+static int skinny_sweep_launch(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
+                               int M, int N, int K, int ks, hipStream_t st) {
   const int groups = (N + 16 * NT - 1) / (16 * NT);
   const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE>), dim3(groups), dim3(64 * ks), smem,
-                     st, (const uint8_t*)A, lda * 2, nullptr, (const uint8_t*)W, ldw * 2, nullptr, C, ldc, nullptr,
-                     nullptr, 0, M, N, K * 2);
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE, NORM_NONE, W8>), dim3(groups),
+                     dim3(64 * ks), smem, st, (const uint8_t*)A, lda * 2, nullptr, (const uint8_t*)W,
+                     W8 ? ldw : ldw * 2, sw, C, ldc, nullptr, nullptr, 0, M, N, W8 ? K : K * 2, nullptr, 0.f);
   return (int)hipGetLastError();
 }
 
-template <int MT>
-static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
-                           int nt, int u, int ks, int pipe, hipStream_t st) {
-#define SW(NTV, UV)                                                                                     \
-  if (nt == NTV && u == UV)                                                                             \
-    return pipe ? skinny_sweep_launch<MT, NTV, UV, true>(A, lda, W, ldw, C, ldc, M, N, K, ks, st)      \
-                : skinny_sweep_launch<MT, NTV, UV, false>(A, lda, W, ldw, C, ldc, M, N, K, ks, st);
+template <int MT, bool W8>
+static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc, int M,
+                           int N, int K, int nt, int u, int ks, int pipe, hipStream_t st) {
+#define SW(NTV, UV)                                                                                               \
+  if (nt == NTV && u == UV)                                                                                       \
+    return pipe ? skinny_sweep_launch<MT, NTV, UV, true, W8>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st)        \
+                : skinny_sweep_launch<MT, NTV, UV, false, W8>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
   SW(1, 2) SW(1, 4) SW(1, 8) SW(2, 2) SW(2, 4) SW(2, 8) SW(4, 2) SW(4, 4)
 #undef SW
   return -2;
 }
 
-extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N,
-                                     int K, int nt, int u, int ks, int pipe, hipStream_t st) {
-  if (M <= 0 || M > 64 || (K * 2) % 64 != 0 || ks < 1 || ks > 8) return -1;
-  if (M <= 16) return skinny_sweep_mt<1>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
-  if (M <= 32) return skinny_sweep_mt<2>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
-  return skinny_sweep_mt<4>(A, lda, W, ldw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, const float* sw, void* C,
+                                     int ldc, int M, int N, int K, int nt, int u, int ks, int pipe, int w8,
+                                     hipStream_t st) {
+  if (M <= 0 || M > 64 || K % 64 != 0 || ks < 1 || ks > 8 || (w8 && sw == nullptr)) return -1;
+#define SWM(MTV)                                                                                  \
+  return w8 ? skinny_sweep_mt<MTV, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st) \
+            : skinny_sweep_mt<MTV, false>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+  if (M <= 16) SWM(1)
+  if (M <= 32) SWM(2)
+  SWM(4)
+#undef SWM
 }
