@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="images sourced per GPU per step")
-    ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--microbatches", type=int, default=2,
+                    help="microbatches per step on N>1 (2 x 32768 rows fill the fc1 GEMM's 256 tiles)")
     ap.add_argument("--placement", default="interleaved", choices=["interleaved", "linear"])
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
@@ -160,22 +161,33 @@ def bench_interleaved(args, info):
     probs = [torch.empty((mb, 10), device=dev) for _ in range(M)]
     splits = [0 if p == r else per_peer for p in range(N)]
 
+    # Steady-state streaming: the hop of the last microbatch of step k is
+    # drained after stage 0 of step k+1's first microbatch has been issued, so
+    # no hop is exposed between steps.  Buffer reuse is ordered by the work
+    # handles: a2a(i) is waited on before stage 1 of microbatch i, which precedes
+    # (in stream order) stage 0 of microbatch i of the next step.
+    pending = []
+
+    def drain():
+        while pending:
+            w, i = pending.pop(0)
+            w.wait()
+            s1.forward(rx[i], probs[i])
+
     def step():
-        works = []
         for i in range(M):
             s0.forward(xs[i], y0[i])
-            works.append(dist.all_to_all_single(rx[i], y0[i], splits, splits, async_op=True))
-            if i > 0:
-                works[i - 1].wait()
-                s1.forward(rx[i - 1], probs[i - 1])
-        works[M - 1].wait()
-        s1.forward(rx[M - 1], probs[M - 1])
+            w = dist.all_to_all_single(rx[i], y0[i], splits, splits, async_op=True)
+            drain()  # stage 1 of the previous microbatch (possibly of the previous step)
+            pending.append((w, i))
 
     for _ in range(args.warmup):
         step()
+    drain()
     t0 = sync_time(info)
     for _ in range(args.steps):
         step()
+    drain()
     t1 = sync_time(info)
     # latency: one image per peer through stage0 -> all-to-all -> stage1
     lx = torch.randn((N - 1, 3, 32, 32), device=dev, generator=g)
