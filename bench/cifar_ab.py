@@ -11,7 +11,8 @@ from distributed_neural_networks_amd.ops import cifar as cops
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    variants = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2").split(",")]
+    # a variant is "V" or "V@PT" (v3/v4: conv1 tiles run by the producer waves)
+    variants = (sys.argv[2] if len(sys.argv) > 2 else "3,4").split(",")
     torch.manual_seed(0)
     model = NeuralNetwork().eval()
     sd = model.state_dict()
@@ -22,8 +23,16 @@ def main():
     ref_mod.load_state_dict(sd, strict=False)
     with torch.no_grad():
         ref = ref_mod(x[:256].cpu())
+    from distributed_neural_networks_amd.ops._lib import lib
+
+    def run(v):
+        var, _, pt = v.partition("@")
+        if pt:
+            assert getattr(lib(), f"cifar_set_v{var}_pt")(int(pt)) == 0
+        cops.stage0_forward(x, w0, outs[v], variant=int(var))
+
     for v in variants:
-        cops.stage0_forward(x, w0, outs[v], variant=v)
+        run(v)
     torch.cuda.synchronize()
     for v in variants:
         err = ((outs[v][:256].float().cpu() - ref).norm() / ref.norm()).item()
@@ -34,7 +43,7 @@ def main():
         for v in variants:
             ev[0].record()
             for _ in range(5):
-                cops.stage0_forward(x, w0, outs[v], variant=v)
+                run(v)
             ev[1].record()
             torch.cuda.synchronize()
             times[v].append(ev[0].elapsed_time(ev[1]) / 5)

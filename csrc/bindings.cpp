@@ -57,6 +57,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("cifar_stage0_v2", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
     return dnn_cifar_stage0_v2(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
   });
+  m.def("cifar_stage0_v4", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
+    return dnn_cifar_stage0_v4(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
+  });
+  m.def("cifar_set_v4_pt", [](int pt) { return dnn_cifar_set_v4_pt(pt); });
+  m.def("cifar_set_v3_pt", [](int pt) { return dnn_cifar_set_v3_pt(pt); });
   m.def("cifar_stage0_v3", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
     return dnn_cifar_stage0_v3(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
   });

@@ -23,6 +23,10 @@ int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1
                      int B, int grid, hipStream_t st);
 int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
+int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
+                        int B, int grid, hipStream_t st);
+int dnn_cifar_set_v4_pt(int pt);
+int dnn_cifar_set_v3_pt(int pt);
 int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
 int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,

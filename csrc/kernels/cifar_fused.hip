@@ -458,16 +458,16 @@ constexpr int V3_A1_OFF = V2_XIN_BYTES;                                  // 1088
 constexpr int V3_OB_OFF = V3_A1_OFF + 2 * V2_A1_BYTES;                   // 80000
 constexpr int V3_OB_BYTES = 64 * V2_OBP;                                 // 8704
 constexpr int V3_LDS = V3_OB_OFF + 2 * V3_OB_BYTES;                      // 97408
-#ifndef DNN_V3_PT
-#define DNN_V3_PT 24
-#endif
-constexpr int V3_PT = DNN_V3_PT;  // conv1 tiles run by producer waves; the rest by consumers (balance, stamps)
+// conv1 tiles run by producer waves (the rest by consumers): a launch
+// argument so the producer/consumer balance can be A/B'd in one process
+// (bench/cifar_stamps.py --pt); default fitted from the phase stamps.
+static int g_v3_pt = 24;
 
 template <bool STAMPS>
 __global__ __launch_bounds__(512, 1) void cifar_stage0_v3_kernel(
     const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
     const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, int V3_PT) {
   __shared__ __attribute__((aligned(16))) char smem[V3_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -656,6 +656,181 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stage 0, v4: v3 with ONE barrier per image.  v3's phase A (input regs -> xin,
+// output staging -> global) ran on every wave with no MFMA in flight (~9 % of
+// an image by the s_memtime stamps).  Here the input image is double-buffered
+// in LDS, so producers stage image it+1 right after their conv1 tiles of image
+// it, and consumers copy out image it-2 before their conv2 of image it-1:
+//   iteration it:  P: conv1(it) [0,pt) <- xin[it&1];  regs(it+1) -> xin[(it+1)&1];  load regs(it+2)
+//                  C: obuf[it&1] -> out[it-2];  conv2(it-1) -> obuf[(it-1)&1];  conv1(it) [pt,32)
+//                  barrier
+// Every LDS buffer is written and read in different iterations (separated by
+// the barrier), or in disjoint halves of a double buffer within one.
+// ---------------------------------------------------------------------------
+constexpr int V4_XIN1_OFF = V3_LDS;                                      // second input buffer
+constexpr int V4_LDS = V4_XIN1_OFF + V2_XIN_BYTES;                       // 108288
+
+__global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
+    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
+    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B, int PT) {
+  __shared__ __attribute__((aligned(16))) char smem[V4_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave < 4;
+  const int rw = wave & 3;
+  const int rt = tid & 255;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int n = B > (int)blockIdx.x ? (B - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+
+  for (int i = tid; i < V3_OB_OFF / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < V2_XIN_BYTES / 16; i += 512)
+    reinterpret_cast<uint4*>(smem + V4_XIN1_OFF)[i] = make_uint4(0, 0, 0, 0);
+
+  bf16x8 w1f[3];
+  bf16x8 w2f[18];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 48 + s * 16 + h * 8);
+  const float bias1 = b1[r32];
+  float bias = 0.f;
+  int oc2 = 0;
+  if (!producer) {
+    oc2 = (rw & 1) * 32 + r32;
+#pragma unroll
+    for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
+    bias = b2[oc2];
+  }
+  resident_fence(w1f, bias1);
+  if (!producer) resident_fence(w2f, bias);
+  float pf[4][3];
+  auto load_img = [&](int k) {
+    const float* xb = x + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 3072;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pf[i][c] = xb[c * 1024 + rt + 256 * i];
+  };
+  auto stage_img = [&](char* xin) {  // prefetch registers -> padded HWC4 bf16 image
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = rt + 256 * i, yy = p >> 5, xx = p & 31;
+      uint2 v;
+      v.x = pack2bf(pf[i][0], pf[i][1]);
+      v.y = pack2bf(pf[i][2], 0.f);
+      *reinterpret_cast<uint2*>(xin + ((yy + 1) * V2_XW + xx + 1) * 8) = v;
+    }
+  };
+  auto xin_of = [&](int k) { return smem + ((k & 1) ? V4_XIN1_OFF : 0); };
+  __syncthreads();  // halos zeroed before any image is staged
+  if (producer && n > 0) {
+    load_img(0);
+    stage_img(xin_of(0));
+    if (n > 1) load_img(1);
+  }
+  __syncthreads();
+
+  const int c1_lane = ((r32 >> 3) * V2_XW + (r32 & 7) + 2 * h) * 8;
+  const int c2_lane = ((r32 >> 3) * V2_A1W + (r32 & 7)) * V2_A1P + h * 16;
+  const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
+  const int cb = r32 & ~3;
+
+  auto conv1_tile = [&](int t, const char* xin, char* a1) {
+    const int ty = t >> 2, tx = t & 3;
+    const char* abase = xin + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
+    }
+    float v[4];
+#pragma unroll
+    for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+      for (int qx = 0; qx < 2; ++qx) {
+        const int g0 = (2 * qy) * 4 + 2 * qx;
+        v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
+      }
+    const bool odd = r32 & 1;
+    const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
+    const float r0 = __int_as_float(dpp_xor1(s0)), r1 = __int_as_float(dpp_xor1(s1));
+    uint32_t u0, u1;
+    if (!odd) { u0 = pack2bf(v[0], r0); u1 = pack2bf(v[1], r1); }
+    else { u0 = pack2bf(r0, v[2]); u1 = pack2bf(r1, v[3]); }
+    const bool hi2 = r32 & 2;
+    const uint32_t rcv = (uint32_t)dpp_xor2((int)(hi2 ? u0 : u1));
+    const uint32_t mine = hi2 ? u1 : u0;
+    uint2 w;
+    w.x = hi2 ? rcv : mine;
+    w.y = hi2 ? mine : rcv;
+    const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
+    *reinterpret_cast<uint2*>(a1 + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
+  };
+  auto copy_out = [&](int k) {  // obuf[k&1] (64 channel rows x 128 B) -> out image k, coalesced 16-B stores
+    int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
+    const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = rt + 256 * u, ch = e >> 3, j = e & 7;
+      const uint2 a = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16);
+      const uint2 b = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16 + 8);
+      dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
+    }
+  };
+
+  for (int it = 0; it <= n; ++it) {
+    if (producer) {
+      if (it < n) {
+        char* a1 = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
+        const char* xin = xin_of(it);
+#pragma unroll 2
+        for (int t = rw; t < PT; t += 4) conv1_tile(t, xin, a1);
+        if (it + 1 < n) {
+          stage_img(xin_of(it + 1));
+          if (it + 2 < n) load_img(it + 2);
+        }
+      }
+    } else {
+      if (it >= 2) copy_out(it - 2);
+      if (it >= 1) {
+        const int k = it - 1;
+        const char* a1 = smem + V3_A1_OFF + (k & 1) * V2_A1_BYTES + c2_lane;
+        char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
+        f32x16 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
+        const int mt0 = (rw >> 1) * 4;
+        conv2_mainloop(a1, w2f, acc, mt0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
+#pragma unroll
+          for (int qy = 0; qy < 2; ++qy) {
+            float pv[2];
+#pragma unroll
+            for (int qx = 0; qx < 2; ++qx) {
+              const int g0 = (2 * qy) * 4 + 2 * qx;
+              pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias,
+                             0.f);
+            }
+            const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;
+            *reinterpret_cast<uint32_t*>(ob + oc2 * V2_OBP + (PY * 8 + PX) * 2) = pack2bf(pv[0], pv[1]);
+          }
+        }
+      }
+      if (it < n) {
+        char* a1w = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
+        const char* xin = xin_of(it);
+        for (int t = PT + rw; t < 32; t += 4) conv1_tile(t, xin, a1w);
+      }
+    }
+    __syncthreads();
+  }
+  if (!producer && n >= 1) copy_out(n - 1);
+}
+
 }  // namespace dnn
 
 using namespace dnn;
@@ -666,7 +841,7 @@ extern "C" int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, c
   if (grid <= 0) grid = 256;
   if (grid > B) grid = B;
   hipLaunchKernelGGL((cifar_stage0_v3_kernel<false>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
-                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, nullptr);
+                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, nullptr, g_v3_pt);
   return (int)hipGetLastError();
 }
 
@@ -677,8 +852,32 @@ extern "C" int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void*
   if (grid <= 0) grid = 256;
   if (grid > B) grid = B;
   hipLaunchKernelGGL((cifar_stage0_v3_kernel<true>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
-                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, stamps);
+                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, stamps, g_v3_pt);
   return (int)hipGetLastError();
+}
+
+static int g_v4_pt = 28;
+
+extern "C" int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
+                                   const float* b2, int B, int grid, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (grid <= 0) grid = 256;
+  if (grid > B) grid = B;
+  hipLaunchKernelGGL(cifar_stage0_v4_kernel, dim3(grid), dim3(512), 0, st, x, (bf16_t*)out, (const bf16_t*)w1p, b1,
+                     (const bf16_t*)w2p, b2, B, g_v4_pt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_cifar_set_v4_pt(int pt) {
+  if (pt < 0 || pt > 32 || pt % 4 != 0) return -1;
+  g_v4_pt = pt;
+  return 0;
+}
+
+extern "C" int dnn_cifar_set_v3_pt(int pt) {
+  if (pt < 0 || pt > 32 || pt % 4 != 0) return -1;
+  g_v3_pt = pt;
+  return 0;
 }
 
 extern "C" int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,

@@ -32,7 +32,7 @@ class CifarStage0Weights:
     w1p2: torch.Tensor = None  # v2: [32][48], k = ky*16 + kx*4 + c (kx<3, c<3 real)
 
 
-STAGE0_VARIANT = 3
+STAGE0_VARIANT = 4  # v4: single-barrier pipeline (csrc/kernels/cifar_fused.hip); 1-3 kept for A/B
 
 
 @dataclass
@@ -102,7 +102,10 @@ def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.T
     if tuple(out.shape) != (B, 4096) or out.dtype != torch.bfloat16 or not out.is_contiguous():
         raise ValueError("stage0: bad output buffer")
     v = variant or STAGE0_VARIANT
-    if v == 3:
+    if v == 4:
+        check(lib().cifar_stage0_v4(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
+                                    stream_ptr()), "cifar_stage0_v4")
+    elif v == 3:
         check(lib().cifar_stage0_v3(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
                                     stream_ptr()), "cifar_stage0_v3")
     elif v == 2:

@@ -129,7 +129,7 @@ def test_cifar_stage0_and_head(B):
     assert torch.equal(pred.cpu().long(), probs.cpu().argmax(1))
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_cifar_stage0_variants_agree(variant):
     from distributed_neural_networks_amd.models.cifar import NeuralNetwork, CifarStage
     from distributed_neural_networks_amd.ops import cifar as cops
