@@ -734,17 +734,10 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
   const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
   const int cb = r32 & ~3;
 
-  auto conv1_tile = [&](int t, const char* xin, char* a1) {
+  // bias + ReLU + 2x2 max-pool in registers, quad-DPP gather of 4 channels of
+  // one pooled pixel per lane, one 8-B store into act1
+  auto conv1_epi = [&](int t, const f32x16& acc, char* a1) {
     const int ty = t >> 2, tx = t & 3;
-    const char* abase = xin + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
-      const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
-      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
-    }
     float v[4];
 #pragma unroll
     for (int qy = 0; qy < 2; ++qy)
@@ -768,6 +761,44 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
     const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
     *reinterpret_cast<uint2*>(a1 + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
   };
+  auto conv1_tile = [&](int t, const char* xin, char* a1) {
+    const char* abase = xin + c1_lane + ((4 * (t >> 2)) * V2_XW + 8 * (t & 3)) * 8;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
+    }
+    conv1_epi(t, acc, a1);
+  };
+  // two conv1 tiles at once: all 12 A-fragment reads issued up front and the two
+  // accumulation chains interleaved, so one LDS latency and the MFMA result
+  // latency of one tile hide under the other's work (the producer wave shares
+  // its SIMD with a consumer wave; its stalls are the consumer's MFMA gaps)
+  auto conv1_pair = [&](int ta, int tb, const char* xin, char* a1) {
+    const char* pa = xin + c1_lane + ((4 * (ta >> 2)) * V2_XW + 8 * (ta & 3)) * 8;
+    const char* pb = xin + c1_lane + ((4 * (tb >> 2)) * V2_XW + 8 * (tb & 3)) * 8;
+    bf16x8 fa[3], fb[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(pa + s * V2_XW * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(pa + s * V2_XW * 8 + 8);
+      fa[s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      const uint2 lo2 = *reinterpret_cast<const uint2*>(pb + s * V2_XW * 8);
+      const uint2 hi2 = *reinterpret_cast<const uint2*>(pb + s * V2_XW * 8 + 8);
+      fb[s] = __builtin_bit_cast(bf16x8, make_uint4(lo2.x, lo2.y, hi2.x, hi2.y));
+    }
+    f32x16 acca = {}, accb = {};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      acca = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s], w1f[s], acca, 0, 0, 0);
+      accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], w1f[s], accb, 0, 0, 0);
+    }
+    conv1_epi(ta, acca, a1);
+    conv1_epi(tb, accb, a1);
+  };
   auto copy_out = [&](int k) {  // obuf[k&1] (64 channel rows x 128 B) -> out image k, coalesced 16-B stores
     int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
     const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
@@ -785,8 +816,9 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
       if (it < n) {
         char* a1 = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
         const char* xin = xin_of(it);
-#pragma unroll 2
-        for (int t = rw; t < PT; t += 4) conv1_tile(t, xin, a1);
+        int t = rw;
+        for (; t + 4 < PT; t += 8) conv1_pair(t, t + 4, xin, a1);
+        if (t < PT) conv1_tile(t, xin, a1);
         if (it + 1 < n) {
           stage_img(xin_of(it + 1));
           if (it + 2 < n) load_img(it + 2);
@@ -856,7 +888,7 @@ extern "C" int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void*
   return (int)hipGetLastError();
 }
 
-static int g_v4_pt = 28;
+static int g_v4_pt = 32;  // bench/cifar_ab.py: producers run all conv1 tiles (paired), consumers only conv2
 
 extern "C" int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
                                    const float* b2, int B, int grid, hipStream_t st) {
