@@ -23,6 +23,7 @@ import torch
 from ..parallel.links import P2PLink
 from ..utils import trace
 from .graph import GraphedStep
+from .ordering import SlotOrder
 from .stages import StageCompute, StageOutput
 
 
@@ -69,9 +70,11 @@ def run_stage_stream(stage: StageCompute, M: int, batch: int, prev: Optional[P2P
     out_slots = [torch.empty(oshp, dtype=odt, device=dev) for _ in range(depth)]
     rwork: List[object] = [None] * depth
     swork: List[object] = [None] * depth
+    ins, outs = SlotOrder("in_slots", depth), SlotOrder("out_slots", depth)  # DNN_DEBUG_ORDER=1 checks
     if prev is not None:
         for k in range(depth):
             rwork[k] = prev.irecv(in_slots[k])
+            ins.post(k, "recv", k)
     for i in range(M):
         k = i % depth
         if prev is None:
@@ -79,19 +82,28 @@ def run_stage_stream(stage: StageCompute, M: int, batch: int, prev: Optional[P2P
         else:
             with trace.span("recv_wait", "p2p", mb=i):
                 rwork[k].wait()
+            ins.waited(k)
+            ins.use(k, "stage input read", i)
             x = in_slots[k]
         if swork[k] is not None:
             with trace.span("slot_reuse_wait", "p2p", mb=i):
                 swork[k].wait()
             swork[k] = None
+            outs.waited(k)
+        outs.use(k, "stage output write", i)
         with trace.span("stage_forward", "compute", device=dev, mb=i):
             y = stage.forward(x, out_slots[k])
         if prev is not None and i + depth < M:
             rwork[k] = prev.irecv(in_slots[k])  # ordered after this slot's compute (see module doc)
+            ins.post(k, "recv", i + depth)
         if nxt is not None:
             swork[k] = nxt.isend(y if isinstance(y, torch.Tensor) else y.probs)
+            outs.post(k, "send", i)
         if sink is not None:
             sink(i, y)
-    for w in swork:
+    for k, w in enumerate(swork):
         if w is not None:
             w.wait()
+            outs.waited(k)
+    ins.drained()
+    outs.drained()

@@ -146,6 +146,7 @@ def test_cli_gpt2_tiny_gloo(tmp_path):
 
 
 def _worker_stream(rank, world, port, q):
+    os.environ["DNN_DEBUG_ORDER"] = "1"  # slot-ordering checks on (runtime/ordering.py)
     import torch.distributed as dist
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.models import cifar
