@@ -28,7 +28,22 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU (nanoGPT's nn.GELU()) without the branchy libm erff: with
+// z = |x|/sqrt2, erf(z) = 1 - t*P(t)*exp(-z^2), t = 1/(1 + p z) (Abramowitz &
+// Stegun 7.1.26, |error| <= 1.5e-7), so
+//   gelu(x) = x - q  (x >= 0),   q  (x < 0),   q = 0.5 x t P(t) exp(-x^2/2).
+// Straight-line: 1 v_rcp + 1 v_exp + ~10 FMA/MUL, no divergence in an epilogue.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);
+  const float q = 0.5f * x * (p * t) * e;
+  return x >= 0.f ? x - q : q;
+}
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 // DPP lane moves (VALU, no LDS round trip — __shfl_xor lowers to

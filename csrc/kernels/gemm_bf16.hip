@@ -116,6 +116,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
 
   // Epilogue (transposed accumulators): lane holds row m = .. + (lane&15), cols n..n+3.
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
+  const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -123,6 +124,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         epi_silu_t4<OUT_F32>(acc[i][j], m, (n0 + wn * 64 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
+    } else if (!OUT_F32 && pair) {
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int nb = n0 + wn * 64 + jp * 32;
+        if (nb + 31 < N)
+          epi_pair_bf16<ACT>(acc[i][2 * jp], acc[i][2 * jp + 1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias,
+                             R, ldr, lane);
+        else
+#pragma unroll
+          for (int j = 2 * jp; j < 2 * jp + 2; ++j)
+            epi_t4<ACT, OUT_F32>(acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr,
+                                 vec);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -284,6 +298,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
   //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
+  const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -296,6 +311,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             epi_silu_t4<OUT_F32>(acc[mq][nq][i][j], m, (nb + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
+        } else if (!OUT_F32 && pair && nb + 31 < N) {
+          epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
+                             bias, R, ldr, lane);
         } else {
 #pragma unroll
           for (int j = 0; j < 2; ++j)

@@ -61,6 +61,59 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
   }
 }
 
+// Widened bf16 store for two horizontally adjacent 16x16 transposed tiles
+// (columns nb..nb+15 in a0, nb+16..nb+31 in a1; lane row q = lane>>4 holds
+// columns 4q..4q+3 of each).  One v_permlane16_swap per dword pairs lane row
+// 0 with 1 and 2 with 3, after which every lane owns 8 contiguous columns:
+//   q=0: nb+0..7   q=1: nb+16..23   q=2: nb+8..15   q=3: nb+24..31
+// so the tile pair leaves as ONE 16-B store per lane instead of two 8-B
+// stores (guide T21: the epilogue tail is store-issue bound).  Preconditions
+// (wave-uniform, checked by the caller): nb + 31 < N, 16-B aligned C/ldc and
+// bias, 8-B aligned R rows.  Every lane must call it (cross-lane swap).
+template <int ACT>
+__device__ __forceinline__ void epi_pair_bf16(f32x4 a0, f32x4 a1, int m, int nb, int M, bf16_t* __restrict__ C,
+                                              int ldc, const float* __restrict__ bias,
+                                              const bf16_t* __restrict__ R, int ldr, int lane) {
+  const int q = lane >> 4;
+  const int n0 = nb + q * 4, n1 = n0 + 16;
+  if (bias != nullptr) {
+    a0 += *reinterpret_cast<const f32x4*>(bias + n0);
+    a1 += *reinterpret_cast<const f32x4*>(bias + n1);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (ACT == ACT_RELU) {
+      a0[r] = fmaxf(a0[r], 0.f);
+      a1[r] = fmaxf(a1[r], 0.f);
+    }
+    if (ACT == ACT_GELU) {
+      a0[r] = gelu_erf(a0[r]);
+      a1[r] = gelu_erf(a1[r]);
+    }
+  }
+  if (R != nullptr && m < M) {
+    const bf16x4 r0 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n0);
+    const bf16x4 r1 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      a0[r] += bf2f((bf16_t)r0[r]);
+      a1[r] += bf2f((bf16_t)r1[r]);
+    }
+  }
+  uint32_t x0 = pack2bf(a0[0], a0[1]), x1 = pack2bf(a0[2], a0[3]);
+  uint32_t y0 = pack2bf(a1[0], a1[1]), y1 = pack2bf(a1[2], a1[3]);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+  if (m >= M) return;
+  const int c = nb + ((q & 1) << 4) + ((q >> 1) << 3);
+  *reinterpret_cast<uint4*>(C + (size_t)m * ldc + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
+__device__ __forceinline__ bool epi_pair_ok(const void* C, int ldc, const float* bias, const bf16_t* R, int ldr) {
+  return ((uintptr_t)C & 15) == 0 && (ldc & 7) == 0 && ((uintptr_t)bias & 15) == 0 &&
+         ((uintptr_t)R & 7) == 0 && (R == nullptr || (ldr & 3) == 0);
+}
+
 // SwiGLU epilogue on a transposed accumulator tile of the packed gate|up
 // weight (ops/gemm.py pack_gate_up: 8 gate rows, then the 8 matching up rows):
 // lanes 0-31 hold gate columns, lanes 32-63 the up columns of the same outputs,

@@ -89,6 +89,38 @@ def test_gemm_asymmetric_layout():
     assert torch.equal(y, w.float().t())
 
 
+@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("n", [512, 520])
+def test_gemm_asymmetric_layout_bf16(tile, n):
+    """bf16 output takes the widened (permlane16-swapped, 16-B) store path; an
+    identity A with an asymmetric W pins every column of the swapped layout,
+    and n = 520 leaves a 32-column group that falls back to 8-B stores."""
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
+    k = 512
+    x = torch.eye(k, device=DEV).bfloat16()
+    w = torch.arange(n * k, device=DEV, dtype=torch.float32).reshape(n, k).remainder(97).bfloat16()
+    set_gemm_tile(tile)
+    try:
+        y = linear(x, w)
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_tile(0)
+    assert y.dtype == torch.bfloat16
+    assert torch.equal(y, w.t())
+
+
+def test_gemm_gelu_erf_accuracy():
+    """The branch-free erf GELU epilogue vs torch's exact-erf GELU, element-wise
+    (identity A, fp32 out): |error| must stay far below one bf16 ulp."""
+    from distributed_neural_networks_amd.ops.gemm import linear
+    n = 256
+    x = torch.eye(n, device=DEV).bfloat16()
+    w = torch.linspace(-12, 12, n * n, device=DEV).reshape(n, n).bfloat16()
+    y = linear(x, w, act=2, out_dtype=torch.float32)
+    ref = torch.nn.functional.gelu(w.float().t())
+    assert (y - ref).abs().max().item() < 2e-6 * 12
+
+
 def test_gemm_silu_mul():
     from distributed_neural_networks_amd.ops.gemm import linear, pack_gate_up
     torch.manual_seed(1)
