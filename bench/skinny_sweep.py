@@ -8,6 +8,8 @@ otherwise serve repeats, which a decode step never does).
 
     python bench/skinny_sweep.py [--m 1,32] [--w8 0,1] [--shapes llama,gpt2,gpt2xl] [--iters 20]
 
+Configs: pipe bit 0 = software pipeline, bit 1 = M split (one 16-row tile per
+workgroup).  Kernels are timed as HIP-graph replays (device time per launch).
 One JSON line per (shape, M, w8): the auto-dispatch time and the best config;
 ``csrc/kernels/gemm_skinny.hip`` launch_skinny's table is fitted to these.
 """
@@ -65,16 +67,25 @@ def main():
             return ptr(w.q) if w8 else ptr(w)
 
         def timed(fn):
+            # One HIP graph of `iters` launches (rotating weight copies), replayed:
+            # the device time per kernel, as in the decode graphs, without the
+            # ~7 us per-call Python/launch floor of an eager loop.
             for i in range(3):
                 fn(ws[i % copies])
             torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(args.iters):
+                    fn(ws[i % copies])
+            g.replay()
+            torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            for i in range(args.iters):
-                fn(ws[i % copies])
+            for _ in range(3):
+                g.replay()
             b.record()
             torch.cuda.synchronize()
-            return a.elapsed_time(b) / args.iters * 1e3  # us
+            return a.elapsed_time(b) / (3 * args.iters) * 1e3  # us
 
         if w8:
             us = timed(lambda w: linear_w8(x, w, out=out))
@@ -83,9 +94,11 @@ def main():
         res["auto_us"] = round(us, 2)
         res["auto_GBs"] = round(wbytes / us / 1e3, 1)
         best = None
-        for nt, u, ks, pipe in itertools.product((1, 2, 4), (2, 4, 8), (2, 4, 8), (0, 1)):
+        for nt, u, ks, pipe in itertools.product((1, 2, 4), (2, 4, 8), (2, 4, 8), (0, 1, 2, 3)):
             if nt == 4 and u == 8:
                 continue
+            if pipe >= 2 and M <= 16:
+                continue  # M split (pipe bit 1) only splits M > 16
 
             def run(w):
                 return L.gemm_skinny_sweep(ptr(x), K, wptr(w), ldw, ptr(sw if not w8 else w.scale), ptr(out), N, M,

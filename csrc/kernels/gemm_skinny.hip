@@ -79,7 +79,7 @@ __device__ __forceinline__ void sk_stats(const i32x4& a, float& s1, float& s2) {
 }
 
 template <int ACT, bool OUT_F32, int MT, int NT, bool FP8, int U, bool PIPE = false, int NORM = NORM_NONE,
-          bool W8 = false>
+          bool W8 = false, bool MS = false>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                            const float* __restrict__ sa, const uint8_t* __restrict__ W,
                                                            int ldw_b, const float* __restrict__ sw,
@@ -94,7 +94,26 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   constexpr int ACH = W8 ? 128 : 64;    // A bytes per row per chunk
   extern __shared__ __attribute__((aligned(16))) f32x4 sk_red[];  // [KS][NT*MT][64], then [KS][MT][16] x2 stats
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, KS = blockDim.x >> 6;
-  const int n0 = blockIdx.x * (16 * NT);
+  // MS (M split): one workgroup per (column tile, 16-row M tile), so M = 32..64
+  // runs 2-4x the workgroups (narrow N, e.g. GPT-2's 768-wide projections, has
+  // too few column tiles to fill 256 CUs otherwise).  The M tiles of a column
+  // tile are consecutive logical ids on one XCD, so its weight slice is read
+  // from HBM once and re-read from that XCD's L2.
+  int n0;
+  if constexpr (MS) {
+    static_assert(MT == 1, "MS: one M tile per workgroup");
+    const int mtiles = (M + 15) >> 4;
+    const int lgc = xcd_remap(blockIdx.x, gridDim.x);
+    const int mo = (lgc % mtiles) * 16;
+    n0 = (lgc / mtiles) * (16 * NT);
+    A += (size_t)mo * lda_b;
+    if (sa != nullptr) sa += mo;
+    Cv = reinterpret_cast<char*>(Cv) + (size_t)mo * ldc * (OUT_F32 ? 4 : 2);
+    if (R != nullptr) R += (size_t)mo * ldr;
+    M = min(16, M - mo);
+  } else {
+    n0 = blockIdx.x * (16 * NT);
+  }
   const int lg = (lane >> 4) * 16;  // byte offset of this lane group inside a 64-B chunk
 
   const uint8_t* wp[NT];
@@ -303,15 +322,15 @@ using namespace dnn;
 //   M <= 64    : by N class (wide >= 16K / mid / narrow <= 4K): 4 / 2 / 1 column
 //                tiles x 2 chunks, 4 waves (activation re-reads dominate as M
 //                grows, so narrow N keeps one column tile for more workgroups)
-template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8>
+template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8, bool MS = false>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                              int ks, const float* colsum, float eps, hipStream_t st) {
-  const int groups = (N + 16 * NT - 1) / (16 * NT);
+  const int groups = (N + 16 * NT - 1) / (16 * NT) * (MS ? (M + 15) / 16 : 1);
   while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
   size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
   if (NORM != NORM_NONE) smem += (size_t)ks * MT * 2 * 16 * sizeof(float);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8>), dim3(groups), dim3(64 * ks), smem,
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8, MS>), dim3(groups), dim3(64 * ks), smem,
                      st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
                      ldr, M, N, kbytes, colsum, eps);
   return (int)hipGetLastError();
@@ -334,6 +353,18 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   // (bf16 and W8 on the GPT-2 / GPT-2 XL / Llama-3 shapes), checked in the decode
   // pipeline: wide N streams 4 column tiles on 2 waves, deep K (bf16 >= 8K) 1 tile
   // x 8 chunks on 2 waves, narrow N one column tile on 4 waves (more workgroups)
+  // M split (one 16-row tile per workgroup) where the column tiles alone are
+  // too few for 256 CUs: graph-timed sweep profiles/r1_skinny_sweep_ms.jsonl —
+  // GPT-2 N=768: 5.8 -> 3.8 us (K=768), 15.9 -> 8.3 us (K=3072) at M=64;
+  // GPT-2 XL W8 N=1600: 9.8 -> 7.0 / 28.5 -> 16.0 us; Llama W8 N=4096 at M=32.
+#define CFG_MS(NTV)                                                                                           \
+  return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, 2, true, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
+                                                                            R, ldr, M, N, kbytes, 4, colsum, eps, st)
+  if (!FP8) {
+    if (N <= 1024) CFG_MS(1);
+    if (N <= 2048 || (W8 && N <= 4096)) CFG_MS(2);
+  }
+#undef CFG_MS
   const bool deep = kbytes >= 16384;
   const bool narrow = N <= 4096;
   if (M <= 32) {
@@ -426,12 +457,12 @@ extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw
 // Configuration sweep for bench/skinny_sweep.py (no epilogue ops): nt in
 // {1,2,4}, u in {2,4,8}, pipe in {0,1}; ks = waves per workgroup; w8 = fp8
 // weights (W8A16, sw = channel scales) instead of bf16.
-template <int MT, int NT, int U, bool PIPE, bool W8>
+template <int MT, int NT, int U, bool PIPE, bool W8, bool MS = false>
 static int skinny_sweep_launch(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                                int M, int N, int K, int ks, hipStream_t st) {
-  const int groups = (N + 16 * NT - 1) / (16 * NT);
+  const int groups = (N + 16 * NT - 1) / (16 * NT) * (MS ? (M + 15) / 16 : 1);
   const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE, NORM_NONE, W8>), dim3(groups),
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE, NORM_NONE, W8, MS>), dim3(groups),
                      dim3(64 * ks), smem, st, (const uint8_t*)A, lda * 2, nullptr, (const uint8_t*)W,
                      W8 ? ldw : ldw * 2, sw, C, ldc, nullptr, nullptr, 0, M, N, W8 ? K : K * 2, nullptr, 0.f);
   return (int)hipGetLastError();
@@ -449,10 +480,28 @@ static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, const
   return -2;
 }
 
+template <bool W8>
+static int skinny_sweep_ms(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc, int M,
+                           int N, int K, int nt, int u, int ks, int pipe, hipStream_t st) {
+#define SW(NTV, UV)                                                                                                  \
+  if (nt == NTV && u == UV)                                                                                          \
+    return pipe ? skinny_sweep_launch<1, NTV, UV, true, W8, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st)      \
+                : skinny_sweep_launch<1, NTV, UV, false, W8, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
+  SW(1, 2) SW(1, 4) SW(1, 8) SW(2, 2) SW(2, 4) SW(2, 8) SW(4, 2) SW(4, 4)
+#undef SW
+  return -2;
+}
+
+// pipe bit 0: software pipeline; bit 1: M split (MS)
 extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, const float* sw, void* C,
                                      int ldc, int M, int N, int K, int nt, int u, int ks, int pipe, int w8,
                                      hipStream_t st) {
   if (M <= 0 || M > 64 || K % 64 != 0 || ks < 1 || ks > 8 || (w8 && sw == nullptr)) return -1;
+  if (pipe & 2) {  // M split: one 16-row tile per workgroup
+    pipe &= 1;
+    return w8 ? skinny_sweep_ms<true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st)
+              : skinny_sweep_ms<false>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+  }
 #define SWM(MTV)                                                                                  \
   return w8 ? skinny_sweep_mt<MTV, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st) \
             : skinny_sweep_mt<MTV, false>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st);
