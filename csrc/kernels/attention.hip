@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const int qrow = qrow0 + r32;                        // this lane's query
   const int q_abs = p0 + min(qrow, T - 1);
   const int wave_qmax = p0 + min(qrow0 + 31, T - 1);   // wave-uniform
+  const int wave_qmin = p0 + min(qrow0, T - 1);
   const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
   const int kv_end = min(min(kv_len, blk_qmax + 1), S);  // never read past the cache
 
@@ -159,27 +160,34 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
         }
       }
       // ---- mask + online softmax (lane = one query; keys in registers) ----
+      // VALU is the bound at hd 64 (2 x 8 MFMAs per 64 keys vs ~5 VALU slots per
+      // score), so: the mask only runs on blocks that cross this wave's diagonal
+      // or the cache end; the max is taken on raw scores (scale > 0), 3-input;
+      // the scale folds into the exponent's FMA; v_exp_f32 directly.
+      if (kb0 + FA_KB - 1 > wave_qmin || kb0 + FA_KB > kv_len) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int key = kb0 + kt * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+            if (key > q_abs || key >= kv_len) sacc[kt][g] = -INFINITY;
+          }
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int key = kb0 + kt * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-          float v = sacc[kt][g] * scale_log2;
-          if (key > q_abs || key >= kv_len) v = -INFINITY;
-          sacc[kt][g] = v;
-          mx = fmaxf(mx, v);
-        }
+        for (int g = 0; g < 16; g += 2) mx = fmaxf(mx, fmaxf(sacc[kt][g], sacc[kt][g + 1]));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
+      const float m_new = fmaxf(m_i, mx * scale_log2);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_i - m_use);
+      const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          const float pv = exp2f(sacc[kt][g] - m_use);
+          const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[kt][g], scale_log2, -m_use));
           sacc[kt][g] = pv;
           rs += pv;
         }

@@ -359,8 +359,10 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
     return;
   }
   // Auto choice by wave quantisation: the 256^2 kernel runs 1 block/CU (256
-  // slots) and is ~1.25x the 128^2 kernel (2 blocks/CU, 512 slots) per slot
-  // when both fill the chip (bench/gemm_bench.py, profiles/).
+  // slots) and is ~1.3x the 128^2 kernel (2 blocks/CU, 512 slots) per slot
+  // when both fill the chip; 1.4 also sends M=32768 N=768 (1.5 waves of 256^2
+  // tiles) to the 256^2 kernel, 6 % faster at K=3072 and equal at K=768
+  // (profiles/r1_gemm_bench_v2_widened_epilogue.jsonl).
   const int tiles256 = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
   const int tiles128 = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
   auto fill = [](int tiles, int slots) {
@@ -368,7 +370,7 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
     return (double)tiles / ((double)waves * slots);
   };
   const bool big = g_gemm_tile == 256 ||
-                   (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.25 * fill(tiles256, 256) > fill(tiles128, 512));
+                   (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.4 * fill(tiles256, 256) > fill(tiles128, 512));
   if (big) {
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
                        (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);

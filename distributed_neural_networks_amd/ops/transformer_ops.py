@@ -4,6 +4,7 @@ only ever launched with the operand shapes its grid assumes."""
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -76,10 +77,15 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
 
 
 def decode_splits(S: int, B: int, Hkv: int) -> int:
-    """Split-K factor for decode attention: enough workgroups for ~4 per CU
-    (1024), at most one split per 256 keys of cache capacity.  Each split takes
+    """Split-K factor for decode attention: one split once B*Hkv alone gives 2
+    workgroups per CU; else enough workgroups for ~4 per CU (1024), at most one
+    split per 256 keys of cache capacity.  Each split takes
     ``ceil(len/splits)`` of the *runtime* length, so short contexts stay
     balanced; with one split the kernel writes the output itself (no combine)."""
+    if os.environ.get("DNN_DECODE_SPLITS"):  # A/B override
+        return max(1, int(os.environ["DNN_DECODE_SPLITS"]))
+    if B * Hkv >= 512:  # >= 2 workgroups per CU already: the combine pass costs more than it hides
+        return 1          # (GPT-2 B=64: 0.754 -> 0.703 ms/step, profiles/r1_decode_benches_v6.jsonl)
     want = max(1, -(-1024 // max(1, B * Hkv)))
     return max(1, min(want, -(-S // 256)))  # >= 256 keys per split: short contexts skip the combine pass
 

@@ -1,0 +1,7 @@
+# tile-choice factor 1.4 + decode splits rule: GEMM/transformer tests, GPT-2 bench, Llama B=32.
+mkdir -p gpurun_out
+export PYTHONPATH=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/v7_tests.log 2>&1; rc=$?; tail -3 gpurun_out/v7_tests.log; [ $rc -eq 0 ] &&
+timeout -k 10 300 python bench/gpt_bench.py --batch 64 --prompt 512 --steps 32 > gpurun_out/v7_gpt2.log 2>&1 && tail -1 gpurun_out/v7_gpt2.log &&
+timeout -k 10 400 python bench/gpt_bench.py --model llama3-8b --stages 8 --batch 32 --prompt 512 --steps 16 > gpurun_out/v7_llama.log 2>&1 && tail -1 gpurun_out/v7_llama.log &&
+timeout -k 10 400 python bench/gpt_bench.py --model gpt2-xl --stages 8 --dtype fp8 --batch 64 --prompt 512 --steps 32 > gpurun_out/v7_xl.log 2>&1 && tail -1 gpurun_out/v7_xl.log
