@@ -85,6 +85,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_qkv_split(CP(qkv), P(q), P(kc), P(vc), B, T, H, Hkv, hd, S, CIP(pos), CFP(cos), CFP(sin), rope,
                          ST(st));
   });
+  m.def("flash_attn_qkv", [](u64 qkv, int ldqkv, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S,
+                             u64 pos, float scale, u64 st) {
+    return dnn_flash_attn_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));
+  });
   m.def("flash_attn", [](u64 q, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
                          float scale, u64 st) {
     return dnn_flash_attn(CP(q), CP(kc), CP(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));

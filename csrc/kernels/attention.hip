@@ -92,11 +92,18 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
   return HD == 64 ? (chunk ^ ((key >> 1) & 7)) : (chunk ^ (key & 15));
 }
 
-template <int HD>
+// QKV: q is the c_attn output itself (rows b*T+t, row stride ldq, columns
+// [q H*hd | k Hkv*hd | v Hkv*hd], no RoPE): Q and the chunk's own keys/values
+// (positions >= pos[b]) are read straight from it, older keys from the cache,
+// and the first query head of each kv group copies its 128-row slice of new
+// K/V into the cache — the qkv_split launch and its round trip disappear.
+template <int HD, bool QKV = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
-                                                            float scale_log2) {
+                                                            float scale_log2, int ldq = 0,
+                                                            bf16_t* __restrict__ kc_out = nullptr,
+                                                            bf16_t* __restrict__ vc_out = nullptr) {
   using SM = FaSmem<HD>;
   __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL];
   char* ks = smem;
@@ -118,10 +125,31 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
   const int kv_end = min(min(kv_len, blk_qmax + 1), S);  // never read past the cache
 
+  const bf16_t* krow_new = nullptr;  // QKV: this sequence's new-key rows (position p0 + t = row b*T + t)
+  const bf16_t* vrow_new = nullptr;
+  if constexpr (QKV) {
+    krow_new = q + (size_t)b * T * ldq + (size_t)(H + kvh) * HD;
+    vrow_new = q + (size_t)b * T * ldq + (size_t)(H + Hkv + kvh) * HD;
+    if (hh % (H / Hkv) == 0) {  // cache write of rows t in [qb*128, qb*128+128), once per kv head
+      bf16_t* kd = kc_out + ((size_t)b * Hkv + kvh) * S * HD;
+      bf16_t* vd = vc_out + ((size_t)b * Hkv + kvh) * S * HD;
+      for (int e = tid; e < FA_QB * CH; e += 256) {
+        const int t = qb * FA_QB + e / CH, c = e % CH;
+        if (t < T && p0 + t < S) {
+          *reinterpret_cast<uint4*>(kd + (size_t)(p0 + t) * HD + c * 8) =
+              *reinterpret_cast<const uint4*>(krow_new + (size_t)t * ldq + c * 8);
+          *reinterpret_cast<uint4*>(vd + (size_t)(p0 + t) * HD + c * 8) =
+              *reinterpret_cast<const uint4*>(vrow_new + (size_t)t * ldq + c * 8);
+        }
+      }
+    }
+  }
+
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[qrow][ks*16 + 8h + j]
   bf16x8 qf[NKS];
   {
-    const bf16_t* qp = q + (((size_t)b * H + hh) * T + min(qrow, T - 1)) * HD + 8 * h;
+    const bf16_t* qp = QKV ? q + ((size_t)b * T + min(qrow, T - 1)) * ldq + (size_t)hh * HD + 8 * h
+                           : q + (((size_t)b * H + hh) * T + min(qrow, T - 1)) * HD + 8 * h;
 #pragma unroll
     for (int s = 0; s < NKS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + s * 16);
   }
@@ -140,8 +168,14 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       const int e = it * 256 + tid;
       const int key = e / CH, c = e % CH;
       const int kk = min(kb0 + key, kv_len - 1);
-      const uint4 kv = *reinterpret_cast<const uint4*>(kbase + (size_t)kk * HD + c * 8);
-      const uint4 vv = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + c * 8);
+      uint4 kv, vv;
+      if (QKV && kk >= p0) {
+        kv = *reinterpret_cast<const uint4*>(krow_new + (size_t)(kk - p0) * ldq + c * 8);
+        vv = *reinterpret_cast<const uint4*>(vrow_new + (size_t)(kk - p0) * ldq + c * 8);
+      } else {
+        kv = *reinterpret_cast<const uint4*>(kbase + (size_t)kk * HD + c * 8);
+        vv = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + c * 8);
+      }
       *reinterpret_cast<uint4*>(ks + key * HD * 2 + (k_swz<HD>(key, c) << 4)) = kv;
       *reinterpret_cast<uint4*>(vs + key * SM::V_STRIDE + c * 16) = vv;
     }
@@ -499,6 +533,24 @@ extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, voi
   } else if (hd == 128) {
     hipLaunchKernelGGL((flash_attn_kernel<128>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
                        (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+  } else {
+    return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+// Prefill straight from the c_attn output (no RoPE): see flash_attn_kernel<HD, true>.
+extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H,
+                                  int Hkv, int hd, int S, const int* pos, float scale, hipStream_t st) {
+  if (H % Hkv != 0 || ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
+  dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (hd == 64) {
+    hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)kc,
+                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc, (bf16_t*)vc);
+  } else if (hd == 128) {
+    hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)kc,
+                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc, (bf16_t*)vc);
   } else {
     return -2;
   }

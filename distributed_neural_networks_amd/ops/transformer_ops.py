@@ -76,6 +76,26 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
     return out
 
 
+def flash_attn_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,
+                   Hkv: int, hd: int, pos: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
+    """Causal prefill straight from the c_attn output (no RoPE): qkv (B*T, ld)
+    rows [q | k | v]; the new keys/values are written into the cache rows
+    pos[b].. as a side effect (what qkv_split would have done)."""
+    if hd not in (64, 128):
+        raise ValueError(f"flash_attn_qkv: head_dim {hd} unsupported (64/128)")
+    S = kc.shape[2]
+    if kc.shape[:2] != (B, Hkv) or kc.shape[3] != hd or vc.shape != kc.shape:
+        raise ValueError(f"flash_attn_qkv: cache {tuple(kc.shape)} does not match B={B} Hkv={Hkv} hd={hd}")
+    if qkv.dim() != 2 or qkv.shape[0] < B * T or qkv.shape[1] < (H + 2 * Hkv) * hd or qkv.stride(1) != 1:
+        raise ValueError(f"flash_attn_qkv: qkv {tuple(qkv.shape)} too small")
+    if not (kc.is_contiguous() and vc.is_contiguous()):
+        raise ValueError("flash_attn_qkv: cache slices must be contiguous")
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    check(lib().flash_attn_qkv(ptr(qkv), qkv.stride(0), ptr(kc), ptr(vc), ptr(out), B, T, H, Hkv, hd, S, ptr(pos),
+                               scale, stream_ptr()), "flash_attn_qkv")
+    return out
+
+
 def decode_splits(S: int, B: int, Hkv: int) -> int:
     """Split-K factor for decode attention: one split once B*Hkv alone gives 2
     workgroups per CU; else enough workgroups for ~4 per CU (1024), at most one

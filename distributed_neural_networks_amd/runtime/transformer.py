@@ -232,6 +232,8 @@ class TransformerStage(StageCompute):
             if T == 1:  # decode: split/RoPE/cache write fused into the attention launch
                 T_.attn_decode_qkv(qkv, kc, vc, att, B, self.H, self.Hkv, self.hd, pos, self.ws, self.splits,
                                    self.cos, self.sin)
+            elif self.cos is None:  # no RoPE (GPT-2): attention reads the c_attn output directly
+                T_.flash_attn_qkv(qkv, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
             else:
                 T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)

@@ -89,6 +89,33 @@ def test_qkv_split_flash(B, Tn, H, Hkv, hd, pos0):
     assert _rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,Tn,H,Hkv,hd,pos0", [(2, 64, 4, 4, 64, 0), (1, 200, 12, 12, 64, 0), (2, 77, 8, 2, 128, 0),
+                                                 (1, 33, 4, 1, 128, 40), (3, 130, 2, 2, 64, 17), (2, 300, 4, 2, 64, 250)])
+def test_flash_attn_qkv_matches_split(B, Tn, H, Hkv, hd, pos0):
+    """Prefill straight from the c_attn output (no qkv_split): identical output
+    and identical cache contents to qkv_split + flash_attn, including chunked
+    prefill (pos0 > 0: older keys from the cache, new ones from qkv) and GQA;
+    S is one short of pos0+Tn in the last case, so the overflow is dropped."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(3)
+    S = pos0 + Tn + 16 if pos0 != 250 else pos0 + Tn - 1
+    kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv = torch.randn(B * Tn, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    pos = torch.full((B,), pos0, device=DEV, dtype=torch.int32)
+    q = torch.empty(B * H * Tn * hd, device=DEV, dtype=torch.bfloat16)
+    T.qkv_split(qkv, q, kc, vc, B, Tn, H, Hkv, hd, pos)
+    ref = torch.empty(B * Tn, H * hd, device=DEV, dtype=torch.bfloat16)
+    T.flash_attn(q, kc, vc, ref, B, Tn, H, Hkv, hd, pos)
+    out = torch.empty_like(ref)
+    T.flash_attn_qkv(qkv, kc2, vc2, out, B, Tn, H, Hkv, hd, pos)
+    torch.cuda.synchronize()
+    assert torch.equal(kc2, kc) and torch.equal(vc2, vc)
+    rows = torch.arange(B * Tn, device=DEV) % Tn + pos0 < S  # queries past the cache attend a clipped prefix
+    assert torch.equal(out[rows], ref[rows])
+
+
 def test_flash_attn_spike_rescale():
     """Force the online-softmax rescale: one huge key score late in the sequence (guide §5.4 rule 26)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
