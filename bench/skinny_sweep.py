@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--w8", default="0")
     ap.add_argument("--shapes", default="llama,gpt2xl")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--pipes", default="0,1,2,3", help="pipe codes: bit0 pipeline, bit1 M split, bit2 shuffled W")
+    ap.add_argument("--shuf", action="store_true", help="also build pre-shuffled weight copies (pipe bit 2)")
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
@@ -94,14 +96,22 @@ def main():
         res["auto_us"] = round(us, 2)
         res["auto_GBs"] = round(wbytes / us / 1e3, 1)
         best = None
-        for nt, u, ks, pipe in itertools.product((1, 2, 4), (2, 4, 8), (2, 4, 8), (0, 1, 2, 3)):
+        shuf = {}
+        if args.shuf:
+            from distributed_neural_networks_amd.ops.gemm import shuffle_weight
+            shuf = {id(w): shuffle_weight(w.q[:, :K] if w8 else w) for w in ws}
+        pipes = [int(p) for p in args.pipes.split(",")]
+        for nt, u, ks, pipe in itertools.product((1, 2, 4), (2, 4, 8), (2, 4, 8), pipes):
             if nt == 4 and u == 8:
                 continue
-            if pipe >= 2 and M <= 16:
+            if pipe & 2 and M <= 16:
                 continue  # M split (pipe bit 1) only splits M > 16
+            if pipe & 4 and not args.shuf:
+                continue
 
-            def run(w):
-                return L.gemm_skinny_sweep(ptr(x), K, wptr(w), ldw, ptr(sw if not w8 else w.scale), ptr(out), N, M,
+            def run(w, pipe=pipe, nt=nt, u=u, ks=ks):
+                wp = ptr(shuf[id(w)]) if pipe & 4 else wptr(w)
+                return L.gemm_skinny_sweep(ptr(x), K, wp, ldw, ptr(sw if not w8 else w.scale), ptr(out), N, M,
                                            N, K, nt, u, ks, pipe, w8, stream_ptr())
 
             if run(ws[0]) != 0:

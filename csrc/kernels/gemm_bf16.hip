@@ -353,9 +353,9 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
-                        const void* R, int ldr, int M, int N, int K, hipStream_t st) {
+                        const void* R, int ldr, int M, int N, int K, hipStream_t st, const void* Wsh) {
   if (M <= 64) {  // decode-sized: weight-streaming skinny kernels (gemm_skinny.hip)
-    dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st);
+    dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh);
     return;
   }
   // Auto choice by wave quantisation: the 256^2 kernel runs 1 block/CU (256
@@ -381,12 +381,13 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
 }
 
 extern "C" int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
-                             const void* R, int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st) {
+                             const void* R, int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st,
+                             const void* Wsh) {
   if (K % 64 != 0 || M <= 0 || N <= 0) return -1;
 #define DISPATCH(a)                                                                     \
   if (act == a) {                                                                       \
-    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st); \
-    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st);        \
+    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh); \
+    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh);        \
     return (int)hipGetLastError();                                                      \
   }
   DISPATCH(ACT_NONE)

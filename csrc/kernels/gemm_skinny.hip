@@ -87,7 +87,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
                                                            const float* __restrict__ bias,
                                                            const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                            int kbytes, const float* __restrict__ colsum = nullptr,
-                                                           float eps = 0.f) {
+                                                           float eps = 0.f, const uint8_t* __restrict__ Wsh = nullptr) {
   static_assert(NORM == NORM_NONE || !FP8, "fused norm needs bf16 activations");
   static_assert(!(FP8 && W8), "W8 = fp8 weights with bf16 activations; FP8 = both fp8");
   constexpr int AU = W8 ? 2 : 1;        // 16-B A loads per chunk per M tile (W8: a chunk is 64 k = 128 B of A)
@@ -116,12 +116,27 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   }
   const int lg = (lane >> 4) * 16;  // byte offset of this lane group inside a 64-B chunk
 
+  // Wsh != nullptr: W pre-shuffled into MFMA fragment order (ops/gemm.py
+  // shuffle_weight): the 16 rows x 64 B of (column tile, chunk) are one
+  // contiguous 1 KiB block, lane l's 16 B at l*16, the blocks of one column tile
+  // consecutive along K — every wave load is a contiguous 1 KiB and a batch of U
+  // chunks one U KiB stream (row-major W: 16 rows x 64 B, 16 DRAM pages per
+  // load).  Llama-3 8B at M = 32: -9..-19 % per projection
+  // (profiles/r1_skinny_sweep_shuf.jsonl).
   const uint8_t* wp[NT];
+  const int wstep = Wsh != nullptr ? 1024 : 64;  // bytes between consecutive chunks of one lane
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    int n = n0 + j * 16 + (lane & 15);
-    n = n < N ? n : N - 1;
-    wp[j] = W + (size_t)n * ldw_b + lg;
+    if (Wsh != nullptr) {
+      const int ntile = (N + 15) >> 4;
+      int tcol = (n0 >> 4) + j;
+      tcol = tcol < ntile ? tcol : ntile - 1;
+      wp[j] = Wsh + ((size_t)tcol * (size_t)(kbytes >> 6) * 64 + lane) * 16;
+    } else {
+      int n = n0 + j * 16 + (lane & 15);
+      n = n < N ? n : N - 1;
+      wp[j] = W + (size_t)n * ldw_b + lg;
+    }
   }
   const uint8_t* ap[MT];
 #pragma unroll
@@ -150,7 +165,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     for (int u = 0; u < U; ++u) {
       const int ci = min(cc + u, c1 - 1);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) wv[j][u] = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)ci * 64);
+      for (int j = 0; j < NT; ++j) wv[j][u] = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)ci * wstep);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -325,25 +340,26 @@ using namespace dnn;
 template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8, bool MS = false>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                             int ks, const float* colsum, float eps, hipStream_t st) {
+                             int ks, const float* colsum, float eps, hipStream_t st, const void* Wsh) {
   const int groups = (N + 16 * NT - 1) / (16 * NT) * (MS ? (M + 15) / 16 : 1);
   while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
   size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
   if (NORM != NORM_NONE) smem += (size_t)ks * MT * 2 * 16 * sizeof(float);
   hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8, MS>), dim3(groups), dim3(64 * ks), smem,
                      st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
-                     ldr, M, N, kbytes, colsum, eps);
+                     ldr, M, N, kbytes, colsum, eps, (const uint8_t*)Wsh);
   return (int)hipGetLastError();
 }
 
 template <int ACT, bool F32, bool FP8, int NORM = NORM_NONE, bool W8 = false>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                         hipStream_t st, const float* colsum = nullptr, float eps = 0.f) {
+                         hipStream_t st, const float* colsum = nullptr, float eps = 0.f,
+                         const void* Wsh = nullptr) {
   const bool wide = N >= 16384;
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
   return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
-                                                                       ldr, M, N, kbytes, KSV, colsum, eps, st)
+                                                                       ldr, M, N, kbytes, KSV, colsum, eps, st, Wsh)
   if (M <= 8) CFG(1, 1, 4, false, 8);
   if (M <= 16) {
     if (wide) CFG(1, 4, 2, false, 2);
@@ -359,7 +375,7 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   // GPT-2 XL W8 N=1600: 9.8 -> 7.0 / 28.5 -> 16.0 us; Llama W8 N=4096 at M=32.
 #define CFG_MS(NTV)                                                                                           \
   return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, 2, true, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
-                                                                            R, ldr, M, N, kbytes, 4, colsum, eps, st)
+                                                                            R, ldr, M, N, kbytes, 4, colsum, eps, st, Wsh)
   if (!FP8) {
     if (N <= 1024) CFG_MS(1);
     if (N <= 2048 || (W8 && N <= 4096)) CFG_MS(2);
@@ -383,7 +399,7 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
 // bf16: K % 32 == 0 (64-B chunks), M <= 64.  fp8: K (bytes) % 64 == 0.
 extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw,
                                void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int K,
-                               int act, int out_f32, int fp8, hipStream_t st) {
+                               int act, int out_f32, int fp8, hipStream_t st, const void* Wsh) {
   const int eb = fp8 ? 1 : 2;
   const int kbytes = K * eb;
   if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
@@ -393,11 +409,15 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
 #define SKD(a)                                                                                              \
   if (act == a) {                                                                                           \
     if (fp8) {                                                                                              \
-      return out_f32 ? launch_skinny<a, true, true>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st)  \
-                     : launch_skinny<a, false, true>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st); \
+      return out_f32 ? launch_skinny<a, true, true>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st,  \
+                                                    nullptr, 0.f, Wsh)                                        \
+                     : launch_skinny<a, false, true>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st, \
+                                                     nullptr, 0.f, Wsh);                                      \
     }                                                                                                       \
-    return out_f32 ? launch_skinny<a, true, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st)   \
-                   : launch_skinny<a, false, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st);  \
+    return out_f32 ? launch_skinny<a, true, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st,   \
+                                                   nullptr, 0.f, Wsh)                                         \
+                   : launch_skinny<a, false, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st,  \
+                                                    nullptr, 0.f, Wsh);                                       \
   }
   SKD(ACT_NONE)
   SKD(ACT_RELU)
@@ -412,7 +432,7 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
 // ops/gemm.py fold_norm.  act: NONE / GELU / SILU_MUL.
 extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                                     const void* R, int ldr, int M, int N, int K, int act, int norm,
-                                    const float* colsum, float eps, hipStream_t st) {
+                                    const float* colsum, float eps, hipStream_t st, const void* Wsh) {
   const int kbytes = K * 2;
   if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
@@ -421,7 +441,7 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
 #define SKN(a, nm)                                                                                                   \
   if (act == a && norm == nm)                                                                                        \
     return launch_skinny<a, false, false, nm>(A, la, nullptr, W, lw, nullptr, C, ldc, bias, R, ldr, M, N, kbytes, st, \
-                                              colsum, eps);
+                                              colsum, eps, Wsh);
   SKN(ACT_NONE, NORM_RMS)
   SKN(ACT_SILU_MUL, NORM_RMS)
   SKN(ACT_NONE, NORM_LN)
@@ -436,7 +456,7 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
 // (norm 0 = none).  K % 64 == 0 (logical K; the weight rows may be padded).
 extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                                   const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
-                                  const float* colsum, float eps, hipStream_t st) {
+                                  const float* colsum, float eps, hipStream_t st, const void* Wsh) {
   if (M <= 0 || M > 64 || N <= 0 || K % 64 != 0 || ldw < K || sw == nullptr) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
   if (norm == NORM_LN && colsum == nullptr) return -1;
@@ -444,7 +464,7 @@ extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw
 #define SKW(a, nm)                                                                                                    \
   if (act == a && norm == nm)                                                                                         \
     return launch_skinny<a, false, false, nm, true>(A, la, nullptr, W, ldw, sw, C, ldc, bias, R, ldr, M, N, K, st,     \
-                                                    colsum, eps);
+                                                    colsum, eps, Wsh);
   SKW(ACT_NONE, NORM_NONE)
   SKW(ACT_NONE, NORM_RMS)
   SKW(ACT_SILU_MUL, NORM_RMS)
@@ -457,24 +477,27 @@ extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw
 // Configuration sweep for bench/skinny_sweep.py (no epilogue ops): nt in
 // {1,2,4}, u in {2,4,8}, pipe in {0,1}; ks = waves per workgroup; w8 = fp8
 // weights (W8A16, sw = channel scales) instead of bf16.
-template <int MT, int NT, int U, bool PIPE, bool W8, bool MS = false>
+template <int MT, int NT, int U, bool PIPE, bool W8, bool MS = false, bool SHUF = false>
 static int skinny_sweep_launch(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                                int M, int N, int K, int ks, hipStream_t st) {
+  // SHUF: W points at the pre-shuffled copy
   const int groups = (N + 16 * NT - 1) / (16 * NT) * (MS ? (M + 15) / 16 : 1);
   const size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
-  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE, NORM_NONE, W8, MS>), dim3(groups),
+  hipLaunchKernelGGL((gemm_skinny_kernel<ACT_NONE, false, MT, NT, false, U, PIPE, NORM_NONE, W8, MS>),
+                     dim3(groups),
                      dim3(64 * ks), smem, st, (const uint8_t*)A, lda * 2, nullptr, (const uint8_t*)W,
-                     W8 ? ldw : ldw * 2, sw, C, ldc, nullptr, nullptr, 0, M, N, W8 ? K : K * 2, nullptr, 0.f);
+                     W8 ? ldw : ldw * 2, sw, C, ldc, nullptr, nullptr, 0, M, N, W8 ? K : K * 2, nullptr, 0.f,
+                     SHUF ? (const uint8_t*)W : nullptr);
   return (int)hipGetLastError();
 }
 
-template <int MT, bool W8>
+template <int MT, bool W8, bool SHUF = false>
 static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc, int M,
                            int N, int K, int nt, int u, int ks, int pipe, hipStream_t st) {
-#define SW(NTV, UV)                                                                                               \
-  if (nt == NTV && u == UV)                                                                                       \
-    return pipe ? skinny_sweep_launch<MT, NTV, UV, true, W8>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st)        \
-                : skinny_sweep_launch<MT, NTV, UV, false, W8>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
+#define SW(NTV, UV)                                                                                                  \
+  if (nt == NTV && u == UV)                                                                                          \
+    return pipe ? skinny_sweep_launch<MT, NTV, UV, true, W8, false, SHUF>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st) \
+                : skinny_sweep_launch<MT, NTV, UV, false, W8, false, SHUF>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
   SW(1, 2) SW(1, 4) SW(1, 8) SW(2, 2) SW(2, 4) SW(2, 8) SW(4, 2) SW(4, 4)
 #undef SW
   return -2;
@@ -492,11 +515,21 @@ static int skinny_sweep_ms(const void* A, int lda, const void* W, int ldw, const
   return -2;
 }
 
-// pipe bit 0: software pipeline; bit 1: M split (MS)
+// pipe bit 0: software pipeline; bit 1: M split (MS); bit 2: pre-shuffled W (SHUF)
 extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, const float* sw, void* C,
                                      int ldc, int M, int N, int K, int nt, int u, int ks, int pipe, int w8,
                                      hipStream_t st) {
   if (M <= 0 || M > 64 || K % 64 != 0 || ks < 1 || ks > 8 || (w8 && sw == nullptr)) return -1;
+  if (pipe & 4) {  // pre-shuffled weights (no M split)
+    pipe &= 1;
+#define SWS(MTV)                                                                                                 \
+  return w8 ? skinny_sweep_mt<MTV, true, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st)        \
+            : skinny_sweep_mt<MTV, false, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+    if (M <= 16) SWS(1)
+    if (M <= 32) SWS(2)
+    SWS(4)
+#undef SWS
+  }
   if (pipe & 2) {  // M split: one 16-row tile per workgroup
     pipe &= 1;
     return w8 ? skinny_sweep_ms<true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st)

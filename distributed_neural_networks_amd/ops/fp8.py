@@ -30,6 +30,7 @@ class Fp8Weight:
     q: torch.Tensor      # (N, Kpad) float8_e4m3fn, K zero-padded to a multiple of 128
     scale: torch.Tensor  # (N,) fp32
     k: int = 0           # logical K
+    shuf: Optional[torch.Tensor] = None  # decode copy in skinny fragment order (gemm.shuffle_weight), or None
 
     @property
     def shape(self):
@@ -102,7 +103,9 @@ def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None
         out = torch.empty((M, Nout), dtype=torch.bfloat16, device=x.device)
     if out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.shape[0] < M or out.shape[1] < Nout:
         raise ValueError("linear_w8: bad output buffer")
+    if w.shuf is not None and w.shuf.numel() != -(-N // 16) * 16 * K:
+        raise ValueError("linear_w8: shuf is not shuffle_weight(w.q[:, :K])")
     check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0), ptr(bias),
                                ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, act, norm,
-                               ptr(colsum), eps, stream_ptr()), "gemm_skinny_w8")
+                               ptr(colsum), eps, stream_ptr(), ptr(w.shuf)), "gemm_skinny_w8")
     return out

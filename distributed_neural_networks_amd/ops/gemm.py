@@ -18,7 +18,8 @@ _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+           out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` when M <= 64."""
     a = _ACTS[act] if not isinstance(act, int) else act
     x2 = x.reshape(-1, x.shape[-1]) if x.dim() != 2 else x
     M, K = x2.shape
@@ -40,9 +41,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     r2 = None
     if residual is not None:
         r2 = residual.reshape(-1, residual.shape[-1]) if residual.dim() != 2 else residual
+    if w_shuf is not None and w_shuf.numel() * w_shuf.element_size() != -(-N // 16) * 16 * K * 2:
+        raise ValueError("linear: w_shuf is not shuffle_weight(w)")
     check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
                           ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
-                          1 if o2.dtype == torch.float32 else 0, stream_ptr()), "gemm_bf16")
+                          1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf)), "gemm_bf16")
     return out
 
 
@@ -72,10 +75,11 @@ class FoldedLinear:
     (``fold_norm``): ``w`` = W diag(gamma) (bf16), ``bias`` = W beta + b
     (fp32 or None), ``colsum`` = row sums of the bf16 ``w`` (LayerNorm only)."""
 
-    __slots__ = ("w", "bias", "colsum", "norm", "eps")
+    __slots__ = ("w", "bias", "colsum", "norm", "eps", "ws")
 
     def __init__(self, w, bias, colsum, norm, eps):
         self.w, self.bias, self.colsum, self.norm, self.eps = w, bias, colsum, norm, eps
+        self.ws = None  # bf16 decode copy in skinny fragment order (shuffle_weight)
 
 
 def fold_norm(w: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor], bias: Optional[torch.Tensor],
@@ -143,7 +147,45 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         raise ValueError("linear_norm: bad output buffer")
     if residual is not None and (residual.shape[0] < M or residual.stride(1) != 1):
         raise ValueError("linear_norm: bad residual")
+    if f.ws is not None and f.ws.numel() != -(-N // 16) * 16 * K * 2:
+        raise ValueError("linear_norm: ws is not shuffle_weight(w)")
     check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0), ptr(f.bias),
                                  ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, a, f.norm,
-                                 ptr(f.colsum), f.eps, stream_ptr()), "gemm_skinny_norm")
+                                 ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws)), "gemm_skinny_norm")
     return out
+
+def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
+    """Pre-shuffle a decode weight [N, K] (bf16, or e4m3 bytes) into the skinny
+    GEMM's MFMA fragment order: for column tile t (16 rows) and 64-B chunk c,
+    the 16 rows x 64 B form one contiguous 1 KiB block with lane l = 16 g + r
+    holding row r, bytes 16 g..16 g+15 of the chunk; blocks of one tile are
+    consecutive along K.  N is zero-padded to a multiple of 16.  Returns a flat
+    uint8 tensor (the kernel addresses it by bytes)."""
+    N = w.shape[0]
+    b = w.contiguous().view(torch.uint8).reshape(N, -1)
+    kb = b.shape[1]
+    if kb % 64:
+        raise ValueError(f"shuffle_weight: row bytes {kb} must be a multiple of 64")
+    Np = -(-N // 16) * 16
+    if Np != N:
+        b = torch.cat([b, b.new_zeros(Np - N, kb)])
+    return b.view(Np // 16, 16, kb // 64, 4, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
+def attach_shuffled(w):
+    """Give a decode weight its fragment-order copy: a ``FoldedLinear`` gets
+    ``.ws`` (bf16) or its ``Fp8Weight`` ``.shuf``; an ``Fp8Weight`` gets
+    ``.shuf``; a bf16 tensor returns its shuffled copy (the caller keeps it and
+    passes it as ``linear(..., w_shuf=)``).  The row-major weight stays for
+    prefill (M > 64), so decode weights take twice their bytes in HBM."""
+    from .fp8 import Fp8Weight
+    if isinstance(w, FoldedLinear):
+        if isinstance(w.w, Fp8Weight):
+            attach_shuffled(w.w)
+        else:
+            w.ws = shuffle_weight(w.w)
+        return w
+    if isinstance(w, Fp8Weight):
+        w.shuf = shuffle_weight(w.q[:, :w.k or w.q.shape[1]])
+        return w
+    return shuffle_weight(w)

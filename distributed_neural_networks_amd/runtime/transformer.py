@@ -26,6 +26,7 @@ All positions/lengths live in device memory so a decode step is one graph.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -60,6 +61,8 @@ class LayerW:
     b_up: Optional[torch.Tensor]
     w_down: object
     b_down: Optional[torch.Tensor]
+    w_o_s: Optional[torch.Tensor] = None     # bf16 decode copies in skinny fragment order (shuffle_weight)
+    w_down_s: Optional[torch.Tensor] = None
 
 
 class TransformerStage(StageCompute):
@@ -103,6 +106,11 @@ class TransformerStage(StageCompute):
                                         self.fp8)
             else:
                 self.w_head = self._w(sd["lm_head.weight"])
+        # decode copies of every projection in the skinny GEMM's fragment order
+        # (contiguous 1 KiB per wave load; DNN_SHUF_WEIGHTS=0 disables): twice
+        # the weight bytes in HBM, -9..-19 % per decode projection at M = 32
+        if os.environ.get("DNN_SHUF_WEIGHTS", "1") != "0":
+            self._attach_decode_copies()
         # RoPE tables (Llama)
         self.cos = self.sin = None
         if self.family == "llama3":
@@ -115,6 +123,22 @@ class TransformerStage(StageCompute):
         self._alloc(self.max_tokens)
 
     # ------------------------------------------------------------------ weights
+    def _attach_decode_copies(self):
+        from ..ops.gemm import attach_shuffled
+        for L in self.layers:
+            for name in ("w_qkv", "w_up"):
+                w = getattr(L, name)
+                if not isinstance(w, torch.Tensor):  # FoldedLinear / Fp8Weight: the copy rides on the object
+                    attach_shuffled(w)
+            for name in ("w_o", "w_down"):
+                w = getattr(L, name)
+                if isinstance(w, torch.Tensor):
+                    setattr(L, name + "_s", attach_shuffled(w))
+                else:
+                    attach_shuffled(w)
+        if self.last and not isinstance(self.w_head, torch.Tensor):
+            attach_shuffled(self.w_head)
+
     def _w(self, w):
         if self.fp8:
             from ..ops.fp8 import quantize_weight
@@ -180,13 +204,13 @@ class TransformerStage(StageCompute):
             self.logits = torch.empty((ntok, self.Vpad), dtype=bf, device=dev)
             self.next_ids = torch.empty((ntok,), dtype=torch.int32, device=dev)
 
-    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None):
+    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None):
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
             if x.shape[0] <= 64:  # decode: weight-only fp8 (bf16 activations, no quantise launch)
                 return linear_w8(x, w, b, act, residual, out)
             return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
-        return linear(x, w, b, act, residual, out)
+        return linear(x, w, b, act, residual, out, w_shuf=w_shuf)
 
     # ------------------------------------------------------------------ specs
     def in_spec(self, batch: int, T: int = 1):
@@ -237,7 +261,7 @@ class TransformerStage(StageCompute):
             else:
                 T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
-            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h)
+            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
             if self.fuse_norm:
                 f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[:ntok], std_buf=a, ones=self.ones, q8=self.q8,
@@ -245,7 +269,7 @@ class TransformerStage(StageCompute):
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
                 f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[:ntok])
-            self._lin(f, L.w_down, L.b_down, residual=h, out=h)
+            self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s)
             h_in = h
         if not self.last:
             if out is not None:

@@ -449,3 +449,52 @@ def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits):
         s = torch.einsum("hd,hkd->hk", qb, k) / math.sqrt(hd)
         ref = torch.einsum("hk,hkd->hd", s.softmax(-1), v).reshape(-1)
         assert _rel(out[b], ref) < 2e-2, b
+
+
+@pytest.mark.parametrize("M", [1, 16, 17, 33, 64])
+@pytest.mark.parametrize("N,K", [(100, 128), (2304, 768), (1600, 1600), (6144, 4096)])
+def test_skinny_shuffled_weights_bitwise(M, N, K):
+    """Decode GEMMs streaming the fragment-order weight copy (shuffle_weight)
+    issue the same MFMAs as the row-major path: bf16 linear, fused-norm
+    linear and W8A16 must agree bit for bit (ragged N pads the last tile)."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import attach_shuffled, fold_norm, linear, linear_norm, shuffle_weight
+    torch.manual_seed(12)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    wb = W.bfloat16()
+    ref = linear(x, wb, b, act=2, residual=r)
+    got = linear(x, wb, b, act=2, residual=r, w_shuf=shuffle_weight(wb))
+    assert torch.equal(got, ref)
+    gamma = torch.rand(K, device=DEV) + 0.5
+    f = fold_norm(W, gamma, None, None, True, 1e-5, DEV)
+    ref = linear_norm(x, f)
+    attach_shuffled(f)
+    assert f.ws is not None
+    assert torch.equal(linear_norm(x, f), ref)
+    if K % 64 == 0:
+        q = quantize_weight(W, DEV)
+        ref = linear_w8(x, q, b, 0, r)
+        attach_shuffled(q)
+        assert torch.equal(linear_w8(x, q, b, 0, r), ref)
+
+
+def test_stage_decode_with_and_without_shuffled_weights(monkeypatch):
+    """A tiny Llama stage decodes identically with DNN_SHUF_WEIGHTS=0 and 1."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    outs = []
+    ids = torch.randint(0, 100, (4, 8), generator=torch.Generator().manual_seed(0), dtype=torch.int32).to(DEV)
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DNN_SHUF_WEIGHTS", flag)
+        sd = ckpt.random_stage_state_dict("llama3-tiny", 0, 1, True, True, 0)
+        st = TransformerStage("llama3-tiny", sd, 0, 1, True, True, DEV, max_batch=4, max_seq=64)
+        assert (st.layers[0].w_o_s is not None) == (flag == "1")
+        pos = torch.zeros(4, device=DEV, dtype=torch.int32)
+        st.step(ids, pos, 4, 8)
+        pos += 8
+        o = st.step(ids[:, -1:].contiguous(), pos, 4, 1)
+        outs.append(o.probs.float().clone())
+    assert torch.equal(outs[0], outs[1])
