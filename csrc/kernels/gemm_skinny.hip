@@ -373,12 +373,27 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   // too few for 256 CUs: graph-timed sweep profiles/r1_skinny_sweep_ms.jsonl —
   // GPT-2 N=768: 5.8 -> 3.8 us (K=768), 15.9 -> 8.3 us (K=3072) at M=64;
   // GPT-2 XL W8 N=1600: 9.8 -> 7.0 / 28.5 -> 16.0 us; Llama W8 N=4096 at M=32.
-#define CFG_MS(NTV)                                                                                           \
-  return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, 2, true, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
-                                                                            R, ldr, M, N, kbytes, 4, colsum, eps, st, Wsh)
+#define CFG_MS(NTV, UV, PV, KSV)                                                                                 \
+  return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, UV, PV, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
+                                                                           R, ldr, M, N, kbytes, KSV, colsum, eps, st, \
+                                                                           Wsh)
+  if (!FP8 && Wsh != nullptr) {
+    // fragment-order weights (M 17..64): graph-timed sweep profiles/r1_skinny_sweep_shuf_fit.jsonl,
+    // every rule within 1.0-1.1x of the best config of its shapes (Llama-3 8B at M = 32,
+    // GPT-2 at M = 64, GPT-2 XL W8 at M = 64)
+    if (wide) {
+      if (M <= 32) CFG(2, 4, 2, false, 2);
+      CFG(4, 4, 2, false, 2);
+    }
+    if (N <= 1024) CFG_MS(1, 4, false, 4);
+    if (!W8 && N > 4096 && M <= 32) CFG(2, 2, 2, true, 4);  // Llama QKV (6144)
+    if (W8 && N > 4096) CFG_MS(4, 2, false, 4);
+    if (kbytes >= 8192) CFG_MS(2, 4, false, 4);
+    CFG_MS(2, 2, false, 4);
+  }
   if (!FP8) {
-    if (N <= 1024) CFG_MS(1);
-    if (N <= 2048 || (W8 && N <= 4096)) CFG_MS(2);
+    if (N <= 1024) CFG_MS(1, 2, true, 4);
+    if (N <= 2048 || (W8 && N <= 4096)) CFG_MS(2, 2, true, 4);
   }
 #undef CFG_MS
   const bool deep = kbytes >= 16384;
@@ -503,13 +518,13 @@ static int skinny_sweep_mt(const void* A, int lda, const void* W, int ldw, const
   return -2;
 }
 
-template <bool W8>
+template <bool W8, bool SHUF = false>
 static int skinny_sweep_ms(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc, int M,
                            int N, int K, int nt, int u, int ks, int pipe, hipStream_t st) {
 #define SW(NTV, UV)                                                                                                  \
   if (nt == NTV && u == UV)                                                                                          \
-    return pipe ? skinny_sweep_launch<1, NTV, UV, true, W8, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st)      \
-                : skinny_sweep_launch<1, NTV, UV, false, W8, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
+    return pipe ? skinny_sweep_launch<1, NTV, UV, true, W8, true, SHUF>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st) \
+                : skinny_sweep_launch<1, NTV, UV, false, W8, true, SHUF>(A, lda, W, ldw, sw, C, ldc, M, N, K, ks, st);
   SW(1, 2) SW(1, 4) SW(1, 8) SW(2, 2) SW(2, 4) SW(2, 8) SW(4, 2) SW(4, 4)
 #undef SW
   return -2;
@@ -520,6 +535,11 @@ extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int 
                                      int ldc, int M, int N, int K, int nt, int u, int ks, int pipe, int w8,
                                      hipStream_t st) {
   if (M <= 0 || M > 64 || K % 64 != 0 || ks < 1 || ks > 8 || (w8 && sw == nullptr)) return -1;
+  if ((pipe & 6) == 6) {  // pre-shuffled weights + M split
+    pipe &= 1;
+    return w8 ? skinny_sweep_ms<true, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st)
+              : skinny_sweep_ms<false, true>(A, lda, W, ldw, sw, C, ldc, M, N, K, nt, u, ks, pipe, st);
+  }
   if (pipe & 4) {  // pre-shuffled weights (no M split)
     pipe &= 1;
 #define SWS(MTV)                                                                                                 \

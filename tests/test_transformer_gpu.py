@@ -453,10 +453,11 @@ def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits):
 
 @pytest.mark.parametrize("M", [1, 16, 17, 33, 64])
 @pytest.mark.parametrize("N,K", [(100, 128), (2304, 768), (1600, 1600), (6144, 4096)])
-def test_skinny_shuffled_weights_bitwise(M, N, K):
-    """Decode GEMMs streaming the fragment-order weight copy (shuffle_weight)
-    issue the same MFMAs as the row-major path: bf16 linear, fused-norm
-    linear and W8A16 must agree bit for bit (ragged N pads the last tile)."""
+def test_skinny_shuffled_weights_match(M, N, K):
+    """Decode GEMMs streaming the fragment-order weight copy (shuffle_weight):
+    bf16 linear, fused-norm linear and W8A16 agree with the row-major path to
+    bf16 rounding (the shuffled path has its own config table, so the K split
+    and summation order may differ; ragged N pads the last tile)."""
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import attach_shuffled, fold_norm, linear, linear_norm, shuffle_weight
     torch.manual_seed(12)
@@ -467,22 +468,23 @@ def test_skinny_shuffled_weights_bitwise(M, N, K):
     wb = W.bfloat16()
     ref = linear(x, wb, b, act=2, residual=r)
     got = linear(x, wb, b, act=2, residual=r, w_shuf=shuffle_weight(wb))
-    assert torch.equal(got, ref)
+    assert _rel(got, ref) < 5e-3
     gamma = torch.rand(K, device=DEV) + 0.5
     f = fold_norm(W, gamma, None, None, True, 1e-5, DEV)
     ref = linear_norm(x, f)
     attach_shuffled(f)
     assert f.ws is not None
-    assert torch.equal(linear_norm(x, f), ref)
+    assert _rel(linear_norm(x, f), ref) < 5e-3
     if K % 64 == 0:
         q = quantize_weight(W, DEV)
         ref = linear_w8(x, q, b, 0, r)
         attach_shuffled(q)
-        assert torch.equal(linear_w8(x, q, b, 0, r), ref)
+        assert _rel(linear_w8(x, q, b, 0, r), ref) < 5e-3
 
 
 def test_stage_decode_with_and_without_shuffled_weights(monkeypatch):
-    """A tiny Llama stage decodes identically with DNN_SHUF_WEIGHTS=0 and 1."""
+    """A tiny Llama stage decodes the same logits (to bf16 rounding) with
+    DNN_SHUF_WEIGHTS=0 and 1."""
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
     outs = []
@@ -497,4 +499,4 @@ def test_stage_decode_with_and_without_shuffled_weights(monkeypatch):
         pos += 8
         o = st.step(ids[:, -1:].contiguous(), pos, 4, 1)
         outs.append(o.probs.float().clone())
-    assert torch.equal(outs[0], outs[1])
+    assert _rel(outs[1], outs[0]) < 1e-2
