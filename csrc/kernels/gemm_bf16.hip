@@ -16,6 +16,8 @@
 // Block ids are remapped so tiles sharing A panels run on one XCD (T1).
 //
 // Decode-sized M (<= 64) goes to the weight-streaming kernels of gemm_skinny.hip.
+#include <type_traits>
+
 #include "api.h"
 #include "gemm_epilogue.h"
 
@@ -261,8 +263,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
   const int arow = wr * 64, brow = wc * 32;
-  for (int t = 0; t < nk; ++t) {
-    const int u = t & 1;
+  // One K-tile; the loop runs two per iteration so the buffer index u is a
+  // compile-time constant and every LDS address an immediate offset.
+  auto ktile = [&](const int t, auto ucst) {
+    constexpr int u = decltype(ucst)::value;
     // ph1
     bg_read<2>(b0, half(u, 2), brow, lane);
     __builtin_amdgcn_sched_barrier(0);
@@ -290,7 +294,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     bg_barrier();
     bg_mfma<4, 2>(acc[1][0], af, b0);
     bg_barrier();
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
   }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
 
