@@ -333,6 +333,163 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
       }
 }
 
+// ---------------------------------------------------------------------------
+// fp8 (OCP e4m3fn) on the same 256^2 4-phase schedule: a K-tile is 128 fp8 =
+// 128 B per row, so every LDS half-tile, glds piece and swizzle is
+// byte-identical to the bf16 kernel's BK = 64 and the staging code is shared.
+// Per (i, j) and K-tile ONE v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 block
+// scales, 2x the bf16 rate) replaces the two bf16 16x16x32: lane group g feeds
+// chunks g and 4+g of its row as its 32 "k" bytes — the same permutation of k
+// for both operands, so the dot product is unchanged and the fragment reads are
+// exactly the bf16 kernel's (conflict-free) ones.  Epilogue: per-token scale
+// sa[m] and per-channel scale sw[n] on the fp32 accumulators, then the shared
+// bias / act / residual / SwiGLU epilogues (16-B paired stores).
+// ---------------------------------------------------------------------------
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ i32x8_t f8_cat(const bf16x8& lo, const bf16x8& hi) {
+  i32x8_t r;
+  const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+template <int MI, int NJ>
+__device__ __forceinline__ void bg_mfma_f8(f32x4 (&acc)[MI][NJ], const bf16x8 (&a)[MI][2], const bf16x8 (&b)[NJ][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(f8_cat(b[j][0], b[j][1]), f8_cat(a[i][0], a[i][1]),
+                                                                   acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
+    const uint8_t* __restrict__ A8, const float* __restrict__ sa, const uint8_t* __restrict__ W8,
+    const float* __restrict__ sw, bf16_t* __restrict__ C, int ldc, const float* __restrict__ bias,
+    const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb) {
+  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
+  const int m0 = tm * BG_M, n0 = tn * BG_N;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nk = Kb / 128;
+  // byte-identical staging: view the e4m3 rows as bf16 rows of half the length
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(A8);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
+  const int lda = Kb / 2, ldw = Kb / 2;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto half = [&](int u, int h) { return smem + (u * 4 + h) * BG_HALF; };
+  auto stA = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(A, lda, m0 + h * 128, M, t * BG_K, half(u, h), wave, lane);
+  };
+  auto stB = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
+  };
+
+  stA(0, 0, 0);
+  stB(0, 1, 0);
+  stA(0, 1, 0);
+  stB(0, 0, 0);
+  stA(1, 0, 1);
+  stB(1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bg_barrier();
+  if (wr == 1) bg_barrier();
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 64, brow = wc * 32;
+  auto ktile = [&](const int t, auto ucst) {
+    constexpr int u = decltype(ucst)::value;
+    bg_read<2>(b0, half(u, 2), brow, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    bg_read<4>(af, half(u, 0), arow, lane);
+    stA(u ^ 1, 1, t + 1);
+    bg_barrier();
+    bg_mfma_f8<4, 2>(acc[0][0], af, b0);
+    bg_barrier();
+    bg_read<2>(b1, half(u, 3), brow, lane);
+    stB(u ^ 1, 0, t + 1);
+    bg_barrier();
+    bg_mfma_f8<4, 2>(acc[0][1], af, b1);
+    bg_barrier();
+    bg_read<4>(af, half(u, 1), arow, lane);
+    stA(u, 0, t + 2);
+    bg_barrier();
+    bg_mfma_f8<4, 2>(acc[1][1], af, b1);
+    bg_barrier();
+    bg_read<2>(b0, half(u, 2), brow, lane);
+    stB(u, 1, t + 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    bg_barrier();
+    bg_mfma_f8<4, 2>(acc[1][0], af, b0);
+    bg_barrier();
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
+  }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wr == 0) bg_barrier();
+
+  const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
+  const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
+        const int nb = n0 + nq * 128 + wc * 32;
+        const float rs = m < M ? sa[m] : 0.f;
+        f32x4 v[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = nb + j * 16 + (lane >> 4) * 4;
+          f32x4 cs;
+          if (n + 3 < N) {
+            cs = *reinterpret_cast<const f32x4*>(sw + n);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[r] = n + r < N ? sw[n + r] : 0.f;
+          }
+          v[j] = acc[mq][nq][i][j] * (cs * rs);
+        }
+        if (ACT == ACT_SILU_MUL) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) epi_silu_t4<false>(v[j], m, (nb + j * 16) / 2, M, N / 2, C, ldc, vec, lane);
+        } else if (pair && nb + 31 < N) {
+          epi_pair_bf16<ACT>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            epi_t4<ACT, false>(v[j], m, nb + j * 16 + (lane >> 4) * 4, M, N, C, ldc, bias, R, ldr, vec);
+        }
+      }
+}
+
 // SwiGLU for the skinny path: h[m, j] = silu(g[m, j]) * u[m, j] where the skinny
 // GEMM produced the packed [M, 2F] fp32/bf16 output.
 __global__ void silu_mul_packed_kernel(const bf16_t* __restrict__ gu, int ld_in, bf16_t* __restrict__ out,
@@ -413,4 +570,24 @@ extern "C" int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_
   hipLaunchKernelGGL(silu_mul_packed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, (const bf16_t*)gu, ld_in,
                      (bf16_t*)out, ld_out, M, F);
   return (int)hipGetLastError();
+}
+
+// fp8 256^2 GEMM (see gemm_fp8_256_kernel); Kb = row bytes of A and W (multiple
+// of 128), sa per-row, sw per-column scales.  Called by dnn_gemm_fp8 when the
+// 256^2 tiles fill the chip.
+extern "C" int dnn_gemm_fp8_256(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc,
+                                const float* bias, const void* R, int ldr, int M, int N, int Kb, int act,
+                                hipStream_t st) {
+  if (Kb % 128 != 0 || M <= 0 || N <= 0 || sa == nullptr || sw == nullptr) return -1;
+  if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
+  const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+#define F8L(a)                                                                                                    \
+  if (act == a) {                                                                                                 \
+    hipLaunchKernelGGL((gemm_fp8_256_kernel<a>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A, sa,            \
+                       (const uint8_t*)W, sw, (bf16_t*)C, ldc, bias, (const bf16_t*)R, ldr, M, N, Kb);            \
+    return (int)hipGetLastError();                                                                                \
+  }
+  F8L(ACT_NONE) F8L(ACT_RELU) F8L(ACT_GELU) F8L(ACT_SILU_MUL)
+#undef F8L
+  return -2;
 }

@@ -12,6 +12,7 @@
 // Tiling mirrors gemm_bf16: 128x128 tiles, BK = 128 bytes of K per stage (so the
 // LDS image is byte-identical to the bf16 BK=64 one: 128-B rows, chunk XOR
 // (row>>1)&7 swizzle on the glds source), 4 waves 2x2, 4x4 16x16 tiles/wave.
+#include "api.h"
 #include "common.h"
 
 namespace dnn {
@@ -153,11 +154,29 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
 
 using namespace dnn;
 
+// 0 = auto, 128 / 256 force a tile (A/B benchmarking, tests)
+static int g_fp8_tile = 0;
+extern "C" int dnn_gemm_fp8_set_tile(int tile) {
+  if (tile != 0 && tile != 128 && tile != 256) return -1;
+  g_fp8_tile = tile;
+  return 0;
+}
+
 extern "C" int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc,
                             const float* bias, const void* R, int ldr, int M, int N, int K, int act, hipStream_t st) {
   if (K % F8_BK != 0) return -1;
   if (act == 3 && N % 16 != 0) return -1;  // packed gate|up groups of 8+8
   const int tiles = ((M + F8_BM - 1) / F8_BM) * ((N + F8_BN - 1) / F8_BN);
+  // large GEMMs: the 256^2 4-phase fp8 kernel (gemm_bf16.hip) when its tiles
+  // still fill the chip (same wave-quantisation rule as the bf16 dispatch)
+  const int tiles256 = ((M + 255) / 256) * ((N + 255) / 256);
+  auto fill = [](int t, int slots) {
+    const int w = (t + slots - 1) / slots;
+    return (double)t / ((double)w * slots);
+  };
+  if (g_fp8_tile != 128 && M >= 256 && N >= 256 &&
+      (g_fp8_tile == 256 || 1.4 * fill(tiles256, 256) > fill(tiles, 512)))
+    return dnn_gemm_fp8_256(A, sa, W, sw, C, ldc, bias, R, ldr, M, N, K, act, st);
 #define F8(a)                                                                                                        \
   if (act == a) {                                                                                                    \
     hipLaunchKernelGGL((gemm_fp8_kernel<a>), dim3(tiles), dim3(256), 0, st, (const uint8_t*)A, sa, (const uint8_t*)W, \

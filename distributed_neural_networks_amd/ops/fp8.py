@@ -87,6 +87,11 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
     return out
 
 
+def set_fp8_tile(tile: int = 0) -> None:
+    """Force the fp8 GEMM tile (128 or 256) or restore the auto choice (0)."""
+    check(lib().gemm_fp8_set_tile(int(tile)), "gemm_fp8_set_tile")
+
+
 def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, norm: int = 0,
               colsum: Optional[torch.Tensor] = None, eps: float = 0.0) -> torch.Tensor:

@@ -210,6 +210,47 @@ def test_fp8_gemm(M, N, K):
     assert _rel(y, ref2) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 512, 1024), (300, 4800, 1600), (1000, 520, 256), (2048, 6400, 1600),
+                                   (4096, 1600, 6400)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_fp8_gemm_256_tile(M, N, K, act):
+    """The 256^2 4-phase fp8 kernel (forced; edge tiles, K padded to 128, every
+    epilogue incl. SwiGLU and residual) vs the 128^2 fp8 kernel and vs the
+    dequantised-operand fp32 reference."""
+    from distributed_neural_networks_amd.ops.fp8 import (kpad_of, linear_fp8, quant_rows, quantize_weight,
+                                                          set_fp8_tile)
+    if act == 3 and N % 16:
+        pytest.skip("packed gate|up needs N % 16 == 0")
+    torch.manual_seed(9)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K) * 0.05
+    b = torch.randn(N, device=DEV) if act != 3 else None
+    r = torch.randn(M, N, device=DEV).bfloat16() if act in (0, 2) else None
+    wq = quantize_weight(w, DEV)
+    outs = {}
+    try:
+        for tile in (128, 256):
+            set_fp8_tile(tile)
+            outs[tile] = linear_fp8(x, wq, b, act, r)
+            torch.cuda.synchronize()
+    finally:
+        set_fp8_tile(0)
+    assert _rel(outs[256], outs[128]) < 2e-3
+    qb = torch.empty(M, kpad_of(K), dtype=torch.uint8, device=DEV)
+    sb = torch.empty(M, device=DEV)
+    quant_rows(x, qb, sb)
+    ref = (qb[:, :K].view(torch.float8_e4m3fn).float() * sb[:, None]) @ (wq.q[:, :K].float() * wq.scale[:, None]).t()
+    if act == 3:
+        g = ref.view(M, N // 16, 2, 8)
+        ref = (F.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, N // 2)
+    else:
+        ref = ref + b
+        ref = torch.relu(ref) if act == 1 else F.gelu(ref) if act == 2 else ref
+        if r is not None:
+            ref = ref + r.float()
+    assert _rel(outs[256], ref) < 1e-2
+
+
 def test_quant_matches_torch_e4m3():
     from distributed_neural_networks_amd.ops.fp8 import quant_rows
     x = (torch.randn(4, 256, device=DEV) * 5).bfloat16()
