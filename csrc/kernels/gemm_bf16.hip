@@ -90,8 +90,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
+  // two K-tiles per trip: the double-buffer index is a compile-time constant
+  auto ktile = [&](const int t, auto ccst) {
+    constexpr int cur = decltype(ccst)::value;
     char* a_s = smem + cur * 2 * G_TILE_BYTES;
     char* b_s = a_s + G_TILE_BYTES;
     if (t + 1 < nk) {
@@ -114,7 +115,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
   }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
 
   // Epilogue (transposed accumulators): lane holds row m = .. + (lane&15), cols n..n+3.
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
