@@ -161,25 +161,38 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const bf16_t* kbase = kc + ((size_t)b * Hkv + kvh) * S * HD;
   const bf16_t* vbase = vc + ((size_t)b * Hkv + kvh) * S * HD;
 
-  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
-    // ---- stage K (swizzled) and V (padded rows) ----
+  // K/V blocks are register double-buffered: block kb0+64 is fetched from
+  // global memory while block kb0 is computed, then written to LDS after the
+  // trailing barrier, so the load latency hides under the MFMA/softmax work.
+  constexpr int NIT = (FA_KB * CH) / 256;
+  i32x4 pk[NIT], pv[NIT];  // ext vectors: uint4 structs do not promote out of scratch
+  auto fetch = [&](int kb0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int it = 0; it < (FA_KB * CH) / 256; ++it) {
+    for (int it = 0; it < NIT; ++it) {
       const int e = it * 256 + tid;
       const int key = e / CH, c = e % CH;
       const int kk = min(kb0 + key, kv_len - 1);
-      uint4 kv, vv;
       if (QKV && kk >= p0) {
-        kv = *reinterpret_cast<const uint4*>(krow_new + (size_t)(kk - p0) * ldq + c * 8);
-        vv = *reinterpret_cast<const uint4*>(vrow_new + (size_t)(kk - p0) * ldq + c * 8);
+        pk[it] = *reinterpret_cast<const i32x4*>(krow_new + (size_t)(kk - p0) * ldq + c * 8);
+        pv[it] = *reinterpret_cast<const i32x4*>(vrow_new + (size_t)(kk - p0) * ldq + c * 8);
       } else {
-        kv = *reinterpret_cast<const uint4*>(kbase + (size_t)kk * HD + c * 8);
-        vv = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + c * 8);
+        pk[it] = *reinterpret_cast<const i32x4*>(kbase + (size_t)kk * HD + c * 8);
+        pv[it] = *reinterpret_cast<const i32x4*>(vbase + (size_t)kk * HD + c * 8);
       }
-      *reinterpret_cast<uint4*>(ks + key * HD * 2 + (k_swz<HD>(key, c) << 4)) = kv;
-      *reinterpret_cast<uint4*>(vs + key * SM::V_STRIDE + c * 16) = vv;
+    }
+  };
+  if (kv_end > 0) fetch(0);
+  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
+    // ---- stage K (swizzled) and V (padded rows) from the prefetch registers ----
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 256 + tid;
+      const int key = e / CH, c = e % CH;
+      *reinterpret_cast<i32x4*>(ks + key * HD * 2 + (k_swz<HD>(key, c) << 4)) = pk[it];
+      *reinterpret_cast<i32x4*>(vs + key * SM::V_STRIDE + c * 16) = pv[it];
     }
     __syncthreads();
+    if (kb0 + FA_KB < kv_end) fetch(kb0 + FA_KB);
     if (kb0 <= wave_qmax) {
       // ---- S^T for two 32-key tiles ----
       f32x16 sacc[2];
