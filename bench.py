@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
+    ap.add_argument("--s0_spare_cus", type=int, default=-1,
+                    help="CUs left free of the persistent stage-0 kernel for the RCCL hop kernels to run "
+                         "concurrently (-1 = auto: 0 on 1 GPU, 16 on N > 1)")
     ap.add_argument("--cut", default="auto", choices=["auto", "1", "2"],
                     help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = cost model")
     return ap.parse_args()
@@ -244,6 +247,14 @@ def main():
     info = dist_setup(args.gpus, args.cpu)
     N = info.world
     args._cut = pick_cut(args, info)
+    spare = args.s0_spare_cus if args.s0_spare_cus >= 0 else (16 if N > 1 else 0)
+    if spare and info.device.type == "cuda":
+        # the stage-0 kernel holds every VGPR of the CUs it runs on, so without
+        # spare CUs the all-to-all / isend kernels only start between stage-0
+        # launches and each hop is exposed; 16 of 256 CUs (2 per XCD) stay free
+        from distributed_neural_networks_amd.ops import cifar as cops
+        n_cu = torch.cuda.get_device_properties(info.device).multi_processor_count
+        cops.set_stage0_grid(max(1, n_cu - spare))
     if N == 1:
         el, imgs_per_gpu, p50, par = bench_colocated(args, info)
     elif args.placement == "interleaved":
@@ -263,6 +274,7 @@ def main():
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": imgs_per_gpu * N, "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
+                       "stage0_spare_cus": spare,
                        "stage_cut": {1: "conv|fc (reference split, 8 KiB/img hop)",
                                      2: "conv+fc1|fc2 (1 KiB/img hop)"}[args._cut]},
         }

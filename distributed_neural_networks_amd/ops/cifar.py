@@ -91,9 +91,22 @@ def head_tail(hid: torch.Tensor, w: CifarHeadWeights, probs: Optional[torch.Tens
     return probs, pred
 
 
+STAGE0_GRID = 0  # persistent stage-0 workgroups; 0 = one per CU (256)
+
+
+def set_stage0_grid(grid: int = 0) -> None:
+    """Persistent stage-0 grid size (0 = one workgroup per CU).  With fewer
+    workgroups than CUs the spare CUs stay free for concurrent kernels — the
+    RCCL all-to-all of the multi-GPU placements cannot start a workgroup on a
+    CU the stage-0 kernel holds (its 2 waves/SIMD fill every VGPR)."""
+    global STAGE0_GRID
+    STAGE0_GRID = int(grid)
+
+
 def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.Tensor] = None,
                    grid: int = 0, variant: Optional[int] = None) -> torch.Tensor:
     """x: (B,3,32,32) fp32 contiguous -> (B,4096) bf16."""
+    grid = grid or STAGE0_GRID
     if x.dtype != torch.float32 or not x.is_contiguous() or tuple(x.shape[1:]) != (3, 32, 32):
         raise ValueError(f"stage0: expected contiguous fp32 (B,3,32,32), got {x.dtype} {tuple(x.shape)}")
     B = x.shape[0]
