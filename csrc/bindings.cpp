@@ -85,6 +85,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("layernorm", [](u64 x, int ldx, u64 w, u64 b, u64 y, int ldy, int M, int N, float eps, int rms, u64 st) {
     return dnn_layernorm(CP(x), ldx, CFP(w), CFP(b), P(y), ldy, M, N, eps, rms, ST(st));
   });
+  m.def("layernorm_q8", [](u64 x, int ldx, u64 w, u64 b, u64 q, int ldq, u64 sq, int M, int N, int kpad, float eps,
+                           int rms, u64 st) {
+    return dnn_layernorm_q8(CP(x), ldx, CFP(w), CFP(b), P(q), ldq, FP(sq), M, N, kpad, eps, rms, ST(st));
+  });
   m.def("embed_gpt2", [](u64 idx, u64 wte, u64 wpe, u64 out, int B, int T, int d, u64 pos, u64 st) {
     return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), ST(st));
   });

@@ -38,6 +38,8 @@ int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const
                                const float* b2, int B, int grid, unsigned long long* stamps, hipStream_t st);
 int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
                         hipStream_t st);
+int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq, int M, int N,
+                     int kpad, float eps, int rms, hipStream_t st);
 int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N, float eps,
                   int rms, hipStream_t st);
 int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d, const int* pos,

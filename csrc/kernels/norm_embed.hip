@@ -90,6 +90,78 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x,
   }
 }
 
+// Normalise + quantise in one pass (fp8 prefill): the normalised row (fp32,
+// still in registers) is scaled by its own amax/448 and written as OCP e4m3
+// with the K padding zeroed, plus the per-row scale — the layout
+// quant_fp8_rows produces — so the activation never round-trips through bf16.
+template <int NC, bool RMS>
+__global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ w,
+                                                      const float* __restrict__ b, uint8_t* __restrict__ q, int ldq,
+                                                      float* __restrict__ sq, int M, int N, int kpad, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  float v[NC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+      const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(s) / N;
+  float qs = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; qs += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(qs) / N + eps);
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float bj = (!RMS && b != nullptr) ? b[c + j] : 0.f;
+        v[i][j] = (v[i][j] - mean) * rstd * w[c + j] + bj;
+        amax = fmaxf(amax, fabsf(v[i][j]));
+      }
+    }
+  }
+  amax = wave_max(amax);
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / sc;
+  if (lane == 0) sq[row] = sc;
+  uint8_t* qr = q + (size_t)row * ldq;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < kpad) {
+      int lo = 0, hi = 0;
+      if (c < N) {
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, hi, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+      }
+      *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)lo, (uint32_t)hi);
+    }
+  }
+}
+
 // out[r, :] = wte[idx[r], :] (+ wpe[pos[b] + t, :]) with r = b*T + t.
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ wte,
                                                     const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int B,
@@ -148,4 +220,24 @@ extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, 
   hipLaunchKernelGGL(embed_kernel, dim3(blocks), dim3(256), 0, st, idx, (const bf16_t*)wte, (const bf16_t*)wpe,
                      (bf16_t*)out, B, T, d, pos);
   return (int)hipGetLastError();
+}
+
+// Normalise (w, b; LayerNorm or RMSNorm) and quantise rows to e4m3 with per-row
+// scales: q [M][ldq bytes] (columns N..kpad-1 zeroed), sq [M].
+extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq,
+                                int M, int N, int kpad, float eps, int rms, hipStream_t st) {
+  if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad || sq == nullptr) return -1;
+  const int nc = (kpad / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), blk(256);
+#define LQ(NCV)                                                                                                   \
+  if (nc <= NCV) {                                                                                                \
+    if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,       \
+                                (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                           \
+    else hipLaunchKernelGGL((norm_q8_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,          \
+                            (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                               \
+    return (int)hipGetLastError();                                                                                \
+  }
+  LQ(1) LQ(2) LQ(4) LQ(8) LQ(16)
+#undef LQ
+  return -1;
 }

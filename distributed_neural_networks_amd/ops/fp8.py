@@ -64,15 +64,22 @@ def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: 
 
 def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
                residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-               qbuf: Optional[torch.Tensor] = None, sbuf: Optional[torch.Tensor] = None) -> torch.Tensor:
+               qbuf: Optional[torch.Tensor] = None, sbuf: Optional[torch.Tensor] = None,
+               prequantized: bool = False) -> torch.Tensor:
+    """W8A8 GEMM.  ``prequantized``: ``qbuf``/``sbuf`` already hold the e4m3
+    rows and scales of x (``transformer_ops.layernorm_q8``); x only gives M, K."""
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
     N, kp = w.q.shape
     if kp != kpad_of(K) or (w.k and w.k != K):
         raise ValueError(f"linear_fp8: x K={K} vs weight K={w.k} (padded {kp})")
-    qbuf = qbuf if qbuf is not None else torch.empty((M, kp), dtype=torch.uint8, device=x.device)
-    sbuf = sbuf if sbuf is not None else torch.empty((M,), dtype=torch.float32, device=x.device)
-    quant_rows(x2, qbuf, sbuf, M)
+    if prequantized:
+        if qbuf is None or sbuf is None:
+            raise ValueError("linear_fp8: prequantized needs qbuf and sbuf")
+    else:
+        qbuf = qbuf if qbuf is not None else torch.empty((M, kp), dtype=torch.uint8, device=x.device)
+        sbuf = sbuf if sbuf is not None else torch.empty((M,), dtype=torch.float32, device=x.device)
+        quant_rows(x2, qbuf, sbuf, M)
     if out is None:
         out = torch.empty((M, N // 2 if act == 3 else N), dtype=torch.bfloat16, device=x.device)
     o2 = out.reshape(-1, out.shape[-1])

@@ -129,9 +129,14 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
     if (not w8 and f.w.shape[1] != K) or x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise ValueError(f"linear_norm: x {tuple(x.shape)} {x.dtype} vs w {tuple(f.w.shape)}")
     if M > 64:
-        from .transformer_ops import layernorm
+        from .transformer_ops import layernorm, layernorm_q8
         if std_buf is None or ones is None:
             raise ValueError("linear_norm: M > 64 needs std_buf and ones")
+        if w8 and q8 is not None and s8 is not None:
+            # standardise + quantise in one pass: the e4m3 rows feed the W8A8 GEMM directly
+            kp = f.w.q.shape[1]
+            layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+            return linear_fp8(x, f.w, f.bias, a, residual, out, q8, s8, prequantized=True)
         xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
         if w8:
             return linear_fp8(xs[:M], f.w, f.bias, a, residual, out, q8, s8)

@@ -37,6 +37,26 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: 
     return out
 
 
+def layernorm_q8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_out: torch.Tensor,
+                 s_out: torch.Tensor, kpad: int, eps: float = 1e-5, rms: bool = False, rows: Optional[int] = None,
+                 ldx: Optional[int] = None) -> torch.Tensor:
+    """Normalise rows and quantise them to e4m3 with per-row scales in one pass
+    (the ``quant_rows`` layout: q_out (M, kpad) bytes, K padding zeroed; s_out (M,))."""
+    _bf16_2d(x, "layernorm_q8")
+    N = x.shape[-1]
+    M = rows if rows is not None else x.numel() // N
+    ldx = ldx if ldx is not None else N
+    if w.dtype != torch.float32 or (b is not None and b.dtype != torch.float32):
+        raise TypeError("layernorm_q8: fp32 weight/bias expected")
+    if N % 8 or N > 8192 or kpad < N or kpad % 8:
+        raise ValueError(f"layernorm_q8: unsupported width {N} / kpad {kpad}")
+    if q_out.numel() * q_out.element_size() < M * kpad or s_out.numel() < M:
+        raise ValueError("layernorm_q8: output too small")
+    check(lib().layernorm_q8(ptr(x), ldx, ptr(w), ptr(b), ptr(q_out), kpad, ptr(s_out), M, N, kpad, eps,
+                             1 if rms else 0, stream_ptr()), "layernorm_q8")
+    return q_out
+
+
 def embed(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], out: torch.Tensor,
           pos: Optional[torch.Tensor]) -> torch.Tensor:
     """out[b*T+t] = wte[idx[b,t]] (+ wpe[pos[b]+t]). idx int32 (B,T)."""

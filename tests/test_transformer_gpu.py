@@ -251,6 +251,33 @@ def test_fp8_gemm_256_tile(M, N, K, act):
     assert _rel(outs[256], ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,rms", [(300, 1600, False), (64, 4096, True), (1000, 768, False)])
+def test_layernorm_q8_matches_norm_then_quant(M, N, rms):
+    """Fused normalise + e4m3 quantise == layernorm then quant_rows, to e4m3
+    rounding (the fused kernel takes the row amax before the bf16 rounding);
+    the K padding is zeroed."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    from distributed_neural_networks_amd.ops.fp8 import kpad_of, quant_rows
+    torch.manual_seed(13)
+    x = (torch.randn(M, N, device=DEV) * 2 + 0.5).bfloat16()
+    w = torch.ones(N, device=DEV)
+    kp = kpad_of(N)
+    q1 = torch.full((M, kp), 7, dtype=torch.uint8, device=DEV)
+    s1 = torch.empty(M, device=DEV)
+    T.layernorm_q8(x, w, None, q1, s1, kp, 1e-5, rms)
+    y = torch.empty_like(x)
+    T.layernorm(x, w, None, y, 1e-5, rms)
+    q2 = torch.empty(M, kp, dtype=torch.uint8, device=DEV)
+    s2 = torch.empty(M, device=DEV)
+    quant_rows(y, q2, s2)
+    d1 = q1[:, :N].view(torch.float8_e4m3fn).float() * s1[:, None]
+    d2 = q2[:, :N].view(torch.float8_e4m3fn).float() * s2[:, None]
+    assert _rel(d1, d2) < 3e-2
+    assert _rel(d1, y.float()) < 4e-2
+    if kp > N:
+        assert int(q1[:, N:].sum().item()) == 0
+
+
 def test_quant_matches_torch_e4m3():
     from distributed_neural_networks_amd.ops.fp8 import quant_rows
     x = (torch.randn(4, 256, device=DEV) * 5).bfloat16()
