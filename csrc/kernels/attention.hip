@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD;
   bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD;
   float qv[G][8];
-  float nk[8], nv[8];
+  float nk[8] = {}, nv[8] = {};
   // FUSED: is the new key inside this split (and inside the cache)?
   const bool own_new = FUSED && p_new < S && p_new >= k0 && p_new < k1;
   if constexpr (FUSED) {
@@ -389,6 +389,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     }
   }
   const int knew = own_new ? p_new - k0 : -1;  // split-relative index of the register-held key
+  // q and the new key are bf16-exact (rounded after RoPE): pack them into bf16
+  // pairs so a score is 4 v_dot2_f32_bf16 per lane instead of 8 converts + 8 FMAs.
+  uint32_t qp[G][4], nkp[4];  // bf16 pairs, reinterpreted only at the dot2 call
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) nkp[j] = pack2bf(nk[j * 2], nk[j * 2 + 1]);
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
   // Scores: batches of DEC_U key rows per thread, all loads issued before the
@@ -404,18 +413,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
     for (int u = 0; u < DEC_U; ++u) {
       const int kk = kb0 + u * GPB + grp;
-      float kf[8];
+      uint32_t kp[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kf[j] = bf2f_s(kr[u][j]);
+      for (int j = 0; j < 4; ++j) kp[j] = (uint32_t)(uint16_t)kr[u][2 * j] | ((uint32_t)(uint16_t)kr[u][2 * j + 1] << 16);
       if (FUSED && kk == knew) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) kf[j] = nk[j];
+        for (int j = 0; j < 4; ++j) kp[j] = nkp[j];
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += qv[g][j] * kf[j];
+        for (int j = 0; j < 4; ++j) d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qp[g][j]), __builtin_bit_cast(bf16x2v, kp[j]), d, false);
         d = group_sum<LPK>(d);  // DPP row reduction over the LPK lanes of this key
         if (sub == 0 && kk < n) sc[g * chunk_cap + kk] = d * scale_log2;
       }
