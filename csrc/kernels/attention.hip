@@ -293,6 +293,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
 // ---------------------------------------------------------------------------
 constexpr int DEC_MAXG = 8;
 constexpr int DEC_U = 8;  // key/value rows in flight per thread
+static_assert(DEC_U % 2 == 0, "P.V folds key pairs");
 
 // 8 consecutive head-dim elements [8*sub, 8*sub+8) of one head row, RoPE'd
 // (rotate-half: element i pairs with i +- hd/2) when cosT != nullptr, and
@@ -398,6 +399,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
 #pragma unroll
   for (int j = 0; j < 4; ++j) nkp[j] = pack2bf(nk[j * 2], nk[j * 2 + 1]);
+  uint32_t nvp[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) nvp[j] = pack2bf(nv[j * 2], nv[j * 2 + 1]);
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
   // Scores: batches of DEC_U key rows per thread, all loads issued before the
@@ -462,23 +466,40 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       vr[u] = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // Key pairs (u, u+1) of this thread share the d chunk: interleave their
+    // value rows into bf16 pairs (v_perm) and fold both probabilities, rounded
+    // to bf16 as in an MFMA P.V, into one v_dot2_f32_bf16 per element.
 #pragma unroll
-    for (int u = 0; u < DEC_U; ++u) {
-      const int kk = kb0 + u * GPB + grp;
-      if (kk < n) {
-        float vf[8];
+    for (int u = 0; u < DEC_U; u += 2) {
+      const int ka = kb0 + u * GPB + grp, kz = ka + GPB;
+      uint32_t wa[4], wz[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vf[j] = bf2f_s(vr[u][j]);
-        if (FUSED && kk == knew) {
+      for (int j = 0; j < 4; ++j) {
+        wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
+        wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
+      }
+      if (FUSED && ka == knew) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) vf[j] = nv[j];
-        }
+        for (int j = 0; j < 4; ++j) wa[j] = nvp[j];
+      }
+      if (FUSED && kz == knew) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const float pw = sc[g * chunk_cap + kk];
+        for (int j = 0; j < 4; ++j) wz[j] = nvp[j];
+      }
+      uint32_t pr[8];  // element e of both rows: (row u, row u+1)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[g][j] += pw * vf[j];
-        }
+      for (int j = 0; j < 4; ++j) {
+        pr[2 * j] = __builtin_amdgcn_perm(wz[j], wa[j], 0x05040100u);
+        pr[2 * j + 1] = __builtin_amdgcn_perm(wz[j], wa[j], 0x07060302u);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pa = ka < n ? sc[g * chunk_cap + ka] : 0.f;
+        const float pz = kz < n ? sc[g * chunk_cap + kz] : 0.f;
+        const bf16x2v pp = __builtin_bit_cast(bf16x2v, pack2bf(pa, pz));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[g][j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2v, pr[j]), acc[g][j], false);
       }
     }
   }
