@@ -416,6 +416,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < DEC_U; ++u) {
+      if (kb0 + u * GPB >= n) break;  // workgroup-uniform: the rest of the batch is past the context
       const int kk = kb0 + u * GPB + grp;
       uint32_t kp[4];
 #pragma unroll
@@ -471,6 +472,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     // to bf16 as in an MFMA P.V, into one v_dot2_f32_bf16 per element.
 #pragma unroll
     for (int u = 0; u < DEC_U; u += 2) {
+      if (kb0 + u * GPB >= n) break;  // workgroup-uniform, as in the score loop
       const int ka = kb0 + u * GPB + grp, kz = ka + GPB;
       uint32_t wa[4], wz[4];
 #pragma unroll
