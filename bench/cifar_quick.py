@@ -14,21 +14,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", default="1,256,4096,65536")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     torch.manual_seed(0)
     sd = NeuralNetwork().state_dict()
-    w0, wh = cops.pack_stage0(sd, "cuda"), cops.pack_head(sd, "cuda")
+    w0, wh = cops.pack_stage0(sd, "cuda", a.precision), cops.pack_head(sd, "cuda", precision=a.precision)
+    adt = cops.act_dtype(a.precision)
     res = []
     for B in [int(b) for b in a.batches.split(",")]:
         x = torch.randn(B, 3, 32, 32, device="cuda")
-        mid = torch.empty(B, 4096, dtype=torch.bfloat16, device="cuda")
-        hid = torch.empty(B, 512, dtype=torch.bfloat16, device="cuda")
+        mid = torch.empty(B, 4096, dtype=adt, device="cuda")
+        hid = torch.empty(B, 512, dtype=adt, device="cuda")
+        spl = torch.empty(B, 3 * 4096, dtype=torch.bfloat16, device="cuda") if a.precision == "fp32" else None
         probs = torch.empty(B, 10, device="cuda")
         pred = torch.empty(B, dtype=torch.int32, device="cuda")
 
         def step():
             cops.stage0_forward(x, w0, mid)
-            cops.head_forward(mid, wh, hid, probs, pred)
+            cops.fc1_forward(mid, wh, hid, scratch=spl)
+            cops.head_tail(hid, wh, probs, pred)
 
         for _ in range(3):
             step()
@@ -51,17 +55,21 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.iters
         # per-stage timing with events
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         e[0].record()
         for _ in range(a.iters):
             cops.stage0_forward(x, w0, mid)
         e[1].record()
         for _ in range(a.iters):
-            cops.head_forward(mid, wh, hid, probs, pred)
+            cops.fc1_forward(mid, wh, hid, scratch=spl)
         e[2].record()
+        for _ in range(a.iters):
+            cops.head_tail(hid, wh, probs, pred)
+        e[3].record()
         torch.cuda.synchronize()
-        r = {"B": B, "ms_per_step": dt * 1e3, "img_per_s": B / dt,
-             "stage0_ms": e[0].elapsed_time(e[1]) / a.iters, "head_ms": e[1].elapsed_time(e[2]) / a.iters}
+        r = {"precision": a.precision, "B": B, "ms_per_step": dt * 1e3, "img_per_s": B / dt,
+             "stage0_ms": e[0].elapsed_time(e[1]) / a.iters, "fc1_ms": e[1].elapsed_time(e[2]) / a.iters,
+             "tail_ms": e[2].elapsed_time(e[3]) / a.iters}
         print(json.dumps(r), flush=True)
         res.append(r)
 

@@ -59,24 +59,20 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {
     return dnn_silu_mul_packed(CP(gu), ld_in, P(out), ld_out, M, F, ST(st));
   });
-  m.def("cifar_stage0", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
-    return dnn_cifar_stage0(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
-  });
-  m.def("cifar_stage0_v2", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
-    return dnn_cifar_stage0_v2(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
-  });
   m.def("cifar_stage0_v4", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
     return dnn_cifar_stage0_v4(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
   });
   m.def("cifar_set_v4_pt", [](int pt) { return dnn_cifar_set_v4_pt(pt); });
-  m.def("cifar_set_v3_pt", [](int pt) { return dnn_cifar_set_v3_pt(pt); });
-  m.def("cifar_stage0_v3", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 st) {
-    return dnn_cifar_stage0_v3(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid, ST(st));
+  m.def("cifar_stage0_x3", [](u64 x, u64 out, u64 w1h, u64 w1l, u64 b1, u64 w2h, u64 w2l, u64 b2, int B, int grid,
+                              u64 st) {
+    return dnn_cifar_stage0_x3(CFP(x), FP(out), CP(w1h), CP(w1l), CFP(b1), CP(w2h), CP(w2l), CFP(b2), B, grid,
+                               ST(st));
   });
-  m.def("cifar_stage0_v3_stamps", [](u64 x, u64 out, u64 w1p, u64 b1, u64 w2p, u64 b2, int B, int grid, u64 stamps,
-                                     u64 st) {
-    return dnn_cifar_stage0_v3_stamps(CFP(x), P(out), CP(w1p), CFP(b1), CP(w2p), CFP(b2), B, grid,
-                                      reinterpret_cast<unsigned long long*>(static_cast<uintptr_t>(stamps)), ST(st));
+  m.def("cifar_split3", [](u64 a, int lda, u64 o, int ldo, int M, int K, u64 st) {
+    return dnn_cifar_split3(CFP(a), lda, P(o), ldo, M, K, ST(st));
+  });
+  m.def("cifar_head_tail_x3", [](u64 hid, u64 w2h, u64 w2l, u64 b2, u64 probs, u64 pred, int B, u64 st) {
+    return dnn_cifar_head_tail_x3(CFP(hid), CP(w2h), CP(w2l), CFP(b2), FP(probs), IP(pred), B, ST(st));
   });
   m.def("cifar_head_tail", [](u64 hid, u64 w2p, u64 b2, u64 probs, u64 pred, int B, u64 st) {
     return dnn_cifar_head_tail(CP(hid), CP(w2p), CFP(b2), FP(probs), IP(pred), B, ST(st));

@@ -24,18 +24,14 @@ int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int 
                     const float* bias, const void* R, int ldr, int M, int N, int K, int act, int out_f32, int fp8,
                     hipStream_t st, const void* Wsh = nullptr);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
-int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
-                     int B, int grid, hipStream_t st);
-int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
-                        int B, int grid, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
 int dnn_cifar_set_v4_pt(int pt);
-int dnn_cifar_set_v3_pt(int pt);
-int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
-                        int B, int grid, hipStream_t st);
-int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
-                               const float* b2, int B, int grid, unsigned long long* stamps, hipStream_t st);
+int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, const void* w1l, const float* b1, const void* w2h,
+                        const void* w2l, const float* b2, int B, int grid, hipStream_t st);
+int dnn_cifar_split3(const float* a, int lda, void* o, int ldo, int M, int K, hipStream_t st);
+int dnn_cifar_head_tail_x3(const float* hid, const void* w2h, const void* w2l, const float* b2, float* probs, int* pred,
+                           int B, hipStream_t st);
 int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
                         hipStream_t st);
 int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq, int M, int N,

@@ -1,18 +1,15 @@
-// CIFAR-10 ConvNet stage kernels for gfx950.
+// CIFAR-10 ConvNet stage kernels for gfx950, bf16 compute (the fp32-accurate
+// path of the reference precision is cifar_x3.hip).
 //
 // Stage 0 (reference ModelPart0_2Node, cifar_model_parts.py:37-42):
 //   conv1(3->32,3x3,p1)+bias+ReLU+maxpool2 -> conv2(32->64,3x3,p1)+bias+ReLU+maxpool2
-//   -> flatten in NCHW order (c*64 + h*8 + w), ONE kernel, bf16 output (B,4096).
-// Both convolutions are implicit GEMMs on v_mfma_f32_32x32x16_bf16; the 32-row
-// M tile is a 4x8 pixel block so that the 2x2 max-pool is done inside each
-// lane's accumulator registers (C/D row = (g&3) + 8*(g>>2) + 4*(lane>>5)).
-// The per-image working set lives in LDS: padded input [3][34][34] bf16, the
-// pooled conv1 map as padded HWC [18][18][32] bf16 with a 16-B chunk XOR
-// swizzle (chunk ^ (Y&3)) that makes conv2's ds_read_b128 A-fragment reads
-// conflict-free, and an 8 KiB output staging buffer for coalesced stores.
-// conv2's B operand (64x288 weights) stays resident in VGPRs for the whole
-// persistent loop (one 32-channel N-tile per wave = 72 VGPRs); the next image
-// is prefetched into registers while conv2 runs.
+//   -> flatten in NCHW order (c*64 + h*8 + w), ONE persistent kernel
+//   (cifar_stage0_v4_kernel), bf16 output (B,4096).  Both convolutions are
+//   implicit GEMMs on v_mfma_f32_32x32x16_bf16; the 32-row M tile is a 4x8
+//   pixel block so that the 2x2 max-pool is done inside each lane's
+//   accumulator registers (C/D row = (g&3) + 8*(g>>2) + 4*(lane>>5)).  conv2's
+//   B operand (64x288 weights) stays resident in VGPRs for the whole
+//   persistent loop (one 32-channel N-tile per wave = 72 VGPRs).
 //
 // Stage 1 tail (reference ModelPart1_2Node, cifar_model_parts.py:53-58, plus the
 // host-side argmax of node.py:61/190, done per row here): after fc1+bias+ReLU
@@ -22,156 +19,6 @@
 
 namespace dnn {
 
-constexpr int XIN_W = 34, XIN_PLANE = 34 * 34;              // padded input plane (elements)
-constexpr int XIN_BYTES = 3 * XIN_PLANE * 2;                 // 6936
-constexpr int XIN_OFF = 0;
-constexpr int ACT1_OFF = 6944;                               // 16-B aligned
-constexpr int ACT1_BYTES = 18 * 18 * 32 * 2;                 // 20736
-constexpr int OBUF_OFF = ACT1_OFF + ACT1_BYTES;              // 27680
-constexpr int S0_LDS = OBUF_OFF + 4096 * 2;                  // 35872
-
-__device__ __forceinline__ int act1_byte(int Y, int X, int c) {
-  return ACT1_OFF + (((Y * 18 + X) * 32) + ((((c >> 3) ^ (Y & 3))) << 3) + (c & 7)) * 2;
-}
-
-// conv1 A-operand offset (elements, relative to the pixel's top-left padded
-// position) of im2col column k = c*9 + ky*3 + kx (PyTorch weight flatten order).
-__device__ __forceinline__ constexpr int c1_off(int k) {
-  return (k / 9) * XIN_PLANE + ((k % 9) / 3) * XIN_W + (k % 3);
-}
-
-__global__ __launch_bounds__(256, 2) void cifar_stage0_kernel(
-    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
-    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B) {
-  __shared__ __attribute__((aligned(16))) char smem[S0_LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, r32 = lane & 31;
-  bf16_t* xin = reinterpret_cast<bf16_t*>(smem + XIN_OFF);
-
-  // Zero the halos once (interiors are rewritten per image; halos never are).
-  for (int i = tid; i < (ACT1_OFF) / 4; i += 256) reinterpret_cast<uint32_t*>(smem)[i] = 0u;
-  for (int i = tid; i < ACT1_BYTES / 4; i += 256) reinterpret_cast<uint32_t*>(smem + ACT1_OFF)[i] = 0u;
-
-  // Resident weights. conv1: B[k][oc] = w1p[oc][k], k in [0,32) (27 real).
-  bf16x8 w1f[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 32 + s * 16 + h * 8);
-  const float bias1 = b1[r32];
-  // conv2: this wave's N-tile (32 output channels), all 18 k-steps of 16.
-  const int nt = wave & 1;
-  const int oc2 = nt * 32 + r32;
-  bf16x8 w2f[18];
-#pragma unroll
-  for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
-  const float bias2 = b2[oc2];
-
-  // Prefetch registers for one input image: 3072 fp32 = 768 float4, 3 per thread.
-  float4 pf[3];
-  int img = blockIdx.x;
-  if (img < B) {
-#pragma unroll
-    for (int u = 0; u < 3; ++u) pf[u] = reinterpret_cast<const float4*>(x + (size_t)img * 3072)[tid + u * 256];
-  }
-  __syncthreads();
-
-  for (; img < B; img += gridDim.x) {
-    // ---- input -> LDS (bf16, padded) ----
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = (tid + u * 256) * 4;      // flat fp32 index into [3][32][32]
-      const int c = e >> 10, y = (e >> 5) & 31, xx = e & 31;
-      bf16_t* d = xin + c * XIN_PLANE + (y + 1) * XIN_W + xx + 1;
-      d[0] = f2bf(pf[u].x); d[1] = f2bf(pf[u].y); d[2] = f2bf(pf[u].z); d[3] = f2bf(pf[u].w);
-    }
-    __syncthreads();
-
-    // ---- conv1 + bias + ReLU + pool -> act1 (HWC, padded, swizzled) ----
-    for (int t = wave; t < 32; t += 4) {
-      const int ty = t >> 2, tx = t & 3;
-      const int py = 4 * ty + (r32 >> 3), px = 8 * tx + (r32 & 7);   // output pixel of this lane's A row
-      const bf16_t* base = xin + py * XIN_W + px;                      // top-left of its 3x3x3 window
-      bf16x8 a0, a1;
-      // k-step 0 covers k in [0,16), k-step 1 k in [16,32) (real up to 26);
-      // lane half h takes k = 16*s + 8*h + j. All offsets are compile-time.
-      if (h == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { a0[j] = (short)base[c1_off(j)]; a1[j] = (short)base[c1_off(16 + j)]; }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          a0[j] = (short)base[c1_off(8 + j)];
-          a1[j] = j < 3 ? (short)base[c1_off(24 + (j < 3 ? j : 0))] : (short)0;
-        }
-      }
-      f32x16 acc = {};
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w1f[0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w1f[1], acc, 0, 0, 0);
-      // lane holds channel r32; reg g -> pixel (y=g>>2, x=(g&3)+4h) of the 4x8 block
-#pragma unroll
-      for (int qy = 0; qy < 2; ++qy)
-#pragma unroll
-        for (int qx = 0; qx < 2; ++qx) {
-          const int g0 = (2 * qy) * 4 + 2 * qx;
-          float v = fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5]));
-          v = fmaxf(v + bias1, 0.f);
-          const int Y = 2 * ty + qy + 1, X = 4 * tx + 2 * h + qx + 1;
-          *reinterpret_cast<bf16_t*>(smem + act1_byte(Y, X, r32)) = f2bf(v);
-        }
-    }
-    __syncthreads();
-
-    // prefetch the next image while conv2 runs
-    const int nimg = img + gridDim.x;
-    if (nimg < B) {
-#pragma unroll
-      for (int u = 0; u < 3; ++u) pf[u] = reinterpret_cast<const float4*>(x + (size_t)nimg * 3072)[tid + u * 256];
-    }
-
-    // ---- conv2 + bias + ReLU + pool -> obuf (NCHW flatten order) ----
-    {
-      f32x16 acc[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
-      const int mt0 = (wave >> 1) * 4;
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const int kk = s >> 1, ky = kk / 3, kx = kk % 3;
-        const int chunk = (s & 1) * 2 + h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
-          const int Y = 4 * ty2 + (r32 >> 3) + ky, X = 8 * tx2 + (r32 & 7) + kx;
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + ACT1_OFF + ((Y * 18 + X) * 32 + ((chunk ^ (Y & 3)) << 3)) * 2);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2f[s], acc[i], 0, 0, 0);
-        }
-      }
-      bf16_t* obuf = reinterpret_cast<bf16_t*>(smem + OBUF_OFF);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
-#pragma unroll
-        for (int qy = 0; qy < 2; ++qy)
-#pragma unroll
-          for (int qx = 0; qx < 2; ++qx) {
-            const int g0 = (2 * qy) * 4 + 2 * qx;
-            float v = fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5]));
-            v = fmaxf(v + bias2, 0.f);
-            const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h + qx;
-            obuf[oc2 * 64 + PY * 8 + PX] = f2bf(v);
-          }
-      }
-    }
-    __syncthreads();
-    // ---- coalesced store of the 8 KiB output row ----
-    {
-      const int4* src = reinterpret_cast<const int4*>(smem + OBUF_OFF);
-      int4* dst = reinterpret_cast<int4*>(out + (size_t)img * 4096);
-      dst[tid] = src[tid];
-      dst[tid + 256] = src[tid + 256];
-    }
-    // next iteration's input write touches only xin (not read after conv1)
-  }
-}
 
 // fc2 (512->10) + bias + softmax + argmax. hid: (B,512) bf16 (fc1+ReLU output).
 // One wave handles 16 rows per iteration with mfma_f32_16x16x32_bf16:
@@ -223,7 +70,7 @@ __global__ __launch_bounds__(256) void cifar_head_tail_kernel(const bf16_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// Stage 0, v2. Same math, re-laid-out for the LDS:
+// Stage-0 LDS layouts (shared by the v4 kernel below):
 //  * input staged as HWC4 bf16 [34][40][4] (3 channels + 1 zero): conv1's
 //    im2col K = (ky, kx<4, c<4) = 48 (3 MFMA k-steps of 16, zero weights on
 //    kx=3/c=3), so a lane's 8 A-values for a k-step are the 2 adjacent pixels
@@ -232,7 +79,7 @@ __global__ __launch_bounds__(256) void cifar_head_tail_kernel(const bf16_t* __re
 //  * act1 = padded HWC [18][24 pitch][32 ch + 8 pad] bf16 (80-B pixels): every
 //    ds_read_b128 A-fragment of conv2 is conflict-free without an XOR, so all
 //    reads are lane_base + compile-time immediates (searched exhaustively over
-//    the 4 lane groups x 9 taps x 4 chunks; tools/lds_layout_search.py).
+//    the 4 lane groups x 9 taps x 4 chunks).
 //  * conv1 epilogue: two quad DPP exchanges gather 4 channels of one pooled
 //    pixel per lane -> one ds_write_b64 (vs 4 ds_write_b16).
 //  * conv2 epilogue: the 2 horizontally adjacent pooled pixels are packed ->
@@ -308,144 +155,9 @@ __device__ __forceinline__ void resident_fence(const bf16x8 (&w)[N], float b) {
 __device__ __forceinline__ int dpp_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ int dpp_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
 
-__global__ __launch_bounds__(256, 2) void cifar_stage0_v2_kernel(
-    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
-    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B) {
-  __shared__ __attribute__((aligned(16))) char smem[V2_LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, r32 = lane & 31;
-
-  for (int i = tid; i < V2_OB_OFF / 16; i += 256) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
-
-  // conv1 weights, B[k][oc] with k = ky*16 + kx*4 + c (48 = 3 k-steps)
-  bf16x8 w1f[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 48 + s * 16 + h * 8);
-  const float bias1 = b1[r32];
-  const int nt = wave & 1;
-  const int oc2 = nt * 32 + r32;
-  bf16x8 w2f[18];
-#pragma unroll
-  for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
-  const float bias2 = b2[oc2];
-  resident_fence(w1f, bias1);
-  resident_fence(w2f, bias2);
-
-  // input prefetch: thread owns pixels p = tid + 256*i (i < 4), 3 channels each
-  float pf[4][3];
-  int img = blockIdx.x;
-  auto load_img = [&](int im) {
-    const float* xb = x + (size_t)im * 3072;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) pf[i][c] = xb[c * 1024 + tid + 256 * i];
-  };
-  if (img < B) load_img(img);
-  __syncthreads();
-
-  // per-lane constant parts of the LDS addresses
-  const int c1_lane = ((r32 >> 3) * V2_XW + (r32 & 7) + 2 * h) * 8;              // conv1 A base (bytes)
-  const int c2_lane = V2_A1_OFF + ((r32 >> 3) * V2_A1W + (r32 & 7)) * V2_A1P + h * 16;  // conv2 A base
-  const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);  // pooled pixel this lane stores after the DPP gather
-  const int cb = r32 & ~3;
-
-  for (; img < B; img += gridDim.x) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = tid + 256 * i, yy = p >> 5, xx = p & 31;
-      uint2 v;
-      v.x = pack2bf(pf[i][0], pf[i][1]);
-      v.y = pack2bf(pf[i][2], 0.f);
-      *reinterpret_cast<uint2*>(smem + ((yy + 1) * V2_XW + xx + 1) * 8) = v;
-    }
-    __syncthreads();
-
-    // ---- conv1: 32 tiles of 4x8 output pixels, 3 k-steps each ----
-    for (int t = wave; t < 32; t += 4) {
-      const int ty = t >> 2, tx = t & 3;
-      const char* abase = smem + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
-        const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
-        bf16x8 a;
-        a[0] = (short)(lo.x & 0xffff); a[1] = (short)(lo.x >> 16); a[2] = (short)(lo.y & 0xffff); a[3] = (short)(lo.y >> 16);
-        a[4] = (short)(hi.x & 0xffff); a[5] = (short)(hi.x >> 16); a[6] = (short)(hi.y & 0xffff); a[7] = (short)(hi.y >> 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
-      }
-      float v[4];
-#pragma unroll
-      for (int qy = 0; qy < 2; ++qy)
-#pragma unroll
-        for (int qx = 0; qx < 2; ++qx) {
-          const int g0 = (2 * qy) * 4 + 2 * qx;
-          v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
-        }
-      // gather 4 channels of one pooled pixel per lane (quad DPP exchanges)
-      const bool odd = r32 & 1;
-      const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
-      const float r0 = __int_as_float(dpp_xor1(s0)), r1 = __int_as_float(dpp_xor1(s1));
-      uint32_t u0, u1;
-      if (!odd) { u0 = pack2bf(v[0], r0); u1 = pack2bf(v[1], r1); }
-      else { u0 = pack2bf(r0, v[2]); u1 = pack2bf(r1, v[3]); }
-      const bool hi2 = r32 & 2;
-      const uint32_t snd = hi2 ? u0 : u1;
-      const uint32_t rcv = (uint32_t)dpp_xor2((int)snd);
-      const uint32_t mine = hi2 ? u1 : u0;
-      uint2 w;
-      w.x = hi2 ? rcv : mine;
-      w.y = hi2 ? mine : rcv;
-      const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
-      *reinterpret_cast<uint2*>(smem + V2_A1_OFF + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
-    }
-    __syncthreads();
-
-    const int nimg = img + gridDim.x;
-    if (nimg < B) load_img(nimg);
-
-    // ---- conv2 ----
-    {
-      f32x16 acc[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
-      const int mt0 = (wave >> 1) * 4;
-      conv2_mainloop(smem + c2_lane, w2f, acc, mt0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
-#pragma unroll
-        for (int qy = 0; qy < 2; ++qy) {
-          float pv[2];
-#pragma unroll
-          for (int qx = 0; qx < 2; ++qx) {
-            const int g0 = (2 * qy) * 4 + 2 * qx;
-            pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias2, 0.f);
-          }
-          const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;
-          *reinterpret_cast<uint32_t*>(smem + V2_OB_OFF + oc2 * V2_OBP + (PY * 8 + PX) * 2) = pack2bf(pv[0], pv[1]);
-        }
-      }
-    }
-    __syncthreads();
-    {
-      // 64 channel rows x 128 B -> global (coalesced 16-B stores; reads 2 x 8 B from the padded image)
-      int4* dst = reinterpret_cast<int4*>(out + (size_t)img * 4096);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = tid + 256 * u;            // 16-B chunk index 0..511
-        const int ch = e >> 3, j = e & 7;
-        const char* src = smem + V2_OB_OFF + ch * V2_OBP + j * 16;
-        const uint2 a = *reinterpret_cast<const uint2*>(src), b = *reinterpret_cast<const uint2*>(src + 8);
-        dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
-// Stage 0, v3: wave-specialised software pipeline (512 threads, 1 WG per CU).
+// Stage-0 pipeline design (v3, refined by v4 below): wave-specialised software pipeline (512 threads, 1 WG per CU).
 // Waves 0-3 ("P") stage the input and run conv1 for image k+1 while waves 4-7
 // ("C") run conv2 for image k, so every SIMD hosts one VALU/LDS-heavy wave and
 // one MFMA-heavy wave at the same time (separate pipes; MI355X_MICROARCH
@@ -458,203 +170,6 @@ constexpr int V3_A1_OFF = V2_XIN_BYTES;                                  // 1088
 constexpr int V3_OB_OFF = V3_A1_OFF + 2 * V2_A1_BYTES;                   // 80000
 constexpr int V3_OB_BYTES = 64 * V2_OBP;                                 // 8704
 constexpr int V3_LDS = V3_OB_OFF + 2 * V3_OB_BYTES;                      // 97408
-// conv1 tiles run by producer waves (the rest by consumers): a launch
-// argument so the producer/consumer balance can be A/B'd in one process
-// (bench/cifar_stamps.py --pt); default fitted from the phase stamps.
-static int g_v3_pt = 24;
-
-template <bool STAMPS>
-__global__ __launch_bounds__(512, 1) void cifar_stage0_v3_kernel(
-    const float* __restrict__ x, bf16_t* __restrict__ out, const bf16_t* __restrict__ w1p,
-    const float* __restrict__ b1, const bf16_t* __restrict__ w2p, const float* __restrict__ b2, int B,
-    unsigned long long* __restrict__ stamps, int V3_PT) {
-  __shared__ __attribute__((aligned(16))) char smem[V3_LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // diagnostic: cycles in [phase A, barrier 1, phase B, barrier 2] for wave 0 (P) and wave 4 (C)
-  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = 0;
-  auto stamp = [&](int slot) {
-    if constexpr (STAMPS) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_sched_barrier(0);
-      if (slot >= 0) st_acc[slot] += t - st_t;
-      st_t = t;
-    }
-  };
-  const bool producer = wave < 4;
-  const int rw = wave & 3;            // wave index within its role
-  const int rt = tid & 255;           // thread index within its role
-  const int h = lane >> 5, r32 = lane & 31;
-  const int n = B > (int)blockIdx.x ? (B - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-
-  for (int i = tid; i < V3_OB_OFF / 16; i += 512) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
-
-  // resident weights: every wave runs conv1 tiles (conv1 weights, 12 VGPRs);
-  // consumer waves also hold their conv2 N-tile (72 VGPRs)
-  bf16x8 w1f[3];
-  bf16x8 w2f[18];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(w1p + r32 * 48 + s * 16 + h * 8);
-  const float bias1 = b1[r32];
-  float bias = 0.f;
-  int oc2 = 0;
-  if (!producer) {
-    oc2 = (rw & 1) * 32 + r32;
-#pragma unroll
-    for (int s = 0; s < 18; ++s) w2f[s] = *reinterpret_cast<const bf16x8*>(w2p + oc2 * 288 + s * 16 + h * 8);
-    bias = b2[oc2];
-  }
-  // Retire the weight loads here, once: otherwise hipcc's waitcnt pass waits
-  // for them at their first use inside the loop with vmcnt(0), which also
-  // drains the in-flight input prefetch (HBM latency on every conv1 tile).
-  resident_fence(w1f, bias1);
-  if (!producer) resident_fence(w2f, bias);
-  float pf[4][3];
-  auto load_img = [&](int k) {
-    const float* xb = x + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 3072;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) pf[i][c] = xb[c * 1024 + rt + 256 * i];
-  };
-  if (producer && n > 0) load_img(0);
-  __syncthreads();
-
-  const int c1_lane = ((r32 >> 3) * V2_XW + (r32 & 7) + 2 * h) * 8;
-  const int c2_lane = ((r32 >> 3) * V2_A1W + (r32 & 7)) * V2_A1P + h * 16;
-  const int q = ((r32 & 1) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
-  const int cb = r32 & ~3;
-
-  // one conv1 output tile (4x8 pixels x 32 channels) -> pooled 2x4 x 32 in act1 `a1`
-  auto conv1_tile = [&](int t, char* a1) {
-    const int ty = t >> 2, tx = t & 3;
-    const char* abase = smem + c1_lane + ((4 * ty) * V2_XW + 8 * tx) * 8;
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const uint2 lo = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8);
-      const uint2 hi = *reinterpret_cast<const uint2*>(abase + s * V2_XW * 8 + 8);
-      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w1f[s], acc, 0, 0, 0);
-    }
-    float v[4];
-#pragma unroll
-    for (int qy = 0; qy < 2; ++qy)
-#pragma unroll
-      for (int qx = 0; qx < 2; ++qx) {
-        const int g0 = (2 * qy) * 4 + 2 * qx;
-        v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
-      }
-    const bool odd = r32 & 1;
-    const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
-    const float r0 = __int_as_float(dpp_xor1(s0)), r1 = __int_as_float(dpp_xor1(s1));
-    uint32_t u0, u1;
-    if (!odd) { u0 = pack2bf(v[0], r0); u1 = pack2bf(v[1], r1); }
-    else { u0 = pack2bf(r0, v[2]); u1 = pack2bf(r1, v[3]); }
-    const bool hi2 = r32 & 2;
-    const uint32_t rcv = (uint32_t)dpp_xor2((int)(hi2 ? u0 : u1));
-    const uint32_t mine = hi2 ? u1 : u0;
-    uint2 w;
-    w.x = hi2 ? rcv : mine;
-    w.y = hi2 ? mine : rcv;
-    const int Y = 2 * ty + (q >> 1) + 1, X = 4 * tx + 2 * h + (q & 1) + 1;
-    *reinterpret_cast<uint2*>(a1 + (Y * V2_A1W + X) * V2_A1P + cb * 2) = w;
-  };
-
-  for (int it = 0; it <= n; ++it) {
-    stamp(-1);
-    // ---------------- phase A ----------------
-    if (producer) {
-      if (it < n) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = rt + 256 * i, yy = p >> 5, xx = p & 31;
-          uint2 v;
-          v.x = pack2bf(pf[i][0], pf[i][1]);
-          v.y = pack2bf(pf[i][2], 0.f);
-          *reinterpret_cast<uint2*>(smem + ((yy + 1) * V2_XW + xx + 1) * 8) = v;
-        }
-      }
-    } else if (it >= 2) {
-      const int k = it - 2;
-      int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
-      const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = rt + 256 * u, ch = e >> 3, j = e & 7;
-        const uint2 a = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16);
-        const uint2 b = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16 + 8);
-        dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
-      }
-    }
-    stamp(0);
-    __syncthreads();
-    stamp(1);
-    // ---------------- phase B ----------------
-    if (producer) {
-      if (it < n) {
-        // xin already holds image `it`: the prefetch registers are free, so the
-        // next image's HBM latency hides under conv1 (not in phase A).
-        if (it + 1 < n) load_img(it + 1);
-        char* a1 = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
-#pragma unroll 2
-        for (int t = rw; t < V3_PT; t += 4) conv1_tile(t, a1);
-      }
-    } else if (it >= 1) {
-      const int k = it - 1;
-      const char* a1 = smem + V3_A1_OFF + (k & 1) * V2_A1_BYTES + c2_lane;
-      char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
-      f32x16 acc[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
-      const int mt0 = (rw >> 1) * 4;
-      conv2_mainloop(a1, w2f, acc, mt0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int t2 = mt0 + i, ty2 = t2 >> 1, tx2 = t2 & 1;
-#pragma unroll
-        for (int qy = 0; qy < 2; ++qy) {
-          float pv[2];
-#pragma unroll
-          for (int qx = 0; qx < 2; ++qx) {
-            const int g0 = (2 * qy) * 4 + 2 * qx;
-            pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
-          }
-          const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;
-          *reinterpret_cast<uint32_t*>(ob + oc2 * V2_OBP + (PY * 8 + PX) * 2) = pack2bf(pv[0], pv[1]);
-        }
-      }
-    }
-    if (!producer && it < n) {  // consumers take the last conv1 tiles of image `it` (load balance)
-      char* a1w = smem + V3_A1_OFF + (it & 1) * V2_A1_BYTES;
-      for (int t = V3_PT + rw; t < 32; t += 4) conv1_tile(t, a1w);
-    }
-    stamp(2);
-    __syncthreads();
-    stamp(3);
-  }
-  // drain: the last image's output staging
-  if (!producer && n >= 1) {
-    const int k = n - 1;
-    int4* dst = reinterpret_cast<int4*>(out + (size_t)(blockIdx.x + (size_t)k * gridDim.x) * 4096);
-    const char* ob = smem + V3_OB_OFF + (k & 1) * V3_OB_BYTES;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = rt + 256 * u, ch = e >> 3, j = e & 7;
-      const uint2 a = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16);
-      const uint2 b = *reinterpret_cast<const uint2*>(ob + ch * V2_OBP + j * 16 + 8);
-      dst[e] = make_int4((int)a.x, (int)a.y, (int)b.x, (int)b.y);
-    }
-  }
-  if constexpr (STAMPS) {
-    if ((wave == 0 || wave == 4) && lane == 0) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) stamps[(blockIdx.x * 2 + (wave >> 2)) * 4 + s] = st_acc[s];
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Stage 0, v4: v3 with ONE barrier per image.  v3's phase A (input regs -> xin,
@@ -867,28 +382,8 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
 
 using namespace dnn;
 
-extern "C" int dnn_cifar_stage0_v3(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
-                                   const float* b2, int B, int grid, hipStream_t st) {
-  if (B <= 0) return 0;
-  if (grid <= 0) grid = 256;
-  if (grid > B) grid = B;
-  hipLaunchKernelGGL((cifar_stage0_v3_kernel<false>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
-                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, nullptr, g_v3_pt);
-  return (int)hipGetLastError();
-}
 
-// Diagnostic build: per-WG [P, C] x [phaseA, barrier1, phaseB, barrier2] cycle sums (s_memtime).
-extern "C" int dnn_cifar_stage0_v3_stamps(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
-                                          const float* b2, int B, int grid, unsigned long long* stamps, hipStream_t st) {
-  if (B <= 0) return 0;
-  if (grid <= 0) grid = 256;
-  if (grid > B) grid = B;
-  hipLaunchKernelGGL((cifar_stage0_v3_kernel<true>), dim3(grid), dim3(512), 0, st, x, (bf16_t*)out,
-                     (const bf16_t*)w1p, b1, (const bf16_t*)w2p, b2, B, stamps, g_v3_pt);
-  return (int)hipGetLastError();
-}
-
-static int g_v4_pt = 32;  // bench/cifar_ab.py: producers run all conv1 tiles (paired), consumers only conv2
+static int g_v4_pt = 32;  // A/B-fitted: producers run all conv1 tiles (paired), consumers only conv2
 
 extern "C" int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
                                    const float* b2, int B, int grid, hipStream_t st) {
@@ -906,31 +401,6 @@ extern "C" int dnn_cifar_set_v4_pt(int pt) {
   return 0;
 }
 
-extern "C" int dnn_cifar_set_v3_pt(int pt) {
-  if (pt < 0 || pt > 32 || pt % 4 != 0) return -1;
-  g_v3_pt = pt;
-  return 0;
-}
-
-extern "C" int dnn_cifar_stage0_v2(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
-                                   const float* b2, int B, int grid, hipStream_t st) {
-  if (B <= 0) return 0;
-  if (grid <= 0) grid = 512;
-  if (grid > B) grid = B;
-  hipLaunchKernelGGL(cifar_stage0_v2_kernel, dim3(grid), dim3(256), 0, st, x, (bf16_t*)out, (const bf16_t*)w1p, b1,
-                     (const bf16_t*)w2p, b2, B);
-  return (int)hipGetLastError();
-}
-
-extern "C" int dnn_cifar_stage0(const float* x, void* out, const void* w1p, const float* b1, const void* w2p,
-                                const float* b2, int B, int grid, hipStream_t st) {
-  if (B <= 0) return 0;
-  if (grid <= 0) grid = 512;
-  if (grid > B) grid = B;
-  hipLaunchKernelGGL(cifar_stage0_kernel, dim3(grid), dim3(256), 0, st, x, (bf16_t*)out, (const bf16_t*)w1p, b1,
-                     (const bf16_t*)w2p, b2, B);
-  return (int)hipGetLastError();
-}
 
 extern "C" int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
                                    hipStream_t st) {

@@ -1,16 +1,24 @@
-"""CIFAR-10 ConvNet on the fused gfx950 kernels (``csrc/kernels/cifar_fused.hip``).
+"""CIFAR-10 ConvNet on the fused gfx950 kernels.
 
-Weight packing happens once at load (reference ``node.py:305-306`` only moves
+Two precisions, packed once at load (reference ``node.py:305-306`` only moves
 fp32 modules to the device):
 
-* conv1 ``(32,3,3,3)`` -> ``w1p [32][32]`` bf16, im2col column ``k = c*9+ky*3+kx``
-  (27 real, 5 zero) = the MFMA B-operand rows;
-* conv2 ``(64,32,3,3)`` -> ``w2p [64][288]`` bf16 with ``k = (ky*3+kx)*32 + c``
-  to match the HWC activation image in LDS;
-* fc1 stays ``[512][4096]`` bf16 (already K-contiguous for the GEMM);
-* fc2 ``(10,512)`` -> ``[16][512]`` bf16 zero-padded to one MFMA N-tile.
-Biases are fp32.  The stage-boundary tensor is ``(B,4096)`` bf16 in the
-reference's NCHW flatten order, so the split matches ``cifar_model_parts.py:41``.
+* ``fp32`` (the reference's precision, default): ``csrc/kernels/cifar_x3.hip``.
+  Every fp32 operand is split into bf16 hi + lo and each product is three bf16
+  MFMAs (hi*hi + hi*lo + lo*hi) accumulated in fp32.  Stage boundary tensor
+  ``(B,4096)`` fp32 exactly as the reference ships it (``node.py:45-48``).
+  fc1 runs as ONE bf16 GEMM over K' = 3*4096 on ``[A_hi | A_hi | A_lo]`` x
+  ``[W_hi | W_lo | W_hi]`` with a ReLU + fp32-out epilogue.
+* ``bf16``: ``csrc/kernels/cifar_fused.hip`` (v4 persistent kernel), bf16
+  boundary, an explicitly reduced-precision mode.
+
+Weight layouts:
+
+* conv1 ``(32,3,3,3)`` -> ``[32][48]`` with ``k = ky*16 + kx*4 + c`` (kx<3, c<3 real);
+* conv2 ``(64,32,3,3)`` -> ``[64][288]`` with ``k = (ky*3+kx)*32 + c`` (HWC activation image);
+* fc1 ``[512][4096]`` (K-contiguous for the GEMM), fc2 ``(10,512)`` -> ``[16][512]``
+  zero-padded to one MFMA N-tile.  Biases are fp32.
+The flatten order is the reference's NCHW ``c*64 + h*8 + w`` (``cifar_model_parts.py:41``).
 """
 from __future__ import annotations
 
@@ -22,73 +30,103 @@ import torch
 from ._lib import check, lib, ptr, stream_ptr
 from .gemm import ACT_RELU, linear
 
+PRECISIONS = ("fp32", "bf16")
+
+
+def split_bf16(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 -> (hi, lo) bf16 with hi + lo == w to ~2^-17 relative."""
+    w = w.float()
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    return hi, lo
+
+
+def _conv1_k48(sd) -> torch.Tensor:
+    w = torch.zeros(32, 3, 4, 4)  # (oc, ky, kx, c) zero-padded kx=3, c=3
+    w[:, :, :3, :3] = sd["conv1.weight"].float().permute(0, 2, 3, 1)
+    return w.reshape(32, 48)
+
+
+def _conv2_k288(sd) -> torch.Tensor:
+    return sd["conv2.weight"].float().permute(0, 2, 3, 1).reshape(64, 288)  # (oc, ky, kx, c)
+
+
+def _fc2_pad(sd) -> torch.Tensor:
+    w = torch.zeros(16, 512)
+    w[:10] = sd["fc2.weight"].float()
+    return w
+
 
 @dataclass
 class CifarStage0Weights:
-    w1p: torch.Tensor      # v1: [32][32], k = c*9+ky*3+kx
+    precision: str
     b1: torch.Tensor
-    w2p: torch.Tensor
     b2: torch.Tensor
-    w1p2: torch.Tensor = None  # v2: [32][48], k = ky*16 + kx*4 + c (kx<3, c<3 real)
-
-
-STAGE0_VARIANT = 4  # v4: single-barrier pipeline (csrc/kernels/cifar_fused.hip); 1-3 kept for A/B
+    w1: torch.Tensor = None    # bf16: [32][48]
+    w2: torch.Tensor = None    # bf16: [64][288]
+    w1h: torch.Tensor = None   # fp32 path: split conv weights
+    w1l: torch.Tensor = None
+    w2h: torch.Tensor = None
+    w2l: torch.Tensor = None
 
 
 @dataclass
 class CifarHeadWeights:
-    w_fc1: torch.Tensor
-    b_fc1: torch.Tensor
-    w_fc2p: torch.Tensor
-    b_fc2: torch.Tensor
+    precision: str
+    w_fc1: torch.Tensor = None   # bf16: [512][4096]; fp32: [512][3*4096] = [hi | lo | hi]
+    b_fc1: torch.Tensor = None
+    w_fc2: torch.Tensor = None   # bf16: [16][512]
+    w_fc2h: torch.Tensor = None  # fp32 path: split fc2
+    w_fc2l: torch.Tensor = None
+    b_fc2: torch.Tensor = None
 
 
-def pack_stage0(sd: Dict[str, torch.Tensor], device) -> CifarStage0Weights:
-    w1 = sd["conv1.weight"].float().reshape(32, 27)
-    w1p = torch.zeros(32, 32)
-    w1p[:, :27] = w1
-    w2 = sd["conv2.weight"].float().permute(0, 2, 3, 1).reshape(64, 288)  # (oc, ky, kx, c)
-    w1p2 = torch.zeros(32, 3, 4, 4)  # (oc, ky, kx, c) zero-padded kx=3, c=3
-    w1p2[:, :, :3, :3] = sd["conv1.weight"].float().permute(0, 2, 3, 1)
-    return CifarStage0Weights(
-        w1p=w1p.to(device=device, dtype=torch.bfloat16).contiguous(),
-        b1=sd["conv1.bias"].float().to(device).contiguous(),
-        w2p=w2.to(device=device, dtype=torch.bfloat16).contiguous(),
-        b2=sd["conv2.bias"].float().to(device).contiguous(),
-        w1p2=w1p2.reshape(32, 48).to(device=device, dtype=torch.bfloat16).contiguous())
+def _check_precision(p: str) -> str:
+    if p not in PRECISIONS:
+        raise ValueError(f"CIFAR precision must be one of {PRECISIONS}, got {p!r}")
+    return p
 
 
-def pack_head(sd: Dict[str, torch.Tensor], device, fc1: bool = True, fc2: bool = True) -> CifarHeadWeights:
-    w_fc1 = b_fc1 = w2p = b_fc2 = None
+def pack_stage0(sd: Dict[str, torch.Tensor], device, precision: str = "fp32") -> CifarStage0Weights:
+    _check_precision(precision)
+    b1 = sd["conv1.bias"].float().to(device).contiguous()
+    b2 = sd["conv2.bias"].float().to(device).contiguous()
+    w1, w2 = _conv1_k48(sd), _conv2_k288(sd)
+    if precision == "bf16":
+        return CifarStage0Weights("bf16", b1, b2,
+                                  w1=w1.to(device=device, dtype=torch.bfloat16).contiguous(),
+                                  w2=w2.to(device=device, dtype=torch.bfloat16).contiguous())
+    (w1h, w1l), (w2h, w2l) = split_bf16(w1), split_bf16(w2)
+    dv = lambda t: t.to(device).contiguous()  # noqa: E731
+    return CifarStage0Weights("fp32", b1, b2, w1h=dv(w1h), w1l=dv(w1l), w2h=dv(w2h), w2l=dv(w2l))
+
+
+def pack_head(sd: Dict[str, torch.Tensor], device, fc1: bool = True, fc2: bool = True,
+              precision: str = "fp32") -> CifarHeadWeights:
+    _check_precision(precision)
+    w = CifarHeadWeights(precision)
     if fc1:
-        w_fc1 = sd["fc1.weight"].to(device=device, dtype=torch.bfloat16).contiguous()
-        b_fc1 = sd["fc1.bias"].float().to(device).contiguous()
+        f = sd["fc1.weight"].float()
+        if precision == "bf16":
+            w.w_fc1 = f.to(device=device, dtype=torch.bfloat16).contiguous()
+        else:
+            hi, lo = split_bf16(f)
+            w.w_fc1 = torch.cat([hi, lo, hi], dim=1).to(device).contiguous()
+        w.b_fc1 = sd["fc1.bias"].float().to(device).contiguous()
     if fc2:
-        w2 = torch.zeros(16, 512)
-        w2[:10] = sd["fc2.weight"].float()
-        w2p = w2.to(device=device, dtype=torch.bfloat16).contiguous()
-        b_fc2 = sd["fc2.bias"].float().to(device).contiguous()
-    return CifarHeadWeights(w_fc1=w_fc1, b_fc1=b_fc1, w_fc2p=w2p, b_fc2=b_fc2)
+        f2 = _fc2_pad(sd)
+        if precision == "bf16":
+            w.w_fc2 = f2.to(device=device, dtype=torch.bfloat16).contiguous()
+        else:
+            hi, lo = split_bf16(f2)
+            w.w_fc2h, w.w_fc2l = hi.to(device).contiguous(), lo.to(device).contiguous()
+        w.b_fc2 = sd["fc2.bias"].float().to(device).contiguous()
+    return w
 
 
-def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Unit 2: (B,4096) bf16 -> relu(fc1) (B,512) bf16 on the MFMA GEMM."""
-    if h.dtype != torch.bfloat16 or tuple(h.shape[1:]) != (4096,):
-        raise ValueError(f"fc1: expected bf16 (B,4096), got {h.dtype} {tuple(h.shape)}")
-    return linear(h, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
-
-
-def head_tail(hid: torch.Tensor, w: CifarHeadWeights, probs: Optional[torch.Tensor] = None,
-              pred: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Unit 3: (B,512) bf16 -> fc2 + softmax (B,10) fp32 + per-row argmax (B,) int32."""
-    if hid.dtype != torch.bfloat16 or tuple(hid.shape[1:]) != (512,) or not hid.is_contiguous():
-        raise ValueError(f"head_tail: expected contiguous bf16 (B,512), got {hid.dtype} {tuple(hid.shape)}")
-    B = hid.shape[0]
-    probs = probs if probs is not None else torch.empty((B, 10), dtype=torch.float32, device=hid.device)
-    pred = pred if pred is not None else torch.empty((B,), dtype=torch.int32, device=hid.device)
-    check(lib().cifar_head_tail(ptr(hid), ptr(w.w_fc2p), ptr(w.b_fc2), ptr(probs), ptr(pred), B, stream_ptr()),
-          "cifar_head_tail")
-    return probs, pred
+def act_dtype(precision: str) -> torch.dtype:
+    """dtype of the stage-boundary activations (flattened conv map, fc1 hidden)."""
+    return torch.float32 if _check_precision(precision) == "fp32" else torch.bfloat16
 
 
 STAGE0_GRID = 0  # persistent stage-0 workgroups; 0 = one per CU (256)
@@ -96,52 +134,75 @@ STAGE0_GRID = 0  # persistent stage-0 workgroups; 0 = one per CU (256)
 
 def set_stage0_grid(grid: int = 0) -> None:
     """Persistent stage-0 grid size (0 = one workgroup per CU).  With fewer
-    workgroups than CUs the spare CUs stay free for concurrent kernels — the
-    RCCL all-to-all of the multi-GPU placements cannot start a workgroup on a
-    CU the stage-0 kernel holds (its 2 waves/SIMD fill every VGPR)."""
+    workgroups than CUs the spare CUs stay free for concurrent kernels (an RCCL
+    hop kernel cannot start a workgroup on a CU the stage-0 kernel holds)."""
     global STAGE0_GRID
     STAGE0_GRID = int(grid)
 
 
+def _check_act(t: torch.Tensor, shape, dtype, what: str) -> None:
+    if t.dtype != dtype or tuple(t.shape[1:]) != tuple(shape) or not t.is_contiguous():
+        raise ValueError(f"{what}: expected contiguous {dtype} (B,{','.join(map(str, shape))}), "
+                         f"got {t.dtype} {tuple(t.shape)}")
+
+
 def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.Tensor] = None,
-                   grid: int = 0, variant: Optional[int] = None) -> torch.Tensor:
-    """x: (B,3,32,32) fp32 contiguous -> (B,4096) bf16."""
+                   grid: int = 0) -> torch.Tensor:
+    """Units 0-1: x (B,3,32,32) fp32 contiguous -> (B,4096) fp32 (or bf16 in bf16 mode)."""
     grid = grid or STAGE0_GRID
-    if x.dtype != torch.float32 or not x.is_contiguous() or tuple(x.shape[1:]) != (3, 32, 32):
-        raise ValueError(f"stage0: expected contiguous fp32 (B,3,32,32), got {x.dtype} {tuple(x.shape)}")
+    _check_act(x, (3, 32, 32), torch.float32, "stage0 input")
     B = x.shape[0]
+    dt = act_dtype(w.precision)
     if out is None:
-        out = torch.empty((B, 4096), dtype=torch.bfloat16, device=x.device)
-    if tuple(out.shape) != (B, 4096) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        out = torch.empty((B, 4096), dtype=dt, device=x.device)
+    if tuple(out.shape) != (B, 4096) or out.dtype != dt or not out.is_contiguous():
         raise ValueError("stage0: bad output buffer")
-    v = variant or STAGE0_VARIANT
-    if v == 4:
-        check(lib().cifar_stage0_v4(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
-                                    stream_ptr()), "cifar_stage0_v4")
-    elif v == 3:
-        check(lib().cifar_stage0_v3(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
-                                    stream_ptr()), "cifar_stage0_v3")
-    elif v == 2:
-        check(lib().cifar_stage0_v2(ptr(x), ptr(out), ptr(w.w1p2), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
-                                    stream_ptr()), "cifar_stage0_v2")
+    if w.precision == "fp32":
+        check(lib().cifar_stage0_x3(ptr(x), ptr(out), ptr(w.w1h), ptr(w.w1l), ptr(w.b1), ptr(w.w2h), ptr(w.w2l),
+                                    ptr(w.b2), B, grid, stream_ptr()), "cifar_stage0_x3")
     else:
-        check(lib().cifar_stage0(ptr(x), ptr(out), ptr(w.w1p), ptr(w.b1), ptr(w.w2p), ptr(w.b2), B, grid,
-                                 stream_ptr()), "cifar_stage0")
+        check(lib().cifar_stage0_v4(ptr(x), ptr(out), ptr(w.w1), ptr(w.b1), ptr(w.w2), ptr(w.b2), B, grid,
+                                    stream_ptr()), "cifar_stage0_v4")
     return out
+
+
+def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor] = None,
+                scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Unit 2: (B,4096) -> relu(fc1) (B,512) on the MFMA GEMM (fp32: split operand,
+    ``scratch`` = (>=B, 12288) bf16 for the [hi | hi | lo] rows)."""
+    dt = act_dtype(w.precision)
+    _check_act(h, (4096,), dt, "fc1 input")
+    B = h.shape[0]
+    if w.precision == "bf16":
+        return linear(h, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
+    if scratch is None or scratch.shape[0] < B or tuple(scratch.shape[1:]) != (3 * 4096,):
+        scratch = torch.empty((B, 3 * 4096), dtype=torch.bfloat16, device=h.device)
+    a3 = scratch[:B]
+    check(lib().cifar_split3(ptr(h), 4096, ptr(a3), 3 * 4096, B, 4096, stream_ptr()), "cifar_split3")
+    if out is None:
+        out = torch.empty((B, 512), dtype=torch.float32, device=h.device)
+    return linear(a3, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
+
+
+def head_tail(hid: torch.Tensor, w: CifarHeadWeights, probs: Optional[torch.Tensor] = None,
+              pred: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Unit 3: (B,512) -> fc2 + softmax (B,10) fp32 + per-row argmax (B,) int32."""
+    _check_act(hid, (512,), act_dtype(w.precision), "head_tail input")
+    B = hid.shape[0]
+    probs = probs if probs is not None else torch.empty((B, 10), dtype=torch.float32, device=hid.device)
+    pred = pred if pred is not None else torch.empty((B,), dtype=torch.int32, device=hid.device)
+    if w.precision == "fp32":
+        check(lib().cifar_head_tail_x3(ptr(hid), ptr(w.w_fc2h), ptr(w.w_fc2l), ptr(w.b_fc2), ptr(probs), ptr(pred),
+                                       B, stream_ptr()), "cifar_head_tail_x3")
+    else:
+        check(lib().cifar_head_tail(ptr(hid), ptr(w.w_fc2), ptr(w.b_fc2), ptr(probs), ptr(pred), B, stream_ptr()),
+              "cifar_head_tail")
+    return probs, pred
 
 
 def head_forward(h: torch.Tensor, w: CifarHeadWeights, hid: Optional[torch.Tensor] = None,
                  probs: Optional[torch.Tensor] = None, pred: Optional[torch.Tensor] = None
                  ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """h: (B,4096) bf16 -> (probs (B,10) fp32, pred (B,) int32)."""
-    if h.dtype != torch.bfloat16 or tuple(h.shape[1:]) != (4096,) or not h.is_contiguous():
-        raise ValueError(f"head: expected contiguous bf16 (B,4096), got {h.dtype} {tuple(h.shape)}")
-    B = h.shape[0]
-    dev = h.device
-    hid = hid if hid is not None else torch.empty((B, 512), dtype=torch.bfloat16, device=dev)
-    probs = probs if probs is not None else torch.empty((B, 10), dtype=torch.float32, device=dev)
-    pred = pred if pred is not None else torch.empty((B,), dtype=torch.int32, device=dev)
-    linear(h, w.w_fc1, w.b_fc1, act=ACT_RELU, out=hid)
-    check(lib().cifar_head_tail(ptr(hid), ptr(w.w_fc2p), ptr(w.b_fc2), ptr(probs), ptr(pred), B, stream_ptr()),
-          "cifar_head_tail")
-    return probs, pred
+    """Units 2-3: h (B,4096) -> (probs (B,10) fp32, pred (B,) int32)."""
+    hid = fc1_forward(h, w, out=hid)
+    return head_tail(hid, w, probs, pred)

@@ -2,8 +2,9 @@
 
 ``StageCompute`` is what a pipeline rank runs per microbatch.  Two families:
 
-* ``CifarHipStage`` — the MI355X path: fused gfx950 kernels over bf16 weights
-  packed once at load (``ops/cifar.py``); no torch op runs in ``forward``.
+* ``CifarHipStage`` — the MI355X path: fused gfx950 kernels over weights
+  packed once at load (``ops/cifar.py``; fp32 by default, the reference's
+  precision, or bf16); no torch op runs in ``forward``.
 * ``TorchStage`` — the golden torch module on CPU (fp32): the data path of the
   reference's CPU/gRPC configuration (``BASELINE.json`` configs[0]) and the
   oracle in tests.  It is never used on a GPU device.
@@ -53,34 +54,42 @@ class CifarHipStage(StageCompute):
     Units 0-1 always run together (the fused conv1/pool/conv2/pool kernel), so
     the supported ranges are (0,1) = reference part 0, (2,3) = reference part 1,
     (0,3) = whole model, and the fc1 cut (0,2) | (3,3) whose stage boundary is
-    the 512-wide hidden (1 KiB/img in bf16 instead of 8 KiB: what the
-    multi-GPU placement uses to cut xGMI traffic 8x, parallel/partition.py
-    ``cifar_cut``)."""
+    the 512-wide hidden (2 KiB/img in fp32 instead of 16 KiB: what the
+    multi-GPU placement uses when the xGMI hop, not compute, would bound the
+    pipeline, parallel/partition.py ``cifar_cut``).
+
+    ``precision`` "fp32" (default, the reference's: fp32 in, fp32 boundary,
+    3-term bf16 split products accumulated in fp32) or "bf16"."""
 
     SUPPORTED = {(0, 1), (2, 3), (0, 3), (0, 2), (3, 3)}
-    _BOUNDARY = {1: (cifar.FLAT_DIM, torch.bfloat16), 2: (512, torch.bfloat16)}
 
-    def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device):
+    def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device,
+                 precision: str = "fp32"):
         from ..ops import cifar as cops
         if (start, end) not in self.SUPPORTED:
             raise ValueError(f"HIP CIFAR backend supports unit ranges {sorted(self.SUPPORTED)}, got ({start},{end})")
         self.start, self.end, self.device = start, end, torch.device(device)
         self.first, self.last = start == 0, end == cifar.NUM_UNITS - 1
+        self.precision = precision
         self._cops = cops
-        self.w0 = cops.pack_stage0(sd, self.device) if start == 0 else None
-        self.wh = cops.pack_head(sd, self.device, fc1=start <= 2 <= end, fc2=end == 3)
+        self.adt = cops.act_dtype(precision)
+        self.w0 = cops.pack_stage0(sd, self.device, precision) if start == 0 else None
+        self.wh = cops.pack_head(sd, self.device, fc1=start <= 2 <= end, fc2=end == 3, precision=precision)
         self._scratch: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def _boundary(self, unit: int):
+        return ((cifar.FLAT_DIM if unit == 1 else 512), self.adt)
 
     def in_spec(self, batch):
         if self.first:
             return (batch, 3, 32, 32), torch.float32
-        w, dt = self._BOUNDARY[self.start - 1]
+        w, dt = self._boundary(self.start - 1)
         return (batch, w), dt
 
     def out_spec(self, batch):
         if self.last:
             return (batch, 10), torch.float32
-        w, dt = self._BOUNDARY[self.end]
+        w, dt = self._boundary(self.end)
         return (batch, w), dt
 
     def _buf(self, batch):
@@ -89,9 +98,11 @@ class CifarHipStage(StageCompute):
             d = self.device
             b = {}
             if self.first and self.end >= 2:
-                b["mid"] = torch.empty((batch, 4096), dtype=torch.bfloat16, device=d)
+                b["mid"] = torch.empty((batch, 4096), dtype=self.adt, device=d)
+            if self.start <= 2 <= self.end and self.precision == "fp32":
+                b["split"] = torch.empty((batch, 3 * 4096), dtype=torch.bfloat16, device=d)
             if self.last:
-                b["hid"] = torch.empty((batch, 512), dtype=torch.bfloat16, device=d)
+                b["hid"] = torch.empty((batch, 512), dtype=self.adt, device=d)
                 b["pred"] = torch.empty((batch,), dtype=torch.int32, device=d)
             self._scratch[batch] = b
         return b
@@ -106,11 +117,14 @@ class CifarHipStage(StageCompute):
             h = self._cops.stage0_forward(h.contiguous(), self.w0, buf["mid"] if self.end >= 2 else out)
             if self.end == 1:
                 return h
+        elif h.dtype != self.adt:
+            h = h.to(self.adt)
         if self.start <= 2 <= self.end:
-            h = self._cops.fc1_forward(h, self.wh, out if self.end == 2 else buf["hid"])
+            h = self._cops.fc1_forward(h.contiguous(), self.wh, out if self.end == 2 else buf["hid"],
+                                       scratch=buf.get("split"))
             if self.end == 2:
                 return h
-        probs, pred = self._cops.head_tail(h, self.wh, out, buf["pred"])
+        probs, pred = self._cops.head_tail(h.contiguous(), self.wh, out, buf["pred"])
         return StageOutput(probs, pred)
 
 

@@ -134,52 +134,77 @@ def test_gemm_silu_mul():
         assert _rel(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("B", [1, 3, 64, 1000])
-def test_cifar_stage0_and_head(B):
-    from distributed_neural_networks_amd.models.cifar import NeuralNetwork, CifarStage
-    from distributed_neural_networks_amd.ops import cifar as cops
-    torch.manual_seed(0)
+def _cifar_golden(seed, B):
+    from distributed_neural_networks_amd.models.cifar import CifarStage, NeuralNetwork
+    torch.manual_seed(seed)
     model = NeuralNetwork().eval()
     sd = model.state_dict()
     x = torch.randn(B, 3, 32, 32)
     with torch.no_grad():
-        ref_mid = CifarStage(0, 1).eval()
-        ref_mid.load_state_dict(sd, strict=False)
-        mid = ref_mid(x)
-        ref_out = model(x)
-    w0 = cops.pack_stage0(sd, DEV)
-    wh = cops.pack_head(sd, DEV)
+        part0 = CifarStage(0, 1).eval()
+        part0.load_state_dict(sd, strict=False)
+        mid = part0(x)
+        ref = model(x)
+    return sd, x, mid, ref
+
+
+@pytest.mark.parametrize("B", [1, 3, 64, 1000])
+def test_cifar_stage0_and_head_bf16(B):
+    from distributed_neural_networks_amd.ops import cifar as cops
+    sd, x, mid, ref_out = _cifar_golden(0, B)
+    w0 = cops.pack_stage0(sd, DEV, "bf16")
+    wh = cops.pack_head(sd, DEV, precision="bf16")
     h = cops.stage0_forward(x.to(DEV), w0)
     torch.cuda.synchronize()
+    assert h.dtype == torch.bfloat16
     assert _rel(h.cpu(), mid) < 1e-2
     probs, pred = cops.head_forward(h, wh)
     torch.cuda.synchronize()
     assert (probs.cpu() - ref_out).abs().max().item() < 2e-2
-    agree = (pred.cpu().long() == ref_out.argmax(1)).float().mean().item()
-    assert agree > 0.9
-    # argmax must be consistent with our own probabilities
+    assert (pred.cpu().long() == ref_out.argmax(1)).float().mean().item() > 0.9
     assert torch.equal(pred.cpu().long(), probs.cpu().argmax(1))
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
-def test_cifar_stage0_variants_agree(variant):
-    from distributed_neural_networks_amd.models.cifar import NeuralNetwork, CifarStage
+@pytest.mark.parametrize("B", [1, 3, 257, 1000])
+def test_cifar_fp32_stage0_and_head(B):
+    """fp32 path (3-term bf16 split on MFMA) against the fp32 torch stages."""
     from distributed_neural_networks_amd.ops import cifar as cops
-    torch.manual_seed(4)
-    sd = NeuralNetwork().state_dict()
+    sd, x, mid, ref_out = _cifar_golden(1, B)
     w0 = cops.pack_stage0(sd, DEV)
-    for B in (1, 5, 300, 4099):
-        x = torch.randn(B, 3, 32, 32)
-        ref = CifarStage(0, 1)
-        ref.load_state_dict(sd, strict=False)
-        with torch.no_grad():
-            r = ref(x)
-        h = cops.stage0_forward(x.to(DEV), w0, variant=variant)
-        assert _rel(h.cpu(), r) < 1e-2, (variant, B)
+    wh = cops.pack_head(sd, DEV)
+    h = cops.stage0_forward(x.to(DEV), w0)
+    torch.cuda.synchronize()
+    assert h.dtype == torch.float32
+    err = (h.cpu() - mid).abs().max().item()
+    assert err <= 2e-5 * max(1.0, mid.abs().max().item()), err
+    probs, pred = cops.head_forward(h, wh)
+    torch.cuda.synchronize()
+    assert (probs.cpu() - ref_out).abs().max().item() <= 1e-5
+    assert torch.equal(pred.cpu().long(), probs.cpu().argmax(1))
 
 
-@pytest.mark.parametrize("cut", [1, 2])
-def test_cifar_stage_cuts(cut):
+def test_cifar_fp32_pipeline_4096_images_matches_reference():
+    """Acceptance: the 2-stage pipeline at the reference's
+    precision on 4096 images: max |dprob| <= 1e-5 vs fp32 torch
+    (cifar_model_parts.py:7-26) and 100 % argmax agreement (rows whose golden
+    top-2 probabilities tie within 1e-6 are excluded as numerically undecidable)."""
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
+    sd, x, _, ref = _cifar_golden(2, 4096)
+    st = [CifarHipStage(sd, 0, 1, DEV), CifarHipStage(sd, 2, 3, DEV)]
+    assert st[0].out_spec(4) == ((4, 4096), torch.float32)
+    out = ColocatedPipeline(st, 4096)(x.to(DEV))
+    torch.cuda.synchronize()
+    dp = (out.probs.cpu() - ref).abs().max().item()
+    assert dp <= 1e-5, dp
+    top2 = ref.topk(2, dim=1).values
+    decidable = (top2[:, 0] - top2[:, 1]) > 1e-6
+    agree = out.pred.cpu().long() == ref.argmax(1)
+    assert bool(agree[decidable].all()), int((~agree[decidable]).sum())
+
+
+@pytest.mark.parametrize("cut,precision", [(1, "fp32"), (2, "fp32"), (1, "bf16"), (2, "bf16")])
+def test_cifar_stage_cuts(cut, precision):
     """Both 2-stage cuts (reference conv|fc and the fc1 cut) reproduce the full model."""
     from distributed_neural_networks_amd.models.cifar import NeuralNetwork
     from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
@@ -187,11 +212,13 @@ def test_cifar_stage_cuts(cut):
     torch.manual_seed(5)
     m = NeuralNetwork().eval()
     sd = m.state_dict()
-    st = [CifarHipStage(sd, 0, cut, DEV), CifarHipStage(sd, cut + 1, 3, DEV)]
+    st = [CifarHipStage(sd, 0, cut, DEV, precision), CifarHipStage(sd, cut + 1, 3, DEV, precision)]
     x = torch.randn(64, 3, 32, 32)
     out = ColocatedPipeline(st, 64)(x.to(DEV))
     torch.cuda.synchronize()
     with torch.no_grad():
         ref = m(x)
-    assert (out.probs.cpu() - ref).abs().max().item() < 2e-2
-    assert st[0].out_spec(8)[0] == (8, 4096 if cut == 1 else 512)
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    assert (out.probs.cpu() - ref).abs().max().item() < tol
+    dt = torch.float32 if precision == "fp32" else torch.bfloat16
+    assert st[0].out_spec(8) == ((8, 4096 if cut == 1 else 512), dt)
