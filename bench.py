@@ -48,7 +48,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="images sourced per GPU per step")
     ap.add_argument("--microbatches", type=int, default=2,
                     help="microbatches per step on N>1 (2 x 32768 rows fill the fc1 GEMM's 256 tiles)")
-    ap.add_argument("--placement", default="interleaved", choices=["interleaved", "linear"])
+    ap.add_argument("--placement", default="linear", choices=["linear", "interleaved"],
+                    help="N>1: linear = the reference topology (one stage per GPU, RCCL send/recv); "
+                         "interleaved = opt-in all-to-all variant")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="compute precision of the headline (fp32 = the reference's)")
+    ap.add_argument("--no_extra", action="store_true", help="skip the extra bf16 / GPT-2 keys")
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
@@ -72,7 +77,7 @@ def dist_setup(n, cpu=False):
     return info
 
 
-def stages_for(device, cut: int = 1):
+def stages_for(device, cut: int = 1, precision: str = "fp32"):
     """The two pipeline stages: units [0..cut] and [cut+1..3] (cut 1 = the reference's conv|fc split)."""
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import CifarHipStage, TorchStage
@@ -81,7 +86,7 @@ def stages_for(device, cut: int = 1):
     if device.type == "cpu":  # schedule-test mode only (never used for a reported number)
         return (TorchStage("cifar10", sd0, 0, cut, True, False, device),
                 TorchStage("cifar10", sd1, cut + 1, 3, False, True, device))
-    return CifarHipStage(sd0, 0, cut, device), CifarHipStage(sd1, cut + 1, 3, device)
+    return CifarHipStage(sd0, 0, cut, device, precision), CifarHipStage(sd1, cut + 1, 3, device, precision)
 
 
 def pick_cut(args, info) -> int:
@@ -122,7 +127,7 @@ def max_over_ranks(info, v):
 def bench_colocated(args, info):
     from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
     dev = info.device
-    s0, s1 = stages_for(dev)
+    s0, s1 = stages_for(dev, 1, args.precision)
     g = torch.Generator(device=dev).manual_seed(0)
     pipe = ColocatedPipeline([s0, s1], args.batch)
     pipe.x.copy_(torch.randn(pipe.x.shape, device=dev, generator=g))
@@ -150,7 +155,7 @@ def bench_colocated(args, info):
 def bench_interleaved(args, info):
     import torch.distributed as dist
     dev, N, r = info.device, info.world, info.rank
-    s0, s1 = stages_for(dev, args._cut)
+    s0, s1 = stages_for(dev, args._cut, args.precision)
     M = max(1, args.microbatches)
     mb = args.batch // M
     per_peer = mb // (N - 1)
@@ -216,7 +221,7 @@ def bench_linear(args, info):
     dev, N, r = info.device, info.world, info.rank
     if N % 2:
         raise SystemExit("linear placement needs an even number of GPUs")
-    s0, s1 = stages_for(dev, args._cut)
+    s0, s1 = stages_for(dev, args._cut, args.precision)
     stage_idx = r % 2
     st = s0 if stage_idx == 0 else s1
     M = max(1, args.microbatches)
@@ -236,6 +241,21 @@ def bench_linear(args, info):
         step()
     t1 = sync_time(info)
     return t1 - t0, mb * M // 2, float("nan"), f"pp2-linear-x{N // 2}"
+
+
+def extra_keys(args, info):
+    """Secondary numbers on the same GPU, same timing discipline: the CIFAR
+    pipeline at reduced (bf16) precision when the headline is fp32."""
+    out = {}
+    if args.precision == "fp32":
+        import copy
+        a = copy.copy(args)
+        a.precision, a.latency_iters = "bf16", 50
+        el, imgs, p50, _ = bench_colocated(a, info)
+        out["bf16_images_per_s"] = round(imgs * args.steps / el, 1)
+        out["bf16_ms_per_step"] = round(el / args.steps * 1e3, 4)
+        out["bf16_p50_latency_ms"] = round(p50, 4)
+    return out
 
 
 def main():
@@ -264,12 +284,15 @@ def main():
     el = max_over_ranks(info, el)
     total = imgs_per_gpu * N * args.steps
     value = total / el
+    extra = {}
+    if N == 1 and not args.no_extra and info.device.type == "cuda":
+        extra = extra_keys(args, info)
     if info.rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
-            "dtype": "bf16", "data": "synthetic (random fp32 images, random-init weights)",
+            "dtype": args.precision, "data": "synthetic (random fp32 images, random-init weights)",
             "p50_latency_ms": None if p50 != p50 else round(p50, 4),
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": imgs_per_gpu * N, "seq_len": None, "parallelism": par,
@@ -278,6 +301,7 @@ def main():
                        "stage_cut": {1: "conv|fc (reference split, 8 KiB/img hop)",
                                      2: "conv+fc1|fc2 (1 KiB/img hop)"}[args._cut]},
         }
+        out.update(extra)
         print(json.dumps(out), flush=True)
     if N > 1:
         from distributed_neural_networks_amd.parallel import comm
