@@ -247,6 +247,23 @@ def extra_keys(args, info):
     """Secondary numbers on the same GPU, same timing discipline: the CIFAR
     pipeline at reduced (bf16) precision when the headline is fp32."""
     out = {}
+    if getattr(args, "gpt", True):
+        # GPT-2 small 4-stage pipeline (BASELINE.json metric, second half): all
+        # 4 stages on this GPU, bf16, B=64 sequences x 512-token prompts,
+        # microbatched decode ring with one HIP graph per microbatch
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        import gpt_bench
+        ga = gpt_bench.parse(["--gpus", "1", "--steps", "32", "--warmup", "4", "--batch", "64", "--prompt", "512",
+                              "--stages", "4", "--dtype", "bf16"])
+        g = gpt_bench.run(ga)
+        out["gpt2_4stage_decode_tok_s"] = g["value"]
+        out["gpt2_4stage_decode_ms_per_step"] = g["ms_per_step"]
+        out["gpt2_4stage_p50_token_ms"] = g["decode_p50_token_latency_ms"]
+        out["gpt2_4stage_prefill_tok_s"] = g["prefill_tokens_per_s"]
+        out["gpt2_4stage_config"] = {"model": "gpt2 (124M, random init)", "stages": 4, "dtype": "bf16",
+                                     "micro_batch": 64, "microbatches": g["config"]["microbatches"],
+                                     "prompt_len": 512, "decode_steps_timed": 32,
+                                     "placement": "4 stages colocated on 1 GPU"}
     if args.precision == "fp32":
         import copy
         a = copy.copy(args)

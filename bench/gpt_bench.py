@@ -59,6 +59,14 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8):
 
 
 def main(args=None):
+    out = run(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    return 0
+
+
+def run(args=None):
+    """Run the bench on every rank; rank 0 returns the JSON record (others None)."""
     if args is None or not hasattr(args, "prompt"):
         base = args
         args = parse([])
@@ -104,16 +112,10 @@ def main(args=None):
     d = model_info(model).cfg.n_embd
     V = model_info(model).cfg.vocab_size
 
-    pos = [torch.zeros((B,), dtype=torch.int32, device=dev) for _ in range(M)]
-    ids = [torch.randint(0, V, (B, T0), device=dev, dtype=torch.int32) for _ in range(M)]
-    xin = [torch.empty((B * T0, d), dtype=torch.bfloat16, device=dev) for _ in range(M)]
-    nid = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(M)]
-
-    def run_group(x, m, Tn):
-        h = x
-        for st in stages:
-            h = st.step(h, pos[m], B, Tn, b0=m * B)
-        return h
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    links = RingLinks(prev=prev, nxt=nxt, back_out=back_to0, back_in=back_from)
+    ring = DecodeRing(stages, links, groups, M, B, use_graphs=not args.no_graph, record=False) if stages else None
+    prompts = [torch.randint(0, V, (B, T0), device=dev, dtype=torch.int32) for _ in range(M)] if grp == 0 else None
 
     def sync():
         torch.cuda.synchronize()
@@ -124,149 +126,47 @@ def main(args=None):
 
     # ---------------- prefill (all microbatches, T0 tokens each) ----------------
     def prefill_round():
-        for m in range(M):
-            pos[m].zero_()
-        for m in range(M):
-            if not stages:
-                continue
-            if grp == 0:
-                x = ids[m]
-            else:
-                x = xin[m][:B * T0]
-                prev.recv(x)
-            y = run_group(x, m, T0)
-            pos[m].add_(T0)
-            if nxt is not None:
-                nxt.send(y)
-            elif stages[-1].last:
-                nid[m].copy_(y.pred)
-        if back_to0 is not None:
-            for m in range(M):
-                back_to0.send(nid[m])
-        if back_from is not None:
-            for m in range(M):
-                back_from.recv(nid[m])
+        if ring is not None:
+            ring.prefill(prompts, T0)
+
+    def finish_prefill():  # the prefill's sampled tokens still travel the back-edge
+        if ring is not None:
+            ring.drain()
 
     prefill_round()
+    finish_prefill()
     t0 = sync()
     for _ in range(args.prefill_iters):
         prefill_round()
+        finish_prefill()
     t1 = sync()
     prefill_s = (t1 - t0) / args.prefill_iters
     prefill_tok = B * M * T0 * replicas
 
-    # ---------------- decode (microbatched ring) ----------------
-    dec_x = [torch.empty((B, d), dtype=torch.bfloat16, device=dev) for _ in range(M)]
-    cur = [n.view(B, 1).clone() for n in nid]
-    lat = []
-
-    def decode_round():
-        for m in range(M):
-            if not stages:
-                continue
-            ta = time.perf_counter()
-            if grp == 0:
-                if groups > 1 and back_from is not None and decode_round.started[m]:
-                    back_from.recv(nid[m])
-                    cur[m].copy_(nid[m].view(B, 1))
-                x = cur[m]
-            else:
-                x = dec_x[m]
-                prev.recv(x)
-            y = run_group(x, m, 1)
-            pos[m].add_(1)
-            if nxt is not None:
-                nxt.send(y)
-            else:
-                if groups > 1:
-                    back_to0.send(y.pred)
-                else:
-                    cur[m].copy_(y.pred.view(B, 1))
-            decode_round.started[m] = True
-            lat.append(time.perf_counter() - ta)
-
-    decode_round.started = [False] * M
-
-    # One HIP graph per microbatch for this group's decode compute (the P2P
-    # hops stay outside: blocking RCCL send/recv order the compute stream).
-    graphs = {}
-    if stages and not args.no_graph:
-        from distributed_neural_networks_amd.runtime.graph import GraphedStep
-        gout = {}
-
-        def body(m):
-            x = cur[m] if grp == 0 else dec_x[m]
-            y = run_group(x, m, 1)
-            pos[m].add_(1)
-            if isinstance(y, torch.Tensor):
-                gout[m] = y
-            else:
-                nid[m].copy_(y.pred)
-            return None
-
-        for m in range(M):
-            snap = pos[m].clone()
-            graphs[m] = GraphedStep(lambda m=m: body(m), dev, warmup=1)
-            pos[m].copy_(snap)
-        torch.cuda.synchronize()
-
-        class _Out:
-            def __init__(self, p):
-                self.pred = p
-
-    def group_step(x, m):
-        if graphs:
-            y = graphs[m]()
-            return gout[m] if m in gout else _Out(nid[m])
-        y = run_group(x, m, 1)
-        pos[m].add_(1)
-        return y
-
-    def decode_round():  # noqa: F811 (graph-aware version)
-        for m in range(M):
-            if not stages:
-                continue
-            ta = time.perf_counter()
-            if grp == 0:
-                if groups > 1 and back_from is not None and decode_round.started[m]:
-                    back_from.recv(nid[m])
-                    cur[m].copy_(nid[m].view(B, 1))
-                x = cur[m]
-            else:
-                x = dec_x[m]
-                prev.recv(x)
-            y = group_step(x, m)
-            if nxt is not None:
-                nxt.send(y)
-            else:
-                if groups > 1:
-                    back_to0.send(y.pred)
-                else:
-                    cur[m].copy_(y.pred.view(B, 1))
-            decode_round.started[m] = True
-            lat.append(time.perf_counter() - ta)
-
-    decode_round.started = [False] * M
+    # ---------------- decode (microbatched ring, one HIP graph per microbatch) ----------------
+    prefill_round()
+    if ring is not None:
+        ring.capture()
     for _ in range(args.warmup):
-        decode_round()
+        if ring is not None:
+            ring.decode_round()
     t0 = sync()
     for _ in range(args.steps):
-        decode_round()
-    # drain the back-edge
-    if back_from is not None:
-        for m in range(M):
-            back_from.recv(nid[m])
+        if ring is not None:
+            ring.decode_round()
+    if ring is not None:
+        ring.drain()
     t1 = sync()
     decode_s = (t1 - t0) / args.steps
     dec_tok = B * M * replicas
-    # per-token latency of one decode step (single group only: a synced step)
-    tok_lat = []
-    if groups == 1 and stages:
+    # per-token latency of one synced decode round (single group only)
+    lat = []
+    if groups == 1 and ring is not None:
         for _ in range(16):
             ta = sync()
-            decode_round()
-            tok_lat.append(sync() - ta)
-    lat[:] = tok_lat
+            ring.decode_round()
+            lat.append(sync() - ta)
+    graphs = ring is not None and bool(ring.graphs)
 
     def mx(v):
         if N == 1:
@@ -277,6 +177,7 @@ def main(args=None):
         return float(t.item())
 
     prefill_s, decode_s = mx(prefill_s), mx(decode_s)
+    out = None
     if r == 0:
         value = dec_tok / decode_s
         out = {
@@ -294,10 +195,9 @@ def main(args=None):
                        "micro_batch": B, "microbatches": M, "prompt_len": T0, "seq_len": max_seq,
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},
         }
-        print(json.dumps(out), flush=True)
     if N > 1:
         comm.shutdown()
-    return 0
+    return out if r == 0 else None
 
 
 if __name__ == "__main__":

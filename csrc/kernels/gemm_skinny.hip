@@ -68,11 +68,15 @@ __device__ __forceinline__ void w8_to_bf16(const i32x4& w, bf16x8& lo, bf16x8& h
   __builtin_memcpy(&hi, &o[4], 16);
 }
 
-// Sum and sum of squares of the 8 bf16 of one A fragment.
-__device__ __forceinline__ void sk_stats(const i32x4& a, float& s1, float& s2) {
+// Shifted sum and sum of squares of the 8 bf16 of one A fragment: x - c with
+// c = the row's first element, so var = E[(x-c)^2] - E[x-c]^2 does not cancel
+// catastrophically when |mean| >> std (the unshifted E[x^2] - mean^2 loses
+// every bit of the variance once mean^2 / var ~ 2^24).
+__device__ __forceinline__ void sk_stats(const i32x4& a, float c, float& s1, float& s2) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float lo = __uint_as_float((uint32_t)a[i] << 16), hi = __uint_as_float((uint32_t)a[i] & 0xffff0000u);
+    const float lo = __uint_as_float((uint32_t)a[i] << 16) - c;
+    const float hi = __uint_as_float((uint32_t)a[i] & 0xffff0000u) - c;
     s1 += lo + hi;
     s2 = fmaf(lo, lo, fmaf(hi, hi, s2));
   }
@@ -150,9 +154,17 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float st1[MT], st2[MT];  // row statistics of this lane's A fragments (NORM)
+  float st1[MT], st2[MT], shift[MT];  // shifted row statistics of this lane's A fragments (NORM)
 #pragma unroll
-  for (int t = 0; t < MT; ++t) st1[t] = st2[t] = 0.f;
+  for (int t = 0; t < MT; ++t) {
+    st1[t] = st2[t] = 0.f;
+    shift[t] = 0.f;
+    if constexpr (NORM == NORM_LN) {  // RMS has no subtraction to protect: c = 0
+      int m = t * 16 + (lane & 15);
+      m = m < M ? m : M - 1;
+      shift[t] = __uint_as_float((uint32_t)(*reinterpret_cast<const uint16_t*>(A + (size_t)m * lda_b)) << 16);
+    }
+  }
 
   const int nch = kbytes >> 6;
   const int per = (nch + KS - 1) / KS;
@@ -190,7 +202,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
-          for (int h = 0; h < AU; ++h) sk_stats(av[t][u * AU + h], st1[t], st2[t]);
+          for (int h = 0; h < AU; ++h) sk_stats(av[t][u * AU + h], shift[t], st1[t], st2[t]);
       }
       if constexpr (W8) {
         // the lane's 16 weight bytes are k = 16g..16g+15 of the chunk; its two A
@@ -289,8 +301,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
         q += sk_st[((w * MT + t) * 2 + 1) * 16 + (lane & 15)];
       }
       const float invk = 1.f / (float)(W8 ? kbytes : kbytes >> 1);
-      const float mean = NORM == NORM_LN ? a * invk : 0.f;
-      const float var = fmaxf(q * invk - mean * mean, 0.f);
+      const float d = a * invk;  // E[x - c]
+      // LN: var = E[(x-c)^2] - E[x-c]^2, mean = c + E[x-c]; RMS (c = 0): E[x^2]
+      const float mean = NORM == NORM_LN ? shift[t] + d : 0.f;
+      const float var = NORM == NORM_LN ? fmaxf(q * invk - d * d, 0.f) : q * invk;
       const float rstd = rsqrtf(var + eps);
 #pragma unroll
       for (int j = 0; j < NT; ++j) {

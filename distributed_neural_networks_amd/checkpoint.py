@@ -150,11 +150,15 @@ def unexpected_keys(model: str, full_sd, start: int, end: int, first: bool, last
 
 
 def random_stage_state_dict(model: str, start: int, end: int, first: bool, last: bool,
-                            seed: int = 0, device=None) -> Dict[str, torch.Tensor]:
+                            seed: int = 0, device=None, nontrivial: bool = False) -> Dict[str, torch.Tensor]:
     """Random-init weights for one stage, identical to slicing a random full model
     generated with the same seed (layer-indexed seeding).  ``device`` generates
     directly on that device (billion-parameter stages without a host copy);
-    values then follow the device RNG, so compare only within one device."""
+    values then follow the device RNG, so compare only within one device.
+
+    The default follows nanoGPT's init (zero biases, unit norm gains).
+    ``nontrivial=True`` (tests) draws biases ~ N(0, 0.02^2) and norm gains
+    ~ 1 + N(0, 0.1^2) so folded-norm / bias epilogues are actually exercised."""
     info = model_info(model)
     if info.family == "cifar":
         return {k: v for k, v in cifar.random_state_dict(seed).items()
@@ -165,9 +169,11 @@ def random_stage_state_dict(model: str, start: int, end: int, first: bool, last:
     for local, shape in shapes.items():
         g = torch.Generator(device=dev).manual_seed(_key_seed(seed, _global_key(model, local, start)))
         if local.endswith("bias"):
-            sd[local] = torch.zeros(shape, device=dev)
+            sd[local] = (torch.randn(shape, generator=g, device=dev) * 0.02 if nontrivial
+                         else torch.zeros(shape, device=dev))
         elif "ln" in local.split(".")[-2] or local.endswith("norm.weight") or "layernorm" in local:
-            sd[local] = torch.ones(shape, device=dev)
+            sd[local] = (1.0 + 0.1 * torch.randn(shape, generator=g, device=dev) if nontrivial
+                         else torch.ones(shape, device=dev))
         else:
             sd[local] = torch.randn(shape, generator=g, device=dev) * 0.02
     if info.family == "gpt2" and last and first:

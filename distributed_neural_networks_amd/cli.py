@@ -49,6 +49,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--trace", default=None, help="write a Chrome trace (host + device spans) to this path")
     p.add_argument("--metrics", action="store_true", help="print one METRICS json line per stage at exit")
+    p.add_argument("--dump_result", default=None,
+                   help="stage 0 (grpc): save the final result tensor of the last request as .npy")
     return p
 
 
@@ -73,13 +75,30 @@ def load_image(path: Optional[str], nid: str) -> torch.Tensor:
 
 
 def make_prompt(ctx: NodeContext, prompt: Optional[str]) -> torch.Tensor:
+    from .runtime.generate import make_prompts
+    return make_prompts(ctx.pipeline, prompt)
+
+
+def kv_needs(ctx: NodeContext, args) -> Tuple[int, int]:
+    """(sequences, positions) the transformer KV caches are sized for, from the
+    config (``micro_batch_size`` x ``num_microbatches``; prompt + decode steps)."""
+    pipe = ctx.pipeline
+    T = pipe.prompt_len or pipe.seq_len
+    if getattr(args, "prompt", None):
+        T = len([v for v in args.prompt.split(",") if v.strip()])
+    return pipe.micro_batch_size * pipe.num_microbatches, T + max(1, pipe.decode_steps or 1)
+
+
+def check_config_capacity(ctx: NodeContext, args) -> None:
+    """Reject, before any weight is loaded, a run whose prompt + decode steps
+    overflow the model's position table / block size."""
     info = model_info(ctx.pipeline.model)
-    if prompt:
-        ids = [int(v) for v in prompt.split(",") if v.strip()]
-        return torch.tensor([ids], dtype=torch.int64)
-    g = torch.Generator().manual_seed(1234)
-    T = ctx.pipeline.prompt_len or ctx.pipeline.seq_len
-    return torch.randint(0, info.cfg.vocab_size, (ctx.pipeline.micro_batch_size, T), generator=g)
+    if info.family == "cifar":
+        return
+    _, n_pos = kv_needs(ctx, args)
+    limit = getattr(info.cfg, "block_size", None) or getattr(info.cfg, "max_seq", None)
+    if limit is not None and n_pos > limit:
+        raise ConfigError(f"ERROR: prompt + decode_steps = {n_pos} positions exceeds the model's limit {limit}")
 
 
 # --------------------------------------------------------------------------- stages
@@ -128,7 +147,7 @@ def load_stage_weights(ctx: NodeContext, part: int, ranges, full_sd=None, device
     return sd, full_sd
 
 
-def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_sd=None):
+def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_sd=None, args=None):
     from .runtime.stages import CifarHipStage, TorchStage
     pipe = ctx.pipeline
     a, b = ranges[part]
@@ -140,7 +159,9 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
             st = CifarHipStage(sd, a, b, device)
         else:
             from .runtime.transformer import build_device_stage
+            n_seq, n_pos = kv_needs(ctx, args) if args is not None else (8, 1024)
             st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
+                                    max_batch=n_seq, max_seq=n_pos,
                                     temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed)
     else:
         st = TorchStage(pipe.model, sd, a, b, first, last, device,
@@ -155,8 +176,6 @@ def _forward_fn(stage, fam: str):
 
     def fwd(x):
         x = x.to(stage.device)
-        if fam == "cifar" and not stage.first and stage.device.type == "cuda":
-            x = x.to(torch.bfloat16)
         y = stage.forward(x)
         if isinstance(y, StageOutput):
             if stage.device.type == "cuda":
@@ -255,6 +274,8 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
             resp = await client.send_tensor(req)
             log(f"[{nid}] Received final status from pipeline: {resp.status}")
             pred = decode_prediction(resp)
+            if pred is not None and args.dump_result:
+                np.save(args.dump_result, codec.decode_numpy(resp.result_tensor))
             if pred is None:
                 log(f"[{nid}] Final result status received, but tensor not included in response.")
                 rc = 1
@@ -268,35 +289,60 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
     return rc
 
 
+def cifar_request(args, nid: str, rows: int, tag: int) -> torch.Tensor:
+    """One CIFAR request of ``rows`` images: row 0 is ``--input_image`` (reference
+    transform, or the reference's random dummy), rows 1.. are seeded synthetic
+    images (``micro_batch_size`` x ``num_microbatches`` > 1 runs)."""
+    x = load_image(args.input_image, nid)
+    if rows > 1:
+        g = torch.Generator().manual_seed(1000 + tag)
+        x = torch.cat([x, torch.randn((rows - 1, 3, 32, 32), generator=g)])
+    return x
+
+
+def _fmt(preds) -> str:
+    p = preds.tolist() if hasattr(preds, "tolist") else list(preds)
+    return str(p[0] if len(p) == 1 else p)
+
+
 def run_colocated(ctx: NodeContext, args, device) -> int:
+    """All stages on one GPU in this process; every request of
+    ``micro_batch_size * num_microbatches`` rows runs microbatch by microbatch
+    through one captured HIP graph (CIFAR) or the decode ring (transformers)."""
     from .runtime.pipeline import ColocatedPipeline
     nid = ctx.node_id
+    pipe = ctx.pipeline
     if ctx.part_index != 0:
         log(f"[{nid}] colocated transport: all stages run in the part-0 process; nothing to do here.")
         return 0
     ranges = stage_ranges(ctx)
-    fam = model_info(ctx.pipeline.model).family
+    fam = model_info(pipe.model).family
     full = None
     stages = []
     for p in range(ctx.num_parts):
-        st, full = build_stage(ctx, p, ranges, device, full)
+        st, full = build_stage(ctx, p, ranges, device, full, args)
         stages.append(st)
     if fam != "cifar":
-        from .runtime.transformer import run_generate_colocated
+        from .runtime.generate import run_generate_colocated
         return run_generate_colocated(ctx, args, stages, device)
+    mbs, M = pipe.micro_batch_size, pipe.num_microbatches
+    cp = ColocatedPipeline(stages, mbs)
+    if device.type == "cuda":
+        cp.capture()
     for r in range(args.num_requests):
-        x = load_image(args.input_image, nid)
-        pipe = ColocatedPipeline(stages, x.shape[0])
-        out = pipe(x.to(device))
-        pred = out.pred.cpu().tolist()
-        log(f"[{nid}] ***** FINAL PREDICTION (Index): {pred[0] if len(pred) == 1 else pred} *****")
+        x = cifar_request(args, nid, mbs * M, r).to(device)
+        preds = []
+        for i in range(M):
+            preds.append(cp(x[i * mbs:(i + 1) * mbs]).pred.clone())
+        log(f"[{nid}] ***** FINAL PREDICTION (Index): {_fmt(torch.cat(preds).cpu())} *****")
     return 0
 
 
 def run_dist(ctx: NodeContext, args, device) -> int:
-    """One rank per stage over torch.distributed P2P (RCCL/gloo)."""
+    """One rank per stage over torch.distributed P2P (RCCL over xGMI / gloo),
+    microbatched (``runtime/scheduler.py``), with the failure watchdog."""
     from .parallel import comm
-    from .parallel.links import KIND_DATA, KIND_STOP, P2PLink
+    from .parallel.watchdog import Watchdog
     nid = ctx.node_id
     pipe = ctx.pipeline
     backend = "nccl" if pipe.transport == "rccl" else "gloo"
@@ -306,70 +352,66 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     if backend == "gloo":
         device = torch.device("cpu")
     s0 = pipe.stage(0)
-    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host, timeout_s=pipe.comm_timeout_s,
-                     master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
+    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host,
+                     timeout_s=pipe.comm_timeout_s, master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
     ranges = stage_ranges(ctx)
-    stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device)
+    stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device, None, args)
     fam = model_info(pipe.model).family
-    if fam != "cifar":
-        from .runtime.transformer import run_generate_dist
-        rc = run_generate_dist(ctx, args, stage, info)
-        comm.shutdown()
-        return rc
-    ret_rank = 0
-    if pipe.return_to_node_id and pipe.by_id(pipe.return_to_node_id):
-        ret_rank = pipe.by_id(pipe.return_to_node_id).part_index
-    prev = P2PLink(ctx.part_index - 1, info.device) if ctx.part_index > 0 else None
-    nxt = P2PLink(ctx.part_index + 1, info.device) if not ctx.is_last else None
-    back = P2PLink(ret_rank, info.device) if (ctx.is_last and ret_rank != ctx.part_index) else None
+    wd = Watchdog(info.rank, info.world, peer_timeout_s=pipe.heartbeat_timeout_s,
+                  stall_timeout_s=pipe.stall_timeout_s, tag=f"[{nid}]")
     comm.barrier(info)
+    wd.start()
     log(f"[{nid}] rank {info.rank}/{info.world} ready on {info.device} (backend {backend})")
     rc = 0
     try:
-        if ctx.part_index == 0:
-            for r in range(args.num_requests):
-                x = load_image(args.input_image, nid).to(info.device)
-                y = stage.forward(x)
-                if ctx.num_parts == 1:
-                    preds = y.pred.cpu().tolist()
-                else:
-                    nxt.send_header(KIND_DATA, x.shape[0], 0, r)
-                    nxt.send(y)
-                    if ret_rank == 0:
-                        rl = P2PLink(ctx.num_parts - 1, info.device)
-                        pr = torch.empty(x.shape[0], dtype=torch.int32, device=info.device)
-                        rl.recv(pr)
-                        preds = pr.cpu().tolist()
-                    else:
-                        preds = None
-                if preds is not None:
-                    log(f"[{nid}] ***** FINAL PREDICTION (Index): {preds[0] if len(preds) == 1 else preds} *****")
-            if nxt is not None:
-                nxt.send_header(KIND_STOP)
+        wd.busy(True)
+        if fam != "cifar":
+            from .runtime.generate import run_generate_dist
+            rc = run_generate_dist(ctx, args, stage, info, progress=wd.beat)
         else:
-            while True:
-                kind, batch, _, tag = prev.recv_header()
-                if kind == KIND_STOP:
-                    if nxt is not None:
-                        nxt.send_header(KIND_STOP)
-                    break
-                shp, dt = stage.in_spec(batch)
-                x = prev.recv(torch.empty(shp, dtype=dt, device=info.device))
-                y = stage.forward(x)
-                if nxt is not None:
-                    nxt.send_header(KIND_DATA, batch, 0, tag)
-                    nxt.send(y)
-                else:
-                    preds = y.pred.cpu().tolist()
-                    log(f"[{nid}] Final Prediction Index: {preds[0] if len(preds) == 1 else preds}")
-                    if back is not None:
-                        back.send(y.pred)
-    except Exception as e:  # noqa: BLE001
+            rc = _cifar_stream(ctx, args, stage, info, wd)
+        wd.busy(False)
+    except Exception as e:  # noqa: BLE001 — a failed rank takes the pipeline down
         log(f"!!! [{nid}] pipeline error: {e}")
         traceback.print_exc()
-        rc = 1
+        wd.abort(f"{type(e).__name__}: {e}")
+        return 1  # only reached when exit_fn does not exit (tests)
+    wd.done()
+    comm.barrier(info)
+    wd.stop()
     comm.shutdown()
     return rc
+
+
+def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
+    from .parallel.links import P2PLink
+    from .runtime.scheduler import ForwardLinks, ForwardPipeline
+    nid, pipe, dev = ctx.node_id, ctx.pipeline, info.device
+    r, S = ctx.part_index, ctx.num_parts
+    ret = pipe.by_id(pipe.return_to_node_id) if pipe.return_to_node_id else None
+    ret_rank = ret.part_index if ret is not None else 0
+    last = r == S - 1
+    links = ForwardLinks(prev=P2PLink(r - 1, dev) if r > 0 else None,
+                         nxt=P2PLink(r + 1, dev) if not last else None,
+                         ret_out=P2PLink(ret_rank, dev) if (last and ret_rank != r) else None,
+                         ret_in=P2PLink(S - 1, dev) if (r == ret_rank and not last) else None)
+
+    def on_result(role, tag, preds):
+        if role == "last":
+            log(f"[{nid}] Final Prediction Index: {_fmt(preds)}")
+        else:
+            log(f"[{nid}] ***** FINAL PREDICTION (Index): {_fmt(preds)} *****")
+
+    fp = ForwardPipeline(stage, links, r == 0, last, r == ret_rank, depth=2, progress=wd.beat, on_result=on_result)
+    mbs, M = pipe.micro_batch_size, pipe.num_microbatches
+    if r == 0:
+        for req in range(args.num_requests):
+            x = cifar_request(args, nid, mbs * M, req).to(dev)
+            fp.run_request(x, mbs, M, tag=req)
+        fp.stop()
+    else:
+        fp.serve()
+    return 0
 
 
 def _finish(args) -> None:
@@ -394,6 +436,7 @@ def main(argv=None) -> int:
     try:
         ctx = load_node(args.config, nid)
         log(f"Loaded configuration from {args.config}")
+        check_config_capacity(ctx, args)
     except ConfigError as e:
         print(str(e), flush=True)
         return 1
@@ -406,7 +449,7 @@ def main(argv=None) -> int:
         if transport in ("rccl", "gloo"):
             return run_dist(ctx, args, device)
         ranges = stage_ranges(ctx)
-        stage, _ = build_stage(ctx, ctx.part_index, ranges, device)
+        stage, _ = build_stage(ctx, ctx.part_index, ranges, device, None, args)
     except FileNotFoundError:
         log(f"[{nid}] ERROR: Weights file not found at '{ctx.model_weights}'")
         return 1

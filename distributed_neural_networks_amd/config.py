@@ -12,7 +12,7 @@ Behavioural contract (reference ``node.py:222-290``, ``config.json:1-18``):
 * Additive optional fields (absent in the reference file, so it still loads):
   top level ``model``, ``dtype``, ``transport``, ``micro_batch_size``,
   ``num_microbatches``, ``seq_len``, ``decode_steps``, ``prompt_len``, ``temperature``, ``top_k``,
-  ``seed``; per node
+  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``; per node
   ``layers: [start, end]`` (inclusive, as in
   ``partitions/gpt_model_parts.py:12``) and ``device``.
 
@@ -71,7 +71,9 @@ class PipelineConfig:
     seed: int = 0                             # sampling seed (counter-based RNG, reproducible)
     rpc_timeout_s: Optional[float] = None     # per-hop SendTensor deadline (reference: none)
     health_timeout_s: float = 120.0           # readiness barrier before stage 0 sends
-    comm_timeout_s: float = 300.0             # process-group (RCCL/gloo) watchdog timeout
+    comm_timeout_s: float = 300.0             # process-group (RCCL/gloo) op timeout
+    heartbeat_timeout_s: float = 15.0         # parallel/watchdog.py: peer declared dead after this
+    stall_timeout_s: Optional[float] = None   # parallel/watchdog.py: abort when this rank stops progressing
     raw: Dict[str, Any] = field(default_factory=dict)
 
     def stage(self, part_index: int) -> NodeSpec:
@@ -159,6 +161,15 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     model = cfg.get("model", "cifar10")
     if model not in MODELS:
         raise ConfigError(f"ERROR: unknown model '{model}', expected one of {MODELS}")
+    for key in ("micro_batch_size", "num_microbatches"):
+        v = cfg.get(key, 1)
+        if not isinstance(v, int) or v < 1:
+            raise ConfigError(f"ERROR: '{key}' must be a positive integer, got {v!r}")
+    ret = cfg.get("return_to_node_id")
+    if ret is not None and transport in ("rccl", "gloo"):
+        rn = next((n for n in nodes if n.id == ret), None)
+        if rn is None:
+            raise ConfigError(f"ERROR: return_to_node_id '{ret}' is not a node of this config")
     return PipelineConfig(
         nodes=nodes, model_weights=str(weights), num_parts=num_parts,
         return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"),
@@ -167,7 +178,9 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),
         temperature=float(cfg.get("temperature", 0.0)), top_k=int(cfg.get("top_k", 0)), seed=int(cfg.get("seed", 0)),
         rpc_timeout_s=cfg.get("rpc_timeout_s"), health_timeout_s=float(cfg.get("health_timeout_s", 120.0)),
-        comm_timeout_s=float(cfg.get("comm_timeout_s", 300.0)), raw=cfg)
+        comm_timeout_s=float(cfg.get("comm_timeout_s", 300.0)),
+        heartbeat_timeout_s=float(cfg.get("heartbeat_timeout_s", 15.0)),
+        stall_timeout_s=(None if cfg.get("stall_timeout_s") is None else float(cfg["stall_timeout_s"])), raw=cfg)
 
 
 def resolve_node(cfg: Dict[str, Any], node_id: str, path: str = "<config>") -> NodeContext:

@@ -191,5 +191,7 @@ def decode_prediction(resp) -> Optional[np.ndarray]:
     if not resp.HasField("result_tensor"):
         return None
     out = codec.decode_numpy(resp.result_tensor)
+    if out.ndim == 3:  # transformer logits (B, T, V): the next token of every sequence
+        return out[:, -1, :].argmax(axis=-1)
     out = out.reshape(out.shape[0], -1) if out.ndim > 1 else out.reshape(1, -1)
     return out.argmax(axis=-1)

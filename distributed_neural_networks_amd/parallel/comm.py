@@ -64,6 +64,10 @@ def init(backend: Optional[str] = None, rank: Optional[int] = None, world: Optio
         device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
+    if backend == "nccl":
+        # a failed/timed-out RCCL op tears the communicator down instead of hanging
+        # (second line of defence behind parallel/watchdog.py)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", master_addr or "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(master_port or 29500))

@@ -1,0 +1,471 @@
+"""Microbatch schedules for one pipeline rank (forward-only inference).
+
+The reference keeps exactly one request in flight: stage i's handler blocks on
+the nested RPC to stage i+1 for the whole downstream latency (``node.py:70-94``)
+and the driver sends one hard-coded request (``node.py:173``), so with S stages
+S-1 devices idle.  This module holds the schedules that keep every stage busy;
+the CLI (``node.py``), ``bench.py`` and ``bench/gpt_bench.py`` all run them:
+
+* ``run_gpipe`` — forward-only GPipe fill/drain of M microbatches through this
+  rank's stage (CIFAR, prefill-style work).  Receives land in a ``depth``-deep
+  slot ring and are posted ``depth`` microbatches ahead; the send of microbatch
+  i overlaps the compute of i+1.  Slot reuse is ordered by the P2P work handles.
+* ``ForwardPipeline`` — the open-ended request stream of the CLI on top of
+  ``run_gpipe``: stage 0 splits each request into ``num_microbatches``
+  microbatches of ``micro_batch_size`` rows, a 4-int64 header announces the
+  shape to the downstream ranks, and the last stage returns per-row
+  predictions over the back-edge to ``return_to_node_id`` (resolved but unused
+  in the reference, ``node.py:272-277``).
+* ``DecodeRing`` — autoregressive decode with M microbatches circulating
+  stage group 0 -> ... -> last -> (sampled token ids over the back-edge) ->
+  stage group 0.  With M >= #groups every rank works on a different microbatch
+  at any time.  On a GPU each microbatch's decode compute for this rank is one
+  HIP graph; the P2P hops stay outside the graph.
+
+Ordering rules (``Link`` = ``parallel/links.py``): an ``isend``'s source buffer
+may be overwritten only after the send's work was waited on (on RCCL that makes
+the compute stream wait on the transfer, no host block); a receive may target a
+buffer the previous microbatch's compute still reads, because RCCL enqueues the
+receive behind the work already queued on the compute stream (gloo runs
+compute synchronously).  ``DNN_DEBUG_ORDER=1`` checks the slot protocol
+(``runtime/ordering.py``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+
+from ..parallel.links import exchange
+from ..utils import trace
+from .ordering import SlotOrder
+from .stages import StageCompute, StageOutput
+
+Progress = Optional[Callable[[], None]]
+
+
+def _noop():
+    return None
+
+
+# --------------------------------------------------------------------------- stage chains
+class StageChain(StageCompute):
+    """Several consecutive stages hosted by one rank (or one GPU), chained over
+    preallocated intermediate buffers: to the schedule they are one stage."""
+
+    def __init__(self, stages: Sequence[StageCompute]):
+        self.stages = list(stages)
+        self.first, self.last = self.stages[0].first, self.stages[-1].last
+        self.device = self.stages[0].device
+        self._mid: Dict[int, List[torch.Tensor]] = {}
+
+    def in_spec(self, batch):
+        return self.stages[0].in_spec(batch)
+
+    def out_spec(self, batch):
+        return self.stages[-1].out_spec(batch)
+
+    def forward(self, x, out=None):
+        B = x.shape[0]
+        mids = self._mid.get(B)
+        if mids is None:
+            mids = []
+            for s in self.stages[:-1]:
+                shp, dt = s.out_spec(B)
+                mids.append(torch.empty(shp, dtype=dt, device=self.device))
+            self._mid[B] = mids
+        h = x
+        for s, buf in zip(self.stages[:-1], mids):
+            h = s.forward(h, buf)
+        return self.stages[-1].forward(h, out)
+
+
+def as_stage(stages) -> StageCompute:
+    if isinstance(stages, StageCompute) or hasattr(stages, "forward"):
+        return stages
+    stages = list(stages)
+    return stages[0] if len(stages) == 1 else StageChain(stages)
+
+
+# --------------------------------------------------------------------------- GPipe forward stream
+def run_gpipe(stage, M: int, batch: int, prev=None, nxt=None,
+              source: Optional[Callable[[int], torch.Tensor]] = None,
+              sink: Optional[Callable[[int, object], None]] = None, depth: int = 2,
+              progress: Progress = None) -> None:
+    """Stream M microbatches of ``batch`` rows through this rank's stage(s).
+
+    ``prev``/``nxt`` are links to the neighbouring ranks (None at the ends);
+    the first rank pulls inputs from ``source(i)``, every rank may observe its
+    outputs with ``sink(i, y)`` (the last rank gets ``StageOutput``)."""
+    stage = as_stage(stage)
+    progress = progress or _noop
+    dev = stage.device
+    ishp, idt = stage.in_spec(batch)
+    oshp, odt = stage.out_spec(batch)
+    depth = max(1, min(depth, M))
+    in_slots = [torch.empty(ishp, dtype=idt, device=dev) for _ in range(depth)] if prev is not None else []
+    out_slots = [torch.empty(oshp, dtype=odt, device=dev) for _ in range(depth)]
+    rwork: List[object] = [None] * depth
+    swork: List[object] = [None] * depth
+    ins, outs = SlotOrder("in_slots", depth), SlotOrder("out_slots", depth)
+    if prev is not None:
+        for k in range(depth):
+            rwork[k] = prev.irecv(in_slots[k])
+            ins.post(k, "recv", k)
+    for i in range(M):
+        k = i % depth
+        if prev is None:
+            x = source(i)
+        else:
+            with trace.span("recv_wait", "p2p", mb=i):
+                rwork[k].wait()
+            ins.waited(k)
+            ins.use(k, "stage input read", i)
+            x = in_slots[k]
+        if swork[k] is not None:
+            with trace.span("slot_reuse_wait", "p2p", mb=i):
+                swork[k].wait()
+            swork[k] = None
+            outs.waited(k)
+        outs.use(k, "stage output write", i)
+        with trace.span("stage_forward", "compute", device=dev, mb=i):
+            y = stage.forward(x, out_slots[k])
+        post_recv = prev is not None and i + depth < M
+        send_t = (y if isinstance(y, torch.Tensor) else y.probs) if nxt is not None else None
+        if post_recv and send_t is not None:
+            # middle stage: send(i) -> next and recv(i+depth) <- prev as one group
+            w = exchange([(nxt, send_t)], [(prev, in_slots[k])])
+            rwork[k] = swork[k] = w
+        elif post_recv:
+            rwork[k] = prev.irecv(in_slots[k])  # queued behind this slot's compute
+        elif send_t is not None:
+            swork[k] = nxt.isend(send_t)
+        if post_recv:
+            ins.post(k, "recv", i + depth)
+        if send_t is not None:
+            outs.post(k, "send", i)
+        if sink is not None:
+            sink(i, y)
+        progress()
+    for k, w in enumerate(swork):
+        if w is not None:
+            w.wait()
+            outs.waited(k)
+    ins.drained()
+    outs.drained()
+
+
+# backwards-compatible name (round-1 API)
+run_stage_stream = run_gpipe
+
+
+# --------------------------------------------------------------------------- CLI forward stream
+KIND_DATA, KIND_STOP = 1, 2
+
+
+@dataclass
+class ForwardLinks:
+    prev: object = None          # link to part_index - 1
+    nxt: object = None           # link to part_index + 1
+    ret_out: object = None       # last stage -> return rank (back-edge), None if last == return rank
+    ret_in: object = None        # return rank <- last stage
+
+
+class ForwardPipeline:
+    """Request stream of the CLI over ``run_gpipe`` (CIFAR-style stages).
+
+    Each request of ``mbs * M`` rows is announced by a header
+    ``[KIND_DATA, mbs, M, tag]`` and streamed as M microbatches; ``stop()``
+    sends ``KIND_STOP`` down the chain.  The last stage sends each microbatch's
+    per-row predictions (int32) to the return rank over the back-edge.
+    ``on_result(role, tag, preds)`` is called with role ``"last"`` on the last
+    stage and ``"return"`` on the return rank (host int32 predictions).
+    """
+
+    def __init__(self, stage, links: ForwardLinks, is_first: bool, is_last: bool, is_ret: bool,
+                 depth: int = 2, progress: Progress = None, on_result: Optional[Callable] = None):
+        self.stage = as_stage(stage)
+        self.links = links
+        self.is_first, self.is_last, self.is_ret = is_first, is_last, is_ret
+        self.depth = depth
+        self.progress = progress or _noop
+        self.on_result = on_result or (lambda role, tag, preds: None)
+        self._slots: Dict[int, List[torch.Tensor]] = {}
+
+    def _send_header(self, kind, a=0, b=0, tag=0):
+        if self.links.nxt is not None:
+            self.links.nxt.send_header(kind, a, b, tag)
+
+    def _stream(self, mbs: int, M: int, tag: int, source=None) -> Optional[torch.Tensor]:
+        """This rank's part of one request; returns the last stage's predictions."""
+        local: Dict[int, torch.Tensor] = {}
+        work: List[object] = [None, None]
+        sink = None
+        if self.is_last:
+            slots = self._slots.get(mbs)
+            if slots is None:
+                slots = self._slots[mbs] = [torch.empty((mbs,), dtype=torch.int32, device=self.stage.device)
+                                            for _ in range(2)]
+
+            def sink(i, y: StageOutput):
+                local[i] = y.pred.clone()
+                if self.links.ret_out is not None:
+                    k = i % 2
+                    if work[k] is not None:
+                        work[k].wait()
+                    slots[k].copy_(y.pred)
+                    work[k] = self.links.ret_out.isend(slots[k])
+        run_gpipe(self.stage, M, mbs, self.links.prev, self.links.nxt, source=source, sink=sink,
+                  depth=self.depth, progress=self.progress)
+        for w in work:
+            if w is not None:
+                w.wait()
+        if not self.is_last:
+            return None
+        preds = torch.cat([local[i] for i in range(M)]).cpu()
+        self.on_result("last", tag, preds)
+        return preds
+
+    def _collect(self, mbs: int, M: int) -> torch.Tensor:
+        dev = self.stage.device
+        preds = [torch.empty((mbs,), dtype=torch.int32, device=dev) for _ in range(M)]
+        for p in preds:
+            self.links.ret_in.recv(p)
+            self.progress()
+        return torch.cat(preds).cpu()
+
+    def _request(self, mbs: int, M: int, tag: int, source=None) -> Optional[torch.Tensor]:
+        own = self._stream(mbs, M, tag, source)
+        if not self.is_ret:
+            return None
+        preds = own if self.links.ret_in is None else self._collect(mbs, M)
+        self.on_result("return", tag, preds)
+        return preds
+
+    def run_request(self, x: torch.Tensor, mbs: int, M: int, tag: int = 0) -> Optional[torch.Tensor]:
+        """Stage 0: stream one request (``x`` has ``mbs * M`` rows, on the
+        stage's device).  Returns the per-row predictions when this rank is
+        the return rank."""
+        if not self.is_first or x.shape[0] != mbs * M:
+            raise ValueError(f"run_request: stage 0 needs mbs*M = {mbs * M} rows, got {tuple(x.shape)}")
+        self._send_header(KIND_DATA, mbs, M, tag)
+        return self._request(mbs, M, tag, source=lambda i: x[i * mbs:(i + 1) * mbs])
+
+    def serve(self) -> int:
+        """Ranks > 0: process requests until ``KIND_STOP``; returns the count."""
+        n = 0
+        while True:
+            kind, mbs, M, tag = self.links.prev.recv_header()
+            self.progress()
+            if kind == KIND_STOP:
+                self._send_header(KIND_STOP)
+                return n
+            self._send_header(KIND_DATA, mbs, M, tag)
+            self._request(mbs, M, tag)
+            n += 1
+
+    def stop(self):
+        self._send_header(KIND_STOP)
+
+
+# --------------------------------------------------------------------------- decode ring
+@dataclass
+class RingLinks:
+    prev: object = None       # hidden states from the previous group
+    nxt: object = None        # hidden states to the next group
+    back_out: object = None   # last group: sampled ids -> group 0
+    back_in: object = None    # group 0: sampled ids <- last group
+
+
+def _act_dtype(st) -> torch.dtype:
+    return getattr(st, "act_dtype", torch.bfloat16)
+
+
+class DecodeRing:
+    """Microbatched autoregressive decode over a pipeline of stage groups.
+
+    ``stages``: this rank's consecutive transformer stages (``step`` API of
+    ``runtime/transformer.py`` / ``TorchStage``).  ``n_groups`` ranks form the
+    ring; microbatch m owns KV-cache rows ``[m*B, (m+1)*B)`` on every stage.
+    Group 0 holds the token state; it receives every sampled token over the
+    back-edge (or, with one group, the graph writes it in place).
+    """
+
+    def __init__(self, stages: Sequence, links: RingLinks, n_groups: int, M: int, B: int,
+                 use_graphs: bool = True, record: bool = True, progress: Progress = None):
+        self.stages = list(stages)
+        self.links = links
+        self.G, self.M, self.B = n_groups, M, B
+        self.first, self.last = self.stages[0].first, self.stages[-1].last
+        self.dev = self.stages[0].device
+        self.progress = progress or _noop
+        self.record = record
+        st0 = self.stages[0]
+        self.d = st0.d if hasattr(st0, "d") else st0.cfg.n_embd
+        for s in self.stages:
+            mb = getattr(s, "max_batch", None)
+            if mb is not None and mb < M * B:
+                raise ValueError(f"stage KV cache holds {mb} sequences, the ring needs M*B = {M * B}")
+        dev = self.dev
+        self.pos = [torch.zeros((B,), dtype=torch.int32, device=dev) for _ in range(M)]
+        self.cur = [torch.zeros((B, 1), dtype=torch.int32, device=dev) for _ in range(M)] if self.first else None
+        in_dt = _act_dtype(self.stages[0])
+        out_dt = _act_dtype(self.stages[-1])
+        self.xin = torch.empty((B, self.d), dtype=in_dt, device=dev) if not self.first else None
+        if self.last:
+            self.out = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(M)]
+        else:
+            self.out = [torch.empty((B, self.d), dtype=out_dt, device=dev) for _ in range(M)]
+        self.swork: List[object] = [None] * M
+        self.sorder = SlotOrder("ring_out", M)
+        self.toks: List[List[torch.Tensor]] = [[] for _ in range(M)]
+        self.use_graphs = use_graphs and dev.type == "cuda"
+        self.graphs: Dict[int, object] = {}
+        self.steps_done = 0
+
+    # -- one microbatch through this rank's stages --------------------------
+    def _run(self, x, m: int, T: int, out=None):
+        h = x
+        n = len(self.stages)
+        for j, s in enumerate(self.stages):
+            h = s.step(h, self.pos[m], self.B, T, b0=m * self.B, out=out if j == n - 1 else None)
+        return h
+
+    def _decode_body(self, m: int):
+        x = self.cur[m] if self.first else self.xin
+        y = self._run(x, m, 1, out=self.out[m])
+        self.pos[m].add_(1)
+        if self.last and self.G == 1:
+            self.cur[m].copy_(self.out[m].view(self.B, 1))
+        return None
+
+    def _out_ready(self, m: int):
+        if self.swork[m] is not None:
+            self.swork[m].wait()
+            self.swork[m] = None
+            self.sorder.waited(m)
+        self.sorder.use(m, "ring output write", m)
+
+    def _send(self, m: int):
+        if self.last:
+            if self.G > 1:
+                self.swork[m] = self.links.back_out.isend(self.out[m])
+                self.sorder.post(m, "send", m)
+        else:
+            self.swork[m] = self.links.nxt.isend(self.out[m])
+            self.sorder.post(m, "send", m)
+
+    def _recv_token(self, m: int):
+        """Group 0: the token sampled for microbatch m arrives over the back-edge."""
+        if self.G > 1:
+            with trace.span("token_recv", "p2p", mb=m):
+                self.links.back_in.recv(self.cur[m].view(self.B))
+        if self.record:
+            self.toks[m].append(self.cur[m].view(self.B).clone())
+
+    # -- prefill ----------------------------------------------------------------
+    def prefill(self, prompts: Optional[Sequence[torch.Tensor]], T: int) -> None:
+        """Run the T-token prompts of all M microbatches (group 0 passes
+        ``prompts[m]`` (B, T) int; other groups pass None)."""
+        B, d = self.B, self.d
+        for m in range(self.M):
+            self.pos[m].zero_()
+            self.toks[m] = []
+        xin_pf = torch.empty((B * T, d), dtype=_act_dtype(self.stages[0]), device=self.dev) if not self.first else None
+        out_pf = None
+        pf_work: List[object] = [None, None]
+        if not self.last:
+            out_pf = [torch.empty((B * T, d), dtype=_act_dtype(self.stages[-1]), device=self.dev) for _ in range(2)]
+        for m in range(self.M):
+            if self.first:
+                x = prompts[m].to(device=self.dev, dtype=torch.int32).contiguous()
+            else:
+                self.links.prev.recv(xin_pf)
+                x = xin_pf
+            k = m % 2
+            if not self.last and pf_work[k] is not None:
+                pf_work[k].wait()
+            self._out_ready(m)
+            with trace.span("prefill", "compute", mb=m):
+                y = self._run(x, m, T, out=(self.out[m] if self.last else out_pf[k]))
+            self.pos[m].add_(T)
+            if self.last:
+                if self.G == 1:
+                    self.cur[m].copy_(self.out[m].view(B, 1))
+                    if self.record:
+                        self.toks[m].append(self.out[m].clone())
+                else:
+                    self._send(m)
+            else:
+                pf_work[k] = self.links.nxt.isend(out_pf[k])
+            self.progress()
+        for w in pf_work:
+            if w is not None:
+                w.wait()
+        self.steps_done = 0
+
+    # -- decode -------------------------------------------------------------------
+    def capture(self) -> None:
+        """One HIP graph per microbatch for this rank's decode compute."""
+        if not self.use_graphs or self.graphs:
+            return
+        from .graph import GraphedStep
+        for m in range(self.M):
+            snap = self.pos[m].clone()
+            cur = self.cur[m].clone() if self.first else None
+            self._out_ready(m)
+            self.graphs[m] = GraphedStep(lambda m=m: self._decode_body(m), self.dev, warmup=1)
+            self.pos[m].copy_(snap)  # the warmup/capture runs advanced the position
+            if cur is not None:
+                self.cur[m].copy_(cur)
+        torch.cuda.synchronize(self.dev)
+
+    def decode_round(self) -> None:
+        """Every microbatch advances one token on this rank's stages."""
+        G = self.G
+        for m in range(self.M):
+            if self.first and G > 1:
+                self._recv_token(m)
+            elif not self.first:
+                with trace.span("hidden_recv", "p2p", mb=m):
+                    self.links.prev.recv(self.xin)
+            self._out_ready(m)
+            with trace.span("decode", "compute", mb=m, step=self.steps_done):
+                if m in self.graphs:
+                    self.graphs[m]()
+                else:
+                    self._decode_body(m)
+            self._send(m)
+            if self.first and G == 1 and self.record:
+                self.toks[m].append(self.cur[m].view(self.B).clone())
+            self.progress()
+        self.steps_done += 1
+
+    def drain(self) -> None:
+        """End of generation: group 0 receives the last sampled tokens; every
+        rank waits for its outstanding sends."""
+        if self.first and self.G > 1:
+            for m in range(self.M):
+                self._recv_token(m)
+                self.progress()
+        for m in range(self.M):
+            if self.swork[m] is not None:
+                self.swork[m].wait()
+                self.swork[m] = None
+                self.sorder.waited(m)
+        self.sorder.drained()
+
+    def generate(self, prompts, T: int, steps: int) -> Optional[torch.Tensor]:
+        """Prefill + ``steps - 1`` decode rounds (``steps`` tokens per sequence).
+        Group 0 returns (M*B, steps) int32 on the host; other groups None."""
+        self.prefill(prompts, T)
+        if steps > 1:
+            self.capture()
+        for _ in range(steps - 1):
+            self.decode_round()
+        self.drain()
+        return self.tokens() if self.first else None
+
+    def tokens(self) -> torch.Tensor:
+        return torch.cat([torch.stack(t, 1) for t in self.toks], 0).cpu()

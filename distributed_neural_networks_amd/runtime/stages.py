@@ -173,26 +173,40 @@ class TorchStage(StageCompute):
     def step(self, x, pos, B: int, T: int, b0: int = 0, out=None, last_only: bool = True):
         """KV-cached transformer step (CPU golden path; same contract as
         ``TransformerStage.step``): x = ids (B,T) on the first stage, else
-        hidden (B*T, d); ``pos`` = tokens already cached (uniform per batch)."""
+        hidden (B*T, d); ``pos`` = tokens already cached (uniform per batch);
+        rows ``[b0, b0+B)`` of the cache (one KV cache per microbatch offset)."""
         cfg = model_info(self.model).cfg
         p = int(pos[0]) if isinstance(pos, torch.Tensor) else int(pos)
-        if getattr(self, "_kv", None) is None or self._kv[0][0].shape[0] != B:
+        caches = getattr(self, "_kv", None)
+        if caches is None:
+            caches = self._kv = {}
+        kv = caches.get(b0)
+        if kv is None or kv[0][0].shape[0] != B:
             S = getattr(cfg, "block_size", getattr(cfg, "max_seq", 1024))
             hkv = getattr(cfg, "n_kv_head", cfg.n_head)
             hd = cfg.n_embd // cfg.n_head
-            self._kv = [(torch.zeros(B, hkv, S, hd, dtype=self.dtype), torch.zeros(B, hkv, S, hd, dtype=self.dtype))
-                        for _ in range(len(self.module.h if self.family == "gpt2" else self.module.layers))]
+            n = len(self.module.h if self.family == "gpt2" else self.module.layers)
+            kv = caches[b0] = [(torch.zeros(B, hkv, S, hd, dtype=self.dtype), torch.zeros(B, hkv, S, hd, dtype=self.dtype))
+                               for _ in range(n)]
         if self.first:
             h = x.to(torch.int64).view(B, T)
         else:
             h = x.view(B, T, cfg.n_embd).to(self.dtype)
-        y = self.module(h, self._kv, p, last_only=last_only)
+        y = self.module(h, kv, p, last_only=last_only)
         if self.last:
             from .sampling import pick
             logits = y[:, -1, :] if last_only else y.reshape(B * T, -1)
             step = pos if isinstance(pos, torch.Tensor) else torch.full((B,), p, dtype=torch.int32)
-            return StageOutput(logits, pick(y[:, -1, :], self.temperature, self.top_k, self.seed, step))
-        return y.reshape(B * T, cfg.n_embd)
+            pred = pick(y[:, -1, :], self.temperature, self.top_k, self.seed, step).to(torch.int32)
+            if out is not None and last_only:
+                out.copy_(pred)
+                pred = out
+            return StageOutput(logits, pred)
+        y = y.reshape(B * T, cfg.n_embd)
+        if out is not None:
+            out.view(B * T, cfg.n_embd).copy_(y)
+            return out
+        return y
 
     @torch.no_grad()
     def forward(self, x, out=None):

@@ -18,7 +18,8 @@ import threading
 import time
 from typing import List, Optional
 
-_state = {"on": False, "path": None, "events": [], "dev": [], "t0": time.perf_counter(), "pid": os.getpid()}
+_state = {"on": False, "path": None, "events": [], "dev": [], "t0": time.perf_counter(), "epoch0": time.time(),
+          "pid": os.getpid()}
 _lock = threading.Lock()
 _roctx = None
 
@@ -108,8 +109,11 @@ def flush(path: Optional[str] = None) -> Optional[str]:
             events.append({"name": name, "cat": cat + ".gpu", "ph": "X", "pid": _state["pid"], "tid": "gpu",
                            "ts": (base[1] - _state["t0"]) * 1e6 + off_ms * 1e3, "dur": e0.elapsed_time(e1) * 1e3,
                            "args": args})
+    # epoch of ts = 0, so traces of several ranks (one file each) can be merged
+    # onto one timeline: wall_us = epoch_t0_us + ts
+    meta = {"epoch_t0_us": _state["epoch0"] * 1e6, "pid": _state["pid"]}
     with open(path, "w") as f:
-        json.dump({"traceEvents": events, "displayTimeUnit": "ms"}, f)
+        json.dump({"traceEvents": events, "displayTimeUnit": "ms", "otherData": meta}, f)
     return path
 
 
@@ -118,3 +122,4 @@ def reset() -> None:
         _state["events"].clear()
         _state["dev"].clear()
         _state["t0"] = time.perf_counter()
+        _state["epoch0"] = time.time()

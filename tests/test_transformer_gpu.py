@@ -568,3 +568,110 @@ def test_stage_decode_with_and_without_shuffled_weights(monkeypatch):
         o = st.step(ids[:, -1:].contiguous(), pos, 4, 1)
         outs.append(o.probs.float().clone())
     assert _rel(outs[1], outs[0]) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 16, 64, 100])
+@pytest.mark.parametrize("w8", [False, True])
+def test_linear_norm_large_mean(M, w8):
+    """LayerNorm folded into the GEMM on rows with |mean| / std >= 50: the fused
+    decode statistics are shifted (gemm_skinny.hip sk_stats), so they agree with
+    the two-pass fp32 reference (the one-pass E[x^2] - mean^2 lost the variance)."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8
+    from distributed_neural_networks_amd.ops.gemm import fold_norm, linear_norm
+    if w8 and M > 64:
+        pytest.skip("W8 fused norm is the decode (M <= 64) path")
+    torch.manual_seed(9)
+    K, N = 768, 1024
+    x = (64.0 + torch.randn(M, K, device=DEV)).bfloat16()  # mean 64, std ~1 (ratio 64)
+    xf = x.float()
+    assert (xf.mean(1).abs() / xf.std(1)).min().item() >= 50
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = torch.randn(K, device=DEV) * 0.1
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = torch.randn(N, device=DEV) * 0.1
+    ref = F.layer_norm(xf, (K,), gamma, beta, 1e-5) @ W.t() + bias
+    f = fold_norm(W, gamma, beta, bias, False, 1e-5, DEV, fp8=w8)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    if w8:
+        linear_w8(x, f.w, f.bias, 0, None, out, f.norm, f.colsum, f.eps)
+        tol = 6e-2
+    else:
+        linear_norm(x, f, out=out, std_buf=torch.empty(M, K, device=DEV, dtype=torch.bfloat16),
+                    ones=torch.ones(K, device=DEV))
+        tol = 1.5e-2
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < tol, _rel(out, ref)
+
+
+def test_transformer_forward_full_prefix():
+    """TransformerStage.forward (the gRPC data path: full-prefix request, hidden
+    states between stages, all-position logits on the last) vs the golden."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import build_golden_stage
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "gpt2-tiny"
+    ranges = [(0, 1), (2, 3)]
+    sds = [ckpt.random_stage_state_dict(model, a, b, i == 0, i == 1, 4, nontrivial=True)
+           for i, (a, b) in enumerate(ranges)]
+    st = [TransformerStage(model, sds[i], a, b, i == 0, i == 1, DEV, max_batch=3, max_seq=48)
+          for i, (a, b) in enumerate(ranges)]
+    ids = torch.randint(0, 512, (3, 21))
+    h = st[0].forward(ids)
+    assert h.shape == (3, 21, 256) and h.dtype == torch.bfloat16
+    out = st[1].forward(h.float())  # the wire carries fp32
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = ids
+        for i, (a, b) in enumerate(ranges):
+            g = build_golden_stage(model, a, b, i == 0, i == 1)
+            g.load_state_dict(sds[i])
+            ref = g.eval()(ref)
+    assert out.probs.shape == (3, 21, 512)
+    assert _rel(out.probs.cpu(), ref) < 2e-2
+    assert torch.equal(out.pred.cpu().long(), out.probs[:, -1].argmax(-1).cpu())
+    with pytest.raises(ValueError):
+        st[0].forward(torch.randint(0, 512, (4, 8)))  # more sequences than the KV cache holds
+
+
+def test_gpt2_small_4stage_vs_golden():
+    """Full-width GPT-2 small (d 768, 12 layers) as 4 device stages with
+    non-trivial gains / biases: prefill logits, then 8 KV-cached decode steps
+    (the device's own tokens fed to both sides), each within 2e-2 relative of
+    the fp32 torch golden."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import build_golden_stage, default_ranges
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "gpt2"
+    ranges = default_ranges(model, 4)
+    B, T, steps = 2, 32, 8
+    sds = [ckpt.random_stage_state_dict(model, a, b, i == 0, i == 3, 21, nontrivial=True)
+           for i, (a, b) in enumerate(ranges)]
+    st = [TransformerStage(model, sds[i], a, b, i == 0, i == 3, DEV, max_batch=B, max_seq=T + steps + 1)
+          for i, (a, b) in enumerate(ranges)]
+    gold = []
+    for i, (a, b) in enumerate(ranges):
+        g = build_golden_stage(model, a, b, i == 0, i == 3)
+        g.load_state_dict(sds[i])
+        gold.append(g.eval())
+    del sds
+    hd = 64
+    kvs = [[(torch.zeros(B, 12, T + steps + 1, hd), torch.zeros(B, 12, T + steps + 1, hd)) for _ in g.h]
+           for g in gold]
+    ids = torch.randint(0, 50257, (B, T), generator=torch.Generator().manual_seed(2))
+    pos = torch.zeros(B, dtype=torch.int32, device=DEV)
+    x, Tn, p = ids, T, 0
+    for step in range(steps + 1):
+        h = x.to(DEV, torch.int32)
+        for s in st:
+            h = s.step(h, pos, B, Tn)
+        pos.add_(Tn)
+        with torch.no_grad():
+            r = x
+            for g, kv in zip(gold, kvs):
+                r = g(r, kv, p, last_only=True)
+        dev_logits = h.probs.float().cpu()
+        rel = _rel(dev_logits, r[:, -1])
+        assert rel < 2e-2, (step, rel)
+        x = h.pred.cpu().long().view(B, 1)
+        p += Tn
+        Tn = 1
