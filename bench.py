@@ -217,7 +217,7 @@ def bench_interleaved(args, info):
 
 def bench_linear(args, info):
     from distributed_neural_networks_amd.parallel.links import P2PLink
-    from distributed_neural_networks_amd.runtime.pipeline import run_stage_stream
+    from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     dev, N, r = info.device, info.world, info.rank
     if N % 2:
         raise SystemExit("linear placement needs an even number of GPUs")
@@ -232,7 +232,7 @@ def bench_linear(args, info):
     nxt = P2PLink(r + 1, dev) if stage_idx == 0 else None
 
     def step():
-        run_stage_stream(st, M, mb, prev, nxt, source=(lambda i: xs[i]) if xs else None, depth=2)
+        run_gpipe(st, M, mb, prev, nxt, source=(lambda i: xs[i]) if xs else None, depth=2)
 
     for _ in range(args.warmup):
         step()

@@ -2,9 +2,13 @@
 and HIP-graph replay of one step, across batch sizes."""
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_neural_networks_amd.models.cifar import NeuralNetwork
 from distributed_neural_networks_amd.ops import cifar as cops
@@ -25,7 +29,8 @@ def main():
         x = torch.randn(B, 3, 32, 32, device="cuda")
         mid = torch.empty(B, 4096, dtype=adt, device="cuda")
         hid = torch.empty(B, 512, dtype=adt, device="cuda")
-        spl = torch.empty(B, 3 * 4096, dtype=torch.bfloat16, device="cuda") if a.precision == "fp32" else None
+        spl = (torch.empty(B, 3 * 4096, dtype=torch.bfloat16, device="cuda")
+               if a.precision == "fp32" and B < cops.FC1_X3_MIN_ROWS else None)
         probs = torch.empty(B, 10, device="cuda")
         pred = torch.empty(B, dtype=torch.int32, device="cuda")
 

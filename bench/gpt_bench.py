@@ -41,16 +41,22 @@ def parse(argv=None):
     ap.add_argument("--prefill_iters", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
+    ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     return ap.parse_args(argv)
 
 
 def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8):
     from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.runtime.stages import TorchStage
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
     S = len(ranges)
     out = []
     for s in stage_ids:
         a, b = ranges[s]
+        if dev.type == "cpu":  # schedule-test mode only (never a reported number)
+            sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0)
+            out.append(TorchStage(model, sd, a, b, s == 0, s == S - 1, dev))
+            continue
         sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0, device=dev)
         out.append(TransformerStage(model, sd, a, b, s == 0, s == S - 1, dev, max_batch=max_batch,
                                     max_seq=max_seq, fp8=fp8))
@@ -79,7 +85,9 @@ def run(args=None):
     from distributed_neural_networks_amd.parallel.links import P2PLink
 
     N = args.gpus
-    if N > 1 or "WORLD_SIZE" in os.environ:
+    if getattr(args, "cpu", False):
+        info = comm.init("gloo")
+    elif N > 1 or "WORLD_SIZE" in os.environ:
         info = comm.init("nccl")
     else:
         torch.cuda.set_device(0)
@@ -118,10 +126,9 @@ def run(args=None):
     prompts = [torch.randint(0, V, (B, T0), device=dev, dtype=torch.int32) for _ in range(M)] if grp == 0 else None
 
     def sync():
-        torch.cuda.synchronize()
-        if N > 1:
-            import torch.distributed as dist
-            dist.barrier(device_ids=[dev.index])
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier(info)
         return time.perf_counter()
 
     # ---------------- prefill (all microbatches, T0 tokens each) ----------------

@@ -23,12 +23,16 @@
 //    16-B chunk XORed by (Y & 3), which makes every conv2 ds_read_b128 fragment
 //    (four 16-lane groups) conflict-free; conv2 results leave straight from
 //    the accumulators as 8-B fp32 stores (no LDS staging).
+//  * cifar_fc1_x3_kernel: fc1 + bias + ReLU on the fp32 boundary tensor, the
+//    split done in registers while staging A (no split copy in HBM): 256x256x32
+//    tiles, 8 waves of 128x64, per k32 step 3 x 32 mfma_f32_16x16x32_bf16 per
+//    wave (A_hi W_hi + A_hi W_lo + A_lo W_hi) on 24 conflict-free ds_read_b128.
 //  * cifar_split3_kernel: fp32 (B,K) -> bf16 (B,3K) = [hi | hi | lo], the A
-//    operand of fc1 as ONE bf16 GEMM over K' = 3K against W' = [W_hi | W_lo | W_hi]
-//    (gemm_bf16_256_kernel, ReLU epilogue, fp32 out).
+//    operand of the small-batch fc1 (one skinny bf16 GEMM over K' = 3K against
+//    W' = [W_hi | W_lo | W_hi]) when the 256^2 tiles cannot fill the chip.
 //  * cifar_head_tail_x3_kernel: fc2 (512->10) + bias + softmax + per-row argmax
 //    on fp32 hidden rows, 3-term split on mfma_f32_16x16x32_bf16.
-#include "common.h"
+#include "gemm_epilogue.h"
 
 namespace dnn {
 namespace x3 {
@@ -312,6 +316,168 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// fc1 at fp32 precision: C = relu(A . W^T + bias), A fp32 [M][K], W = W_hi + W_lo
+// (bf16 [N][K] each), C fp32.  A is read from HBM once per tile pair as fp32 and
+// split in registers (global_load_dwordx4 -> split2 -> ds_write_b128) while the
+// W halves stream into LDS by DMA (global_load_lds, source-side swizzle).  LDS:
+// 2 buffers x [A_hi A_lo W_hi W_lo] planes of 256 rows x 32 k (64-B rows, 16 KiB)
+// = 128 KiB.  The 16-B chunk c of row r is stored at c ^ ((r >> 2) & 2): the
+// four ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) of a fragment read
+// (lane: row l & 15, chunk l >> 4) then hit 16 distinct slots, and the A
+// writes (8 contiguous lanes = 2 rows x 4 chunks) 8 distinct ds_write slots.
+// One barrier per k32 step: the step's next-tile loads are issued before its
+// MFMAs and land in the other buffer.
+// ---------------------------------------------------------------------------
+constexpr int F1_T = 256, F1_K = 32, F1_PLANE = 256 * 64;
+
+__device__ __forceinline__ int f1_swz(int r) { return (r >> 2) & 2; }
+
+__device__ __forceinline__ bf16x8 f1_frag(const char* plane, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(plane + row * 64 + ((chunk ^ f1_swz(row)) << 4));
+}
+
+__device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, int& tm, int& tn) {
+  // M fastest inside groups of 8 M-tiles: the ntn column tiles of one A panel
+  // run close together on one XCD, so A's second read hits L2 / MALL
+  constexpr int G = 8;
+  const int per = G * ntn, grp = logical / per, first = grp * G;
+  const int gm = min(ntm - first, G), r = logical - grp * per;
+  tm = first + r % gm;
+  tn = r / gm;
+}
+
+// A goes to registers one k-step ahead; a variant that moved A by DMA into a
+// 32 KiB fp32 staging area two k-steps ahead measured 5 % slower (A latency is
+// not the limiter; profiles/r2_cifar_fc1_fused_ab.jsonl) and was dropped.
+__global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __restrict__ A, int lda,
+                                                              const bf16_t* __restrict__ Wh,
+                                                              const bf16_t* __restrict__ Wl, int ldw,
+                                                              const float* __restrict__ bias, float* __restrict__ C,
+                                                              int ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * F1_PLANE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = N / F1_T, ntm = (M + F1_T - 1) / F1_T;
+  int tm, tn;
+  f1_tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
+  const int m0 = tm * F1_T, n0 = tn * F1_T;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nk = K / F1_K;
+  auto plane = [&](int u, int p) { return smem + (u * 4 + p) * F1_PLANE; };  // p: 0 A_hi, 1 A_lo, 2 W_hi, 3 W_lo
+
+  // A: 2 chunks (8 fp32 each) per thread; chunk q = tid + 512 i -> row q >> 2, k-chunk q & 3
+  float4 ar[2][2];
+  auto a_src = [&](int t, int i) {
+    const int q = tid + 512 * i, r = q >> 2, c = q & 3;
+    const int row = min(m0 + r, M - 1);
+    return A + (size_t)row * lda + t * F1_K + c * 8;
+  };
+  auto load_a = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float* p = a_src(t, i);
+      ar[i][0] = *reinterpret_cast<const float4*>(p);
+      ar[i][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
+  };
+  auto store_a = [&](int u) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 512 * i, r = q >> 2, c = q & 3;
+      uint4 hi, lo;
+      split2(ar[i][0].x, ar[i][0].y, hi.x, lo.x);
+      split2(ar[i][0].z, ar[i][0].w, hi.y, lo.y);
+      split2(ar[i][1].x, ar[i][1].y, hi.z, lo.z);
+      split2(ar[i][1].z, ar[i][1].w, hi.w, lo.w);
+      const int o = r * 64 + ((c ^ f1_swz(r)) << 4);
+      *reinterpret_cast<uint4*>(plane(u, 0) + o) = hi;
+      *reinterpret_cast<uint4*>(plane(u, 1) + o) = lo;
+    }
+  };
+  // W: per plane 16 pieces of 16 rows (1 KiB per wave instruction), 2 per wave
+  auto stage_w = [&](int u, int t) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bf16_t* W = p ? Wl : Wh;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int piece = wave * 2 + j, rl = piece * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ f1_swz(rl);
+        glds16(W + (size_t)(n0 + rl) * ldw + t * F1_K + c * 8, plane(u, 2 + p) + piece * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_a(0);
+  stage_w(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  store_a(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fc = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    const int u = t & 1;
+    if (t + 1 < nk) {
+      load_a(t + 1);
+      stage_w(u ^ 1, t + 1);
+    }
+    const char* ah_p = plane(u, 0);
+    const char* al_p = plane(u, 1);
+    const char* bh_p = plane(u, 2);
+    const char* bl_p = plane(u, 3);
+    bf16x8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = f1_frag(bh_p, wc * 64 + j * 16 + fr, fc);
+      bl[j] = f1_frag(bl_p, wc * 64 + j * 16 + fr, fc);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 ah[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ah[i] = f1_frag(ah_p, wr * 128 + (h * 4 + i) * 16 + fr, fc);
+        al[i] = f1_frag(al_p, wr * 128 + (h * 4 + i) * 16 + fr, fc);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4& a = acc[h * 4 + i][j];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], a, 0, 0, 0);
+        }
+    }
+    if (t + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_a(u ^ 1);
+    }
+    // raw barrier (lgkmcnt for this step's LDS writes; the DMAs were waited
+    // above): 6 % faster than __syncthreads here
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // epilogue (transposed accumulators): row m0 + wr*128 + i*16 + (lane & 15), cols n..n+3
+  const bool vec = epi_vec_ok(C, ldc, bias, nullptr, 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_t4<ACT_RELU, true>(acc[i][j], m, n0 + wc * 64 + j * 16 + fc * 4, M, N, C, ldc, bias, nullptr, 0, vec);
+  }
+}
+
 // fp32 (M,K) -> bf16 (M,3K) rows [hi | hi | lo]; K % 8 == 0, 16-B aligned rows.
 __global__ __launch_bounds__(256) void cifar_split3_kernel(const float* __restrict__ a, int lda,
                                                            bf16_t* __restrict__ o, int ldo, int M, int K) {
@@ -407,6 +573,16 @@ extern "C" int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, 
   if (grid > B) grid = B;
   hipLaunchKernelGGL(cifar_stage0_x3_kernel, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
                      (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_cifar_fc1_x3(const float* A, int lda, const void* Wh, const void* Wl, int ldw, const float* bias,
+                                float* C, int ldc, int M, int N, int K, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % F1_T != 0 || K % F1_K != 0 || lda % 4 != 0 || ldw % 8 != 0 || ldc % 4 != 0) return -1;
+  const int blocks = ((M + F1_T - 1) / F1_T) * (N / F1_T);
+  hipLaunchKernelGGL(cifar_fc1_x3_kernel, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
+                     (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
   return (int)hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ Stage semantics mirror the reference part classes:
   ``last_only=True`` restricts the head to the final position (decode/serving);
   the default computes logits for all T like the reference.
 
-This is the fp32/bf16 torch oracle; the MI355X path is ``runtime/gpt_engine.py``.
+This is the fp32/bf16 torch oracle; the MI355X path is ``runtime/transformer.py``.
 """
 from __future__ import annotations
 

@@ -7,8 +7,10 @@ fp32 modules to the device):
   Every fp32 operand is split into bf16 hi + lo and each product is three bf16
   MFMAs (hi*hi + hi*lo + lo*hi) accumulated in fp32.  Stage boundary tensor
   ``(B,4096)`` fp32 exactly as the reference ships it (``node.py:45-48``).
-  fc1 runs as ONE bf16 GEMM over K' = 3*4096 on ``[A_hi | A_hi | A_lo]`` x
-  ``[W_hi | W_lo | W_hi]`` with a ReLU + fp32-out epilogue.
+  fc1 at large batch is ``cifar_fc1_x3``: the fp32 boundary rows are split in
+  registers while staged to LDS (A read once as fp32, no split copy); at small
+  batch (too few 256-row tiles to fill the chip) it runs as ONE skinny/128^2
+  bf16 GEMM over K' = 3*4096 on ``[A_hi | A_hi | A_lo]`` x ``[W_hi | W_lo | W_hi]``.
 * ``bf16``: ``csrc/kernels/cifar_fused.hip`` (v4 persistent kernel), bf16
   boundary, an explicitly reduced-precision mode.
 
@@ -73,7 +75,9 @@ class CifarStage0Weights:
 @dataclass
 class CifarHeadWeights:
     precision: str
-    w_fc1: torch.Tensor = None   # bf16: [512][4096]; fp32: [512][3*4096] = [hi | lo | hi]
+    w_fc1: torch.Tensor = None   # bf16: [512][4096]; fp32: [512][3*4096] = [hi | lo | hi] (small batch)
+    w_fc1h: torch.Tensor = None  # fp32 path, large batch: W hi / lo [512][4096] each (cifar_fc1_x3)
+    w_fc1l: torch.Tensor = None
     b_fc1: torch.Tensor = None
     w_fc2: torch.Tensor = None   # bf16: [16][512]
     w_fc2h: torch.Tensor = None  # fp32 path: split fc2
@@ -112,6 +116,7 @@ def pack_head(sd: Dict[str, torch.Tensor], device, fc1: bool = True, fc2: bool =
         else:
             hi, lo = split_bf16(f)
             w.w_fc1 = torch.cat([hi, lo, hi], dim=1).to(device).contiguous()
+            w.w_fc1h, w.w_fc1l = hi.to(device).contiguous(), lo.to(device).contiguous()
         w.b_fc1 = sd["fc1.bias"].float().to(device).contiguous()
     if fc2:
         f2 = _fc2_pad(sd)
@@ -130,6 +135,9 @@ def act_dtype(precision: str) -> torch.dtype:
 
 
 STAGE0_GRID = 0  # persistent stage-0 workgroups; 0 = one per CU (256)
+# fused fp32 fc1 from this batch on: 2 x B/256 tiles of 128 k32 steps each need
+# >= 128 tiles to occupy the chip; below, split3 + the K-concat GEMM is faster
+FC1_X3_MIN_ROWS = 16384
 
 
 def set_stage0_grid(grid: int = 0) -> None:
@@ -175,6 +183,12 @@ def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor
     B = h.shape[0]
     if w.precision == "bf16":
         return linear(h, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
+    if B >= FC1_X3_MIN_ROWS:
+        if out is None:
+            out = torch.empty((B, 512), dtype=torch.float32, device=h.device)
+        check(lib().cifar_fc1_x3(ptr(h), 4096, ptr(w.w_fc1h), ptr(w.w_fc1l), 4096, ptr(w.b_fc1), ptr(out), 512,
+                                 B, 512, 4096, stream_ptr()), "cifar_fc1_x3")
+        return out
     if scratch is None or scratch.shape[0] < B or tuple(scratch.shape[1:]) != (3 * 4096,):
         scratch = torch.empty((B, 3 * 4096), dtype=torch.bfloat16, device=h.device)
     a3 = scratch[:B]

@@ -2,8 +2,7 @@
 
 Stage forwards are chained on one stream over preallocated buffers and the
 whole step is captured into one HIP graph.  The multi-rank schedules (GPipe
-stream, CLI request stream, decode ring) live in ``runtime/scheduler.py``;
-``run_stage_stream`` is re-exported from there.
+stream, CLI request stream, decode ring) live in ``runtime/scheduler.py``.
 """
 from __future__ import annotations
 
@@ -13,7 +12,6 @@ import torch
 
 from ..utils import trace
 from .graph import GraphedStep
-from .scheduler import run_gpipe, run_stage_stream  # noqa: F401 (re-export)
 from .stages import StageCompute, StageOutput
 
 

@@ -156,10 +156,6 @@ def run_gpipe(stage, M: int, batch: int, prev=None, nxt=None,
     outs.drained()
 
 
-# backwards-compatible name (round-1 API)
-run_stage_stream = run_gpipe
-
-
 # --------------------------------------------------------------------------- CLI forward stream
 KIND_DATA, KIND_STOP = 1, 2
 

@@ -99,7 +99,7 @@ class CifarHipStage(StageCompute):
             b = {}
             if self.first and self.end >= 2:
                 b["mid"] = torch.empty((batch, 4096), dtype=self.adt, device=d)
-            if self.start <= 2 <= self.end and self.precision == "fp32":
+            if self.start <= 2 <= self.end and self.precision == "fp32" and batch < self._cops.FC1_X3_MIN_ROWS:
                 b["split"] = torch.empty((batch, 3 * 4096), dtype=torch.bfloat16, device=d)
             if self.last:
                 b["hid"] = torch.empty((batch, 512), dtype=self.adt, device=d)

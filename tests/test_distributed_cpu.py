@@ -152,7 +152,7 @@ def _worker_stream(rank, world, port, q):
     from distributed_neural_networks_amd.models import cifar
     from distributed_neural_networks_amd.parallel import comm
     from distributed_neural_networks_amd.parallel.links import P2PLink
-    from distributed_neural_networks_amd.runtime.pipeline import run_stage_stream
+    from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     from distributed_neural_networks_amd.runtime.stages import TorchStage
     torch.set_num_threads(1)
     info = comm.init("gloo", rank=rank, world=world, master_addr="127.0.0.1", master_port=port)
@@ -165,7 +165,7 @@ def _worker_stream(rank, world, port, q):
     res = {}
     prev = P2PLink(rank - 1, info.device) if rank > 0 else None
     nxt = P2PLink(rank + 1, info.device) if rank < world - 1 else None
-    run_stage_stream(st, 5, 3, prev, nxt, source=lambda i: xs[i],
+    run_gpipe(st, 5, 3, prev, nxt, source=lambda i: xs[i],
                      sink=(lambda i, y: res.__setitem__(i, y.probs.clone())) if rank == world - 1 else None, depth=2)
     if rank == world - 1:
         q.put({i: v.numpy() for i, v in res.items()})
@@ -195,18 +195,44 @@ def test_stream_schedule_gloo(world):
             assert torch.allclose(torch.from_numpy(out[i]), m(x), atol=1e-5)
 
 
-@pytest.mark.parametrize("placement", ["interleaved", "linear"])
-def test_bench_distributed_schedule_cpu(placement):
+@pytest.mark.parametrize("placement,n", [("linear", 2), ("linear", 4), ("linear", 8), ("interleaved", 2)])
+def test_bench_distributed_schedule_cpu(placement, n):
+    """bench.py's multi-GPU placements with gloo on CPU (the driver's N = 2/4/8
+    scaling runs use the same schedule over RCCL); the JSON line has the same
+    metric / config / dtype keys as the N = 1 run."""
     port = free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu",
-           "--batch", "32", "--steps", "2", "--warmup", "1", "--microbatches", "2", "--latency_iters", "3",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--cpu",
+           "--batch", "16", "--steps", "2", "--warmup", "1", "--microbatches", "2", "--latency_iters", "3",
            "--placement", placement]
-    r = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=300)
+    env = dict(ENV, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
+    assert d["n_gpus"] == n and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
+    assert d["dtype"] == "fp32" and d["scaling"] == "weak"
+    assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
+    if placement == "linear":
+        assert d["config"]["parallelism"] == f"pp2-linear-x{n // 2}"
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_gpt_decode_ring_bench_cpu(n):
+    """bench/gpt_bench.py's microbatched decode ring over n gloo ranks (4
+    stage groups; 8 ranks = 2 replicas of the 4-stage ring)."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench", "gpt_bench.py"), "--gpus", str(n),
+           "--cpu", "--model", "gpt2-tiny", "--stages", "4", "--batch", "2", "--prompt", "8", "--steps", "4",
+           "--warmup", "1", "--prefill_iters", "1"]
+    env = dict(ENV, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == n and d["value"] > 0
+    assert d["config"]["gpu_groups"] == 4 and d["config"]["replicas"] == n // 4
+    assert d["config"]["microbatches"] == 4
 
 
 # ----------------------------------------------------------------------------- failure detection

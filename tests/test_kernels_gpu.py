@@ -222,3 +222,44 @@ def test_cifar_stage_cuts(cut, precision):
     assert (out.probs.cpu() - ref).abs().max().item() < tol
     dt = torch.float32 if precision == "fp32" else torch.bfloat16
     assert st[0].out_spec(8) == ((8, 4096 if cut == 1 else 512), dt)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 64), (1000, 512, 4096), (16384 + 77, 512, 4096)])
+def test_cifar_fc1_x3_kernel(M, N, K):
+    """Fused fp32 fc1 (split in registers while staging): relu(A W^T + b) vs
+    fp32 torch, relative error at the ~2^-16 level of the 3-term split."""
+    from distributed_neural_networks_amd.ops import _lib
+    from distributed_neural_networks_amd.ops.cifar import split_bf16
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) / K ** 0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    wh, wl = split_bf16(w)
+    out = torch.empty(M, N, device=DEV)
+    rc = _lib.lib().cifar_fc1_x3(a.data_ptr(), K, wh.data_ptr(), wl.data_ptr(), K, b.data_ptr(), out.data_ptr(), N,
+                                 M, N, K, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = torch.relu(a.double() @ w.double().t() + b.double())
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 2e-5 * ref.abs().max().item(), err
+
+
+def test_cifar_fp32_pipeline_large_batch_fused_fc1():
+    """The large-batch fp32 head (fused fc1) on 20000 images: max |dprob| <= 1e-5
+    vs the fp32 torch model and argmax agreement on every decidable row."""
+    from distributed_neural_networks_amd.ops import cifar as cops
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
+    B = 20000
+    assert B >= cops.FC1_X3_MIN_ROWS
+    sd, x, _, ref = _cifar_golden(3, B)
+    st = [CifarHipStage(sd, 0, 1, DEV), CifarHipStage(sd, 2, 3, DEV)]
+    out = ColocatedPipeline(st, B)(x.to(DEV))
+    torch.cuda.synchronize()
+    dp = (out.probs.cpu() - ref).abs().max().item()
+    assert dp <= 1e-5, dp
+    top2 = ref.topk(2, dim=1).values
+    decidable = (top2[:, 0] - top2[:, 1]) > 1e-6
+    agree = out.pred.cpu().long() == ref.argmax(1)
+    assert bool(agree[decidable].all()), int((~agree[decidable]).sum())

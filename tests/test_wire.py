@@ -75,3 +75,41 @@ def test_large_message_roundtrip():
     m = proto.TensorRequest(request_id="big", tensor=codec.encode(a))
     b = proto.TensorRequest.FromString(m.SerializeToString())
     assert codec.decode(b.tensor).shape == (300, 4096)
+
+
+REF_PB2 = "/root/reference/node_service_pb2.py"
+
+
+def _reference_descriptor():
+    """The reference's serialized FileDescriptorProto (node_service_pb2.py:27),
+    parsed as DATA: the bytes literal is read with ast.literal_eval (literals
+    only, nothing of the reference file is executed or imported)."""
+    import ast
+    import os
+    import re
+    from google.protobuf import descriptor_pb2
+    if not os.path.exists(REF_PB2):
+        pytest.skip("reference tree not present")
+    src = open(REF_PB2).read()
+    m = re.search(r"AddSerializedFile\((b'(?:[^'\\]|\\.)*')\)", src)
+    assert m, "serialized descriptor literal not found"
+    return descriptor_pb2.FileDescriptorProto.FromString(ast.literal_eval(m.group(1)))
+
+
+def test_descriptor_matches_reference_field_by_field():
+    from google.protobuf import descriptor_pb2
+    ref = _reference_descriptor()
+    ours = descriptor_pb2.FileDescriptorProto()
+    proto.FILE_DESCRIPTOR.CopyToProto(ours)
+    assert ours.package == ref.package == "node_service"
+    assert ours.syntax == ref.syntax
+
+    def msgs(fd):
+        return {m.name: [(f.name, f.number, f.type, f.label, f.type_name, f.proto3_optional, f.oneof_index
+                          if f.HasField("oneof_index") else None) for f in m.field] for m in fd.message_type}
+    assert msgs(ours) == msgs(ref)
+
+    def svcs(fd):
+        return {s.name: [(x.name, x.input_type, x.output_type, x.client_streaming, x.server_streaming)
+                         for x in s.method] for s in fd.service}
+    assert svcs(ours) == svcs(ref)
