@@ -4,23 +4,26 @@
 Metric/config from BASELINE.json (the reference's only measured headline:
 CIFAR-10 2-stage images/s; 3.40-4.15 k img/s on CPU over localhost gRPC,
 BASELINE.md).  Synthetic fp32 images, random-init weights of the reference
-architecture, bf16 compute on the fused gfx950 kernels.  Every timed step runs
-the complete forward of both stages (conv stage + fc/softmax/argmax stage) on
+architecture, computed at the reference's precision (fp32: every product as
+three bf16 MFMA terms, ops/cifar.py); ``--precision bf16`` is the reduced-
+precision variant and is reported as extra keys.  Every timed step runs the
+complete forward of both stages (conv stage + fc/softmax/argmax stage) on
 fresh launches; nothing is cached across steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Placements:
-* N = 1: both stages colocated on the GPU, one HIP graph per step.
-* N > 1 (one process per GPU, RCCL): ``interleaved`` (default) — N pipelines,
-  pipeline r's stage 0 on GPU r and its stage 1 spread over the other N-1
-  GPUs; the stage hop is one all-to-all over the xGMI mesh per microbatch
-  (each GPU uses all of its links instead of one, and every GPU hosts a
-  stage-0 and a stage-1 so the 73/27 stage imbalance cancels), overlapped with
-  the next microbatch's stage-0 compute.  ``linear`` — N/2 replicas of the
-  reference topology (stage 0 on GPU 2k, stage 1 on GPU 2k+1, isend/irecv).
-Scaling is weak: each GPU sources ``--batch`` images per step.
+* N = 1: both stages colocated on the GPU, one HIP graph per step; extra keys:
+  the bf16 pipeline and the GPT-2 small 4-stage pipeline (decode / prefill
+  tokens/s, p50 per-token latency; bench/gpt_bench.py).
+* N > 1 (one process per GPU, RCCL): ``linear`` (default) — the reference
+  topology, one stage per GPU, isend/irecv over the direct xGMI links; the
+  bottleneck stage is replicated (``parallel/partition.py::linear_plan``: n0
+  stage-0 GPUs feed n1 stage-1 GPUs, each sender on its own link), the K steps
+  stream as one fill/drain.  ``interleaved`` (opt-in) — every GPU hosts stage
+  0 of its pipeline and stage 1 of the others; the hop is an all-to-all.
+Scaling is weak: each stage-0 GPU sources ``--batch`` images per step.
 
 ``--model gpt2`` runs the GPT-2 4-stage token throughput bench instead
 (bench/gpt_bench.py).
@@ -95,7 +98,7 @@ def pick_cut(args, info) -> int:
         return int(args.cut)
     if info.world == 1:
         return 1  # colocated: no hop; keep the reference split
-    return cifar_cut(args.placement, info.world)
+    return cifar_cut(args.placement, info.world, precision=args.precision)
 
 
 def dsync(dev):
@@ -216,31 +219,43 @@ def bench_interleaved(args, info):
 
 
 def bench_linear(args, info):
+    """Linear 2-stage pipeline, one stage per GPU, RCCL isend/irecv over the
+    direct xGMI links (``parallel/partition.py::linear_plan``): n0 stage-0 GPUs
+    each source ``--batch`` images per step and stream them to one of n1
+    stage-1 GPUs.  The K timed steps run as ONE stream of K x M microbatches
+    (fill and drain once, not per step)."""
     from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.parallel.partition import linear_plan, linear_role
     from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     dev, N, r = info.device, info.world, info.rank
-    if N % 2:
-        raise SystemExit("linear placement needs an even number of GPUs")
+    plan = linear_plan(N, args.precision)
+    if args.cut != "auto":
+        plan = dict(plan, cut=args._cut)
+    args._cut = plan["cut"]
+    role = linear_role(r, plan)
     s0, s1 = stages_for(dev, args._cut, args.precision)
-    stage_idx = r % 2
-    st = s0 if stage_idx == 0 else s1
     M = max(1, args.microbatches)
-    mb = args.batch * 2 // M  # a pair sources 2*batch images per step (weak scaling per GPU)
+    mb = args.batch // M
     g = torch.Generator(device=dev).manual_seed(1 + r)
-    xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)] if stage_idx == 0 else None
-    prev = P2PLink(r - 1, dev) if stage_idx == 1 else None
-    nxt = P2PLink(r + 1, dev) if stage_idx == 0 else None
+    if role["stage"] == 0:
+        xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
+        nxt = P2PLink(role["send_to"], dev)
 
-    def step():
-        run_gpipe(st, M, mb, prev, nxt, source=(lambda i: xs[i]) if xs else None, depth=2)
+        def stream(steps):
+            run_gpipe(s0, steps * M, mb, None, nxt, source=lambda i: xs[i % M], depth=2)
+    else:
+        prevs = [P2PLink(p, dev) for p in role["recv_from"]]
 
-    for _ in range(args.warmup):
-        step()
+        def stream(steps):
+            run_gpipe(s1, steps * M * len(prevs), mb, prevs, None, depth=2 * len(prevs))
+
+    stream(args.warmup)
     t0 = sync_time(info)
-    for _ in range(args.steps):
-        step()
+    stream(args.steps)
     t1 = sync_time(info)
-    return t1 - t0, mb * M // 2, float("nan"), f"pp2-linear-x{N // 2}"
+    imgs_total_per_step = plan["n0"] * mb * M
+    par = f"pp2-linear-{plan['n0']}x{plan['n1']}"
+    return t1 - t0, imgs_total_per_step / N, float("nan"), par
 
 
 def extra_keys(args, info):
@@ -312,7 +327,7 @@ def main():
             "dtype": args.precision, "data": "synthetic (random fp32 images, random-init weights)",
             "p50_latency_ms": None if p50 != p50 else round(p50, 4),
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
-                       "global_batch": imgs_per_gpu * N, "seq_len": None, "parallelism": par,
+                       "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
                        "stage0_spare_cus": spare,
                        "stage_cut": {1: "conv|fc (reference split, 8 KiB/img hop)",

@@ -104,16 +104,57 @@ def choose_cut(unit_ns: Sequence[float], boundary_bytes: Sequence[int], cuts: Se
     return best
 
 
-# Measured on 1x MI355X (profiles/r1_*): per-image ns of the CIFAR units with the
-# fused kernels (conv stage = units 0-1 together) and bf16 boundary sizes.
-CIFAR_UNIT_NS = (0.0, 10.8, 5.3, 0.3)
-CIFAR_BOUNDARY_BYTES = (32 * 16 * 16 * 2, 4096 * 2, 512 * 2, 10 * 4)
+# Measured on 1x MI355X: per-image ns of the CIFAR units with the fused kernels
+# (conv stage = units 0-1 together) and the boundary bytes per image, per
+# precision (bf16: profiles/r1_*; fp32: profiles/r2_cifar_fc1_fused_ab.jsonl,
+# profiles/r2_bench_cifar_fp32_n1_kernels.md at B = 65536).
+CIFAR_UNIT_NS = {"bf16": (0.0, 10.8, 5.3, 0.3), "fp32": (0.0, 27.0, 11.7, 0.5)}
+CIFAR_BOUNDARY_BYTES = {"bf16": (32 * 16 * 16 * 2, 4096 * 2, 512 * 2, 10 * 4),
+                        "fp32": (32 * 16 * 16 * 4, 4096 * 4, 512 * 4, 10 * 4)}
 XGMI_LINK_GBS = 50.0  # conservative usable P2P GB/s per direction per link (7 links x ~153 GB/s aggregate spec)
 
 
-def cifar_cut(placement: str, world: int, link_gbs: float = XGMI_LINK_GBS) -> int:
+def cifar_cut(placement: str, world: int, link_gbs: float = XGMI_LINK_GBS, precision: str = "fp32") -> int:
     """Cut for the CIFAR 2-stage pipeline on MI355X: 1 (reference conv|fc) or 2 (after fc1)."""
-    return choose_cut(CIFAR_UNIT_NS, CIFAR_BOUNDARY_BYTES, (1, 2), placement, world, link_gbs)
+    if placement == "linear":
+        return linear_plan(world, precision, link_gbs)["cut"]
+    return choose_cut(CIFAR_UNIT_NS[precision], CIFAR_BOUNDARY_BYTES[precision], (1, 2), placement, world, link_gbs)
+
+
+def linear_plan(world: int, precision: str = "fp32", link_gbs: float = XGMI_LINK_GBS,
+                unit_ns: Optional[Sequence[float]] = None, boundary_bytes: Optional[Sequence[int]] = None,
+                cuts: Sequence[int] = (1, 2)) -> dict:
+    """Linear 2-stage pipeline on ``world`` GPUs, one stage per GPU: ``n0``
+    GPUs run stage 0 (units [0..cut]) and each sends its activations over its
+    own direct xGMI link to one of ``n1`` stage-1 GPUs (sender s -> receiver
+    n0 + s % n1).  The bottleneck stage is replicated instead of left idle:
+    with stage 0 at ~99 % of the compute after the fc1 cut, 7 stage-0 GPUs feed
+    1 stage-1 GPU on 8 GPUs (every sender on a link of its own on the fully
+    connected board).  Chooses (cut, n0, n1) maximising items per ns:
+    min(n0 / t0, n1 / t1, n0 / hop) (a hop overlaps the next microbatch)."""
+    unit_ns = unit_ns or CIFAR_UNIT_NS[precision]
+    boundary_bytes = boundary_bytes or CIFAR_BOUNDARY_BYTES[precision]
+    if world < 2:
+        raise ValueError("a linear pipeline needs >= 2 GPUs")
+    best, best_rate = None, -1.0
+    for c in cuts:
+        t0, t1 = sum(unit_ns[:c + 1]), sum(unit_ns[c + 1:])
+        hop = boundary_bytes[c] / link_gbs
+        for n1 in range(1, world):
+            n0 = world - n1
+            rate = min(n0 / t0, n1 / max(t1, 1e-9), n0 / hop)
+            if rate > best_rate + 1e-12:
+                best, best_rate = {"cut": c, "n0": n0, "n1": n1}, rate
+    best["items_per_ns"] = best_rate
+    return best
+
+
+def linear_role(rank: int, plan: dict) -> dict:
+    """This rank's role in ``linear_plan``: stage, its peer(s)."""
+    n0, n1 = plan["n0"], plan["n1"]
+    if rank < n0:
+        return {"stage": 0, "send_to": n0 + rank % n1}
+    return {"stage": 1, "recv_from": [s for s in range(n0) if n0 + s % n1 == rank]}
 
 
 def resolve_ranges(num_layers: int, num_stages: int, given: Sequence[Optional[Range]],

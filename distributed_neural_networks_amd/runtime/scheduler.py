@@ -97,8 +97,15 @@ def run_gpipe(stage, M: int, batch: int, prev=None, nxt=None,
 
     ``prev``/``nxt`` are links to the neighbouring ranks (None at the ends);
     the first rank pulls inputs from ``source(i)``, every rank may observe its
-    outputs with ``sink(i, y)`` (the last rank gets ``StageOutput``)."""
+    outputs with ``sink(i, y)`` (the last rank gets ``StageOutput``).  ``prev``
+    may be a list of links (fan-in from replicated upstream ranks): microbatch i
+    then comes from ``prev[i % len(prev)]``, each sender's stream in order."""
     stage = as_stage(stage)
+    prevs = list(prev) if isinstance(prev, (list, tuple)) else ([prev] if prev is not None else [])
+    prev = prevs[0] if prevs else None
+
+    def src_link(i):
+        return prevs[i % len(prevs)]
     progress = progress or _noop
     dev = stage.device
     ishp, idt = stage.in_spec(batch)
@@ -111,7 +118,7 @@ def run_gpipe(stage, M: int, batch: int, prev=None, nxt=None,
     ins, outs = SlotOrder("in_slots", depth), SlotOrder("out_slots", depth)
     if prev is not None:
         for k in range(depth):
-            rwork[k] = prev.irecv(in_slots[k])
+            rwork[k] = src_link(k).irecv(in_slots[k])
             ins.post(k, "recv", k)
     for i in range(M):
         k = i % depth
@@ -135,10 +142,10 @@ def run_gpipe(stage, M: int, batch: int, prev=None, nxt=None,
         send_t = (y if isinstance(y, torch.Tensor) else y.probs) if nxt is not None else None
         if post_recv and send_t is not None:
             # middle stage: send(i) -> next and recv(i+depth) <- prev as one group
-            w = exchange([(nxt, send_t)], [(prev, in_slots[k])])
+            w = exchange([(nxt, send_t)], [(src_link(i + depth), in_slots[k])])
             rwork[k] = swork[k] = w
         elif post_recv:
-            rwork[k] = prev.irecv(in_slots[k])  # queued behind this slot's compute
+            rwork[k] = src_link(i + depth).irecv(in_slots[k])  # queued behind this slot's compute
         elif send_t is not None:
             swork[k] = nxt.isend(send_t)
         if post_recv:
