@@ -328,7 +328,7 @@ __device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int s
 // cache; its own scores use the register copy, so no other split touches that
 // row and there is no qkv_split launch.  Otherwise q is head-major (B,H,hd)
 // and lens[b] keys are cached.
-template <int HD, int G, bool FUSED>
+template <int HD, int G, bool FUSED, bool NT>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
                                                           bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                           float* __restrict__ ws, int H, int Hkv, int S,
@@ -411,7 +411,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
     for (int u = 0; u < DEC_U; ++u) {
       const int kk = min(kb0 + u * GPB + grp, n - 1);
-      kr[u] = *reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
+      // NT: the caches are far larger than L2 / MALL and every row is read once
+      // per step, so stream them non-temporally (GPT-2 B=64: 0.658 -> 0.590 ms
+      // per decode step); small caches (batch 1) stay cacheable: they live in
+      // the MALL from one step to the next
+      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
+      kr[u] = NT ? __builtin_nontemporal_load(kp) : *kp;
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -464,7 +469,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
     for (int u = 0; u < DEC_U; ++u) {
       const int kk = min(kb0 + u * GPB + grp, n - 1);
-      vr[u] = *reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+      const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+      vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
     }
     __builtin_amdgcn_sched_barrier(0);
     // Key pairs (u, u+1) of this thread share the d chunk: interleave their
@@ -613,17 +619,26 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
   if (smem > 160 * 1024) return -3;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(B * Hkv, splits);
+  // cache bytes this launch may stream (capacity bound): > 32 MB -> non-temporal
+  const bool nt = (double)B * Hkv * S * hd * 4.0 > 32.0 * 1024 * 1024;
+#define DEC_NT(HDV, GV, NTV)                                                                                          \
+  if (fused)                                                                                                          \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, true, NTV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,    \
+                       (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, chunk_cap, (bf16_t*)o);        \
+  else                                                                                                                \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, false, NTV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,   \
+                       (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2, chunk_cap, (bf16_t*)o);
 #define DEC(HDV, GV)                                                                                                  \
   if (hd == HDV && G == GV) {                                                                                         \
-    if (fused)                                                                                                        \
-      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, true>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,       \
-                         (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, chunk_cap, (bf16_t*)o);      \
-    else                                                                                                              \
-      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, false>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,      \
-                         (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2, chunk_cap, (bf16_t*)o); \
+    if (nt) {                                                                                                         \
+      DEC_NT(HDV, GV, true)                                                                                           \
+    } else {                                                                                                          \
+      DEC_NT(HDV, GV, false)                                                                                          \
+    }                                                                                                                 \
   } else
   DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(128, 1) DEC(128, 2) DEC(128, 4) DEC(128, 8) { return -2; }
 #undef DEC
+#undef DEC_NT
   if (splits > 1)
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
   return (int)hipGetLastError();

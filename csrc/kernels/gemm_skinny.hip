@@ -177,7 +177,15 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     for (int u = 0; u < U; ++u) {
       const int ci = min(cc + u, c1 - 1);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) wv[j][u] = *reinterpret_cast<const i32x4*>(wp[j] + (size_t)ci * wstep);
+      for (int j = 0; j < NT; ++j) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(wp[j] + (size_t)ci * wstep);
+        // each weight byte is read by exactly one wave of one workgroup (no M
+        // split): stream it non-temporally so it does not evict the activations
+        // and the next kernel's operands from L2 (guide: nt-weights, 5-10 % per
+        // decode layer); with the M split the slice is re-read from L2 by the
+        // other M tiles, so keep the default policy there
+        wv[j][u] = MS ? *src : __builtin_nontemporal_load(src);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -345,7 +353,8 @@ using namespace dnn;
 // bench/skinny_sweep.py on MI355X (profiles/r1_skinny_sweep.jsonl, weights
 // rotated past the 256 MB MALL):
 //   M <= 8     : 1 tile, 4 chunks in flight, 8 waves/WG (within 3% of the best
-//                config on every Llama-3 / GPT-2 XL shape)
+//                row-major config on every Llama-3 / GPT-2 XL shape); with the
+//                fragment-order copy (Wsh) the per-class rules below
 //   M <= 16    : wide N (>= 16K): 4 tiles x 2 chunks, 2 waves; else 2 tiles x 2
 //                chunks pipelined, 4 waves
 //   M <= 64    : by N class (wide >= 16K / mid / narrow <= 4K): 4 / 2 / 1 column
@@ -374,7 +383,14 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
   return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
                                                                        ldr, M, N, kbytes, KSV, colsum, eps, st, Wsh)
-  if (M <= 8) CFG(1, 1, 4, false, 8);
+  if (M <= 8) {
+    // fragment-order weights at batch 1-8 only for the mid-size N (QKV): in the
+    // Llama-3 8B fp8 decode graph 12.25 -> 10.33 us; on gate|up, O and down the
+    // row-major stream stayed as fast or faster in-graph (25.6 vs 26.3, 9.7 vs
+    // 10.1 us) although the cold-cache sweep favoured the copy
+    if (!FP8 && Wsh != nullptr && N > 4096 && N < 16384 && kbytes <= 8192) CFG(1, 1, 4, false, 4);
+    CFG(1, 1, 4, false, 8);
+  }
   if (M <= 16) {
     if (wide) CFG(1, 4, 2, false, 2);
     CFG(1, 2, 2, true, 4);

@@ -15,16 +15,50 @@ import torch  # noqa: F401  (must precede the extension: shared HIP runtime)
 _lib = None
 
 
+def verify_stamp(path: str) -> dict:
+    """Build provenance check: the library must carry a stamp
+    (``ops/build.py::write_stamp``) whose library hash matches the file and
+    whose source hashes match the sources in this tree.  A stale binary (built
+    from other sources) raises instead of silently running old kernels.
+    ``DNN_SKIP_STAMP=1`` skips the check (kernel development only)."""
+    import hashlib
+    import json
+    stamp_path = os.path.join(os.path.dirname(path), "_dnn_hip.build.json")
+    if os.environ.get("DNN_SKIP_STAMP"):
+        return {}
+    if not os.path.exists(stamp_path):
+        raise RuntimeError(f"{path} has no build stamp ({stamp_path}); rebuild with "
+                           "`python -m distributed_neural_networks_amd.ops.build`")
+    stamp = json.load(open(stamp_path))
+    if hashlib.sha256(open(path, "rb").read()).hexdigest() != stamp.get("library_sha256"):
+        raise RuntimeError(f"{path} does not match its build stamp (library replaced after the build); rebuild")
+    from .build import source_digest
+    now = source_digest()
+    stale = sorted(k for k in set(now) | set(stamp.get("sources", {})) if now.get(k) != stamp["sources"].get(k))
+    if stale:
+        raise RuntimeError(f"{path} was built from different sources ({', '.join(stale[:6])}); rebuild with "
+                           "`python -m distributed_neural_networks_amd.ops.build`")
+    return stamp
+
+
 def lib():
     global _lib
     if _lib is None:
         try:
-            _lib = importlib.import_module("distributed_neural_networks_amd._dnn_hip")
+            mod = importlib.import_module("distributed_neural_networks_amd._dnn_hip")
         except ImportError as e:
             raise RuntimeError(
                 "HIP kernel library _dnn_hip is not built; run "
                 "`python -m distributed_neural_networks_amd.ops.build` (hipcc, gfx950)") from e
+        verify_stamp(mod.__file__)
+        _lib = mod
     return _lib
+
+
+def build_stamp() -> dict:
+    import json
+    p = os.path.join(os.path.dirname(library_path()), "_dnn_hip.build.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
 
 
 def available() -> bool:

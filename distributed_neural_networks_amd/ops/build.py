@@ -90,9 +90,38 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    write_stamp(srcs)
     if verbose:
         print(f"[build] {LIB_PATH} ({len(objs)} objects, arch {ARCH})")
     return LIB_PATH
+
+
+STAMP_PATH = os.path.join(PKG, "_dnn_hip.build.json")
+
+
+def source_digest(srcs: List[str] = None) -> dict:
+    """sha256 of every source and header the library is built from."""
+    import hashlib
+    srcs = srcs or sources()
+    files = sorted(set(srcs) | set(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)))
+    return {os.path.relpath(f, ROOT): hashlib.sha256(open(f, "rb").read()).hexdigest() for f in files}
+
+
+def write_stamp(srcs: List[str]) -> None:
+    """Build provenance next to the .so: source hashes, per-file flags, the
+    compiler, the library's own hash (``_lib.verify_stamp`` checks them at
+    load, so a stale or foreign binary fails loudly instead of running)."""
+    import hashlib
+    import json
+    import time
+    r = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True)
+    stamp = {"arch": ARCH, "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"),
+             "hipcc": (r.stdout or r.stderr).strip().splitlines()[:2],
+             "flags": {os.path.basename(s): _flags(s) for s in srcs},
+             "sources": source_digest(srcs),
+             "library_sha256": hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()}
+    with open(STAMP_PATH, "w") as f:
+        json.dump(stamp, f, indent=1)
 
 
 def main(argv=None) -> int:

@@ -520,7 +520,7 @@ def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits):
 
 
 @pytest.mark.parametrize("M", [1, 16, 17, 33, 64])
-@pytest.mark.parametrize("N,K", [(100, 128), (2304, 768), (1600, 1600), (6144, 4096)])
+@pytest.mark.parametrize("N,K", [(100, 128), (2304, 768), (1600, 1600), (6144, 4096), (16400, 256)])
 def test_skinny_shuffled_weights_match(M, N, K):
     """Decode GEMMs streaming the fragment-order weight copy (shuffle_weight):
     bf16 linear, fused-norm linear and W8A16 agree with the row-major path to
