@@ -279,6 +279,12 @@ def extra_keys(args, info):
                                      "micro_batch": 64, "microbatches": g["config"]["microbatches"],
                                      "prompt_len": 512, "decode_steps_timed": 32,
                                      "placement": "4 stages colocated on 1 GPU"}
+        # throughput point: 256 sequences per decode step (medium-M skinny GEMMs)
+        ga = gpt_bench.parse(["--gpus", "1", "--steps", "32", "--warmup", "4", "--batch", "256", "--prompt", "512",
+                              "--stages", "4", "--dtype", "bf16", "--prefill_iters", "2"])
+        g = gpt_bench.run(ga)
+        out["gpt2_4stage_b256_decode_tok_s"] = g["value"]
+        out["gpt2_4stage_b256_decode_ms_per_step"] = g["ms_per_step"]
     if args.precision == "fp32":
         import copy
         a = copy.copy(args)

@@ -528,7 +528,10 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                         const void* R, int ldr, int M, int N, int K, hipStream_t st, const void* Wsh) {
-  if (M <= 64) {  // decode-sized: weight-streaming skinny kernels (gemm_skinny.hip)
+  // decode-sized: the weight-streaming skinny kernels (gemm_skinny.hip); medium
+  // M (<= 256) too while the 128^2 tiles would not fill 3/4 of the CUs (same
+  // rule as ops/gemm.py skinny_rows)
+  if (M <= 64 || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192)) {
     dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh);
     return;
   }

@@ -348,6 +348,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 
 using namespace dnn;
 
+constexpr int SKINNY_MAX_M = 256;  // M > 64 only through the M split (medium-batch decode)
+
 // Per chunk a wave issues NT weight loads and MT activation loads (L2) for
 // NT x MT MFMAs.  The configuration table below is fitted to
 // bench/skinny_sweep.py on MI355X (profiles/r1_skinny_sweep.jsonl, weights
@@ -383,6 +385,18 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
   return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
                                                                        ldr, M, N, kbytes, KSV, colsum, eps, st, Wsh)
+#define CFG_MS(NTV, UV, PV, KSV)                                                                                 \
+  return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, UV, PV, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
+                                                                           R, ldr, M, N, kbytes, KSV, colsum, eps, st, \
+                                                                           Wsh)
+  // medium M (64, 256], decode of larger batches: always the M split, one
+  // 16-row tile per workgroup; the weight slice of a column tile is re-read
+  // from its XCD's L2 by the M tiles (the 128^2 GEMM would launch only a
+  // handful of tiles at these shapes)
+  if (M > 64) {
+    if (N <= 1024) CFG_MS(1, 4, false, 4);
+    CFG_MS(2, 2, false, 4);
+  }
   if (M <= 8) {
     // fragment-order weights at batch 1-8 only for the mid-size N (QKV): in the
     // Llama-3 8B fp8 decode graph 12.25 -> 10.33 us; on gate|up, O and down the
@@ -403,10 +417,6 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   // too few for 256 CUs: graph-timed sweep profiles/r1_skinny_sweep_ms.jsonl —
   // GPT-2 N=768: 5.8 -> 3.8 us (K=768), 15.9 -> 8.3 us (K=3072) at M=64;
   // GPT-2 XL W8 N=1600: 9.8 -> 7.0 / 28.5 -> 16.0 us; Llama W8 N=4096 at M=32.
-#define CFG_MS(NTV, UV, PV, KSV)                                                                                 \
-  return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, UV, PV, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
-                                                                           R, ldr, M, N, kbytes, KSV, colsum, eps, st, \
-                                                                           Wsh)
   if (!FP8 && Wsh != nullptr) {
     // fragment-order weights (M 17..64): graph-timed sweep profiles/r1_skinny_sweep_shuf_fit.jsonl,
     // every rule within 1.0-1.1x of the best config of its shapes (Llama-3 8B at M = 32,
@@ -441,13 +451,13 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
 #undef CFG
 }
 
-// bf16: K % 32 == 0 (64-B chunks), M <= 64.  fp8: K (bytes) % 64 == 0.
+// bf16: K % 32 == 0 (64-B chunks), M <= SKINNY_MAX_M (M > 64: M split).  fp8: K (bytes) % 64 == 0, M <= 64.
 extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw,
                                void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int K,
                                int act, int out_f32, int fp8, hipStream_t st, const void* Wsh) {
   const int eb = fp8 ? 1 : 2;
   const int kbytes = K * eb;
-  if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
+  if (M <= 0 || M > (fp8 ? 64 : SKINNY_MAX_M) || N <= 0 || kbytes % 64 != 0) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;  // packed gate|up groups of 8+8
   if (fp8 && (sa == nullptr || sw == nullptr)) return -1;
   const int la = lda * eb, lw = ldw * eb;
@@ -479,7 +489,7 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
                                     const void* R, int ldr, int M, int N, int K, int act, int norm,
                                     const float* colsum, float eps, hipStream_t st, const void* Wsh) {
   const int kbytes = K * 2;
-  if (M <= 0 || M > 64 || N <= 0 || kbytes % 64 != 0) return -1;
+  if (M <= 0 || M > SKINNY_MAX_M || N <= 0 || kbytes % 64 != 0) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
   if (norm == NORM_LN && colsum == nullptr) return -1;
   const int la = lda * 2, lw = ldw * 2;
@@ -502,7 +512,7 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
 extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                                   const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
                                   const float* colsum, float eps, hipStream_t st, const void* Wsh) {
-  if (M <= 0 || M > 64 || N <= 0 || K % 64 != 0 || ldw < K || sw == nullptr) return -1;
+  if (M <= 0 || M > SKINNY_MAX_M || N <= 0 || K % 64 != 0 || ldw < K || sw == nullptr) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
   if (norm == NORM_LN && colsum == nullptr) return -1;
   const int la = lda * 2;

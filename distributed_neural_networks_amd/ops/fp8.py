@@ -102,11 +102,11 @@ def set_fp8_tile(tile: int = 0) -> None:
 def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, norm: int = 0,
               colsum: Optional[torch.Tensor] = None, eps: float = 0.0) -> torch.Tensor:
-    """Weight-only fp8 GEMM for M <= 64: bf16 x (M, K) times e4m3 w, bf16 out.
+    """Weight-only fp8 GEMM for decode-sized M (<= 256): bf16 x (M, K) times e4m3 w, bf16 out.
     ``norm`` (1 RMS / 2 LN, with ``colsum`` for LN) fuses a folded pre-norm."""
     M, K = x.shape
     N, kp = w.q.shape
-    if M > 64 or (w.k and w.k != K) or kp < K or K % 64:
+    if M > 256 or (w.k and w.k != K) or kp < K or K % 64:
         raise ValueError(f"linear_w8: x {tuple(x.shape)} vs weight {tuple(w.q.shape)} (k={w.k})")
     if x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise TypeError("linear_w8: bf16 activations with a contiguous last dim")

@@ -13,13 +13,21 @@ import torch
 from ._lib import check, lib, ptr, stream_ptr
 
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_SILU_MUL = 0, 1, 2, 3
+SKINNY_MAX_M = 256
+
+
+def skinny_rows(M: int, N: int) -> bool:
+    """Decode-sized GEMM -> the weight-streaming skinny kernels: M <= 64, or
+    medium M (<= 256, M split into 16-row tiles) while 128^2 tiles would not
+    fill 3/4 of the CUs (same rule as gemm_bf16.hip launch_gemm)."""
+    return M <= 64 or (M <= SKINNY_MAX_M and -(-M // 128) * -(-N // 128) < 192)
 _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "silu_mul": ACT_SILU_MUL}
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` when M <= 64."""
+    """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` on the skinny path (``skinny_rows``)."""
     a = _ACTS[act] if not isinstance(act, int) else act
     x2 = x.reshape(-1, x.shape[-1]) if x.dim() != 2 else x
     M, K = x2.shape
@@ -128,10 +136,10 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
     N = f.w.shape[0]
     if (not w8 and f.w.shape[1] != K) or x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise ValueError(f"linear_norm: x {tuple(x.shape)} {x.dtype} vs w {tuple(f.w.shape)}")
-    if M > 64:
+    if not skinny_rows(M, N):
         from .transformer_ops import layernorm, layernorm_q8
         if std_buf is None or ones is None:
-            raise ValueError("linear_norm: M > 64 needs std_buf and ones")
+            raise ValueError("linear_norm: large M needs std_buf and ones")
         if w8 and q8 is not None and s8 is not None:
             # standardise + quantise in one pass: the e4m3 rows feed the W8A8 GEMM directly
             kp = f.w.q.shape[1]

@@ -35,7 +35,7 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import transformer_ops as T_
-from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up
+from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up, skinny_rows
 from .stages import StageCompute, StageOutput
 
 
@@ -207,7 +207,7 @@ class TransformerStage(StageCompute):
     def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None):
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
-            if x.shape[0] <= 64:  # decode: weight-only fp8 (bf16 activations, no quantise launch)
+            if skinny_rows(x.shape[0], w.q.shape[0]):  # decode: weight-only fp8 (bf16 activations, no quantise launch)
                 return linear_w8(x, w, b, act, residual, out)
             return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
         return linear(x, w, b, act, residual, out, w_shuf=w_shuf)

@@ -13,7 +13,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 768), (77, 200, 128), (4096, 512, 4096),
                                    (1, 768, 768), (7, 3072, 768), (16, 50257, 768), (300, 2304, 768),
-                                   (32, 4096, 14336), (64, 2304, 768), (40, 100, 128), (2, 28672, 4096)])
+                                   (32, 4096, 14336), (64, 2304, 768), (40, 100, 128), (2, 28672, 4096),
+                                   (128, 768, 768), (200, 2304, 768), (256, 3072, 768), (97, 768, 3072)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_gemm_bf16(M, N, K, act):
     from distributed_neural_networks_amd.ops.gemm import linear

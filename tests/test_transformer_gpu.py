@@ -334,7 +334,7 @@ def test_fp8_stage_runs(model, Tn):
     assert _rel(out.probs.view(2, Tn, -1).cpu(), ref) < 0.15
 
 
-@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("M", [1, 17, 64, 200])
 @pytest.mark.parametrize("norm,act", [(0, 0), (1, 0), (1, 3), (2, 0), (2, 2)])
 def test_linear_w8(M, norm, act):
     """Weight-only fp8 skinny GEMM (e4m3 weights converted in registers, bf16
@@ -412,7 +412,7 @@ def test_fp8_skinny_act_residual(M, act):
     assert _rel(y, ref + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100, 256, 300])
 @pytest.mark.parametrize("rms,act", [(True, "none"), (True, "silu_mul"), (False, "none"), (False, "gelu")])
 def test_linear_norm_fused(M, rms, act):
     """Pre-norm folded into the skinny GEMM (row stats from the streamed A
