@@ -57,11 +57,17 @@ def main():
         ga = s.get("GRBM_GUI_ACTIVE", 0)
         mfma = f"{s['SQ_VALU_MFMA_BUSY_CYCLES'] / (ga / 8 * 1024):.2f}" if ga and "SQ_VALU_MFMA_BUSY_CYCLES" in s else "-"
         clk = f"{ga / 8 / t / 1e9:.2f} GHz" if ga and t else "-"
+        # FETCH_SIZE is in KiB; its own pass's wall time (the pass holding FETCH_SIZE)
+        fetch = "-"
+        if "FETCH_SIZE" in s:
+            tf = [per_pass[f] for f in per_pass if any(r_ for r_ in [f] if "p2" in f)] or [t]
+            if tf and tf[0] > 0:
+                fetch = f"{s['FETCH_SIZE'] * 1024 / tf[0] / 1e12:.2f}"
         rows.append((k, mfma, ratio(k, "SQ_INSTS_VALU", "SQ_INSTS_MFMA"),
-                     ratio(k, "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", 100), clk))
+                     ratio(k, "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", 100), clk, fetch))
     print()
-    print("| kernel | MFMA busy / SIMD-cycle | VALU : MFMA | LDS conflict % | effective clock |")
-    print("|---|---|---|---|---|")
+    print("| kernel | MFMA busy / SIMD-cycle | VALU : MFMA | LDS conflict % | effective clock | HBM fetch TB/s (profiled) |")
+    print("|---|---|---|---|---|---|")
     for r in rows:
         print("| `" + r[0] + "` | " + " | ".join(r[1:]) + " |")
 
