@@ -89,8 +89,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
                            int rms, u64 st) {
     return dnn_layernorm_q8(CP(x), ldx, CFP(w), CFP(b), P(q), ldq, FP(sq), M, N, kpad, eps, rms, ST(st));
   });
-  m.def("embed_gpt2", [](u64 idx, u64 wte, u64 wpe, u64 out, int B, int T, int d, u64 pos, u64 st) {
-    return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), ST(st));
+  m.def("embed_gpt2", [](u64 idx, u64 wte, u64 wpe, u64 out, int B, int T, int d, u64 pos, int V, int Pn, u64 st) {
+    return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), V, Pn, ST(st));
   });
   m.def("qkv_split", [](u64 qkv, u64 q, u64 kc, u64 vc, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
                         u64 cos, u64 sin, int rope, u64 st) {

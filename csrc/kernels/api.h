@@ -41,7 +41,7 @@ int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, voi
 int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N, float eps,
                   int rms, hipStream_t st);
 int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d, const int* pos,
-                   hipStream_t st);
+                   int V, int P, hipStream_t st);
 int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
                   const int* pos, const float* cos, const float* sin, int rope, hipStream_t st);
 int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H, int Hkv,

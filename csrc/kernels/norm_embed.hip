@@ -165,18 +165,21 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__
 // out[r, :] = wte[idx[r], :] (+ wpe[pos[b] + t, :]) with r = b*T + t.
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ wte,
                                                     const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int B,
-                                                    int T, int d, const int* __restrict__ pos) {
+                                                    int T, int d, const int* __restrict__ pos, int V, int P) {
   const int chunks = d / 8;
   const long total = (long)B * T * chunks;
   for (long g = blockIdx.x * (long)blockDim.x + threadIdx.x; g < total; g += (long)gridDim.x * blockDim.x) {
     const int c = (int)(g % chunks);
     const long r = g / chunks;
     const int b = (int)(r / T), t = (int)(r % T);
-    const int tok = idx[r];
+    // ids and positions clamped to the tables: a bad id or a position past
+    // block_size reads a valid row (wrong but bounded) instead of faulting;
+    // the host rejects such runs at config load (cli.check_config_capacity)
+    const int tok = min(max(idx[r], 0), V - 1);
     const bf16x8 e = *reinterpret_cast<const bf16x8*>(wte + (size_t)tok * d + c * 8);
     uint4 o;
     if (wpe != nullptr) {
-      const int p = (pos != nullptr ? pos[b] : 0) + t;
+      const int p = min((pos != nullptr ? pos[b] : 0) + t, P - 1);
       const bf16x8 q = *reinterpret_cast<const bf16x8*>(wpe + (size_t)p * d + c * 8);
       uint32_t* op = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
@@ -212,13 +215,13 @@ extern "C" int dnn_layernorm(const void* x, int ldx, const float* w, const float
 }
 
 extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d,
-                              const int* pos, hipStream_t st) {
-  if (d % 8 != 0) return -1;
+                              const int* pos, int V, int P, hipStream_t st) {
+  if (d % 8 != 0 || V <= 0 || (wpe != nullptr && P <= 0)) return -1;
   const long total = (long)B * T * (d / 8);
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(embed_kernel, dim3(blocks), dim3(256), 0, st, idx, (const bf16_t*)wte, (const bf16_t*)wpe,
-                     (bf16_t*)out, B, T, d, pos);
+                     (bf16_t*)out, B, T, d, pos, V, P);
   return (int)hipGetLastError();
 }
 

@@ -37,8 +37,10 @@ int main() {
   expect_reject(dnn_gemm_bf16(p, 96, p, 96, p, 8, nullptr, nullptr, 0, 128, 128, 96, 0, 0, st), "gemm K%64");
   expect_reject(dnn_gemm_bf16(p, 64, p, 64, p, 8, nullptr, nullptr, 0, 0, 128, 64, 0, 0, st), "gemm M=0");
   expect_reject(dnn_gemm_set_tile(64), "gemm tile 64");
-  expect_reject(dnn_gemm_skinny(p, 64, nullptr, p, 64, nullptr, p, 8, nullptr, nullptr, 0, 65, 16, 64, 0, 0, 0, st),
-                "skinny M>64");
+  expect_reject(dnn_gemm_skinny(p, 64, nullptr, p, 64, nullptr, p, 8, nullptr, nullptr, 0, 257, 16, 64, 0, 0, 0, st),
+                "skinny M>256");
+  expect_reject(dnn_gemm_skinny(p, 64, f, p, 64, f, p, 8, nullptr, nullptr, 0, 65, 16, 64, 0, 0, 1, st),
+                "skinny fp8 M>64");
   expect_reject(dnn_gemm_skinny(p, 64, nullptr, p, 64, nullptr, p, 8, nullptr, nullptr, 0, 4, 16, 64, 0, 0, 1, st),
                 "skinny fp8 without scales");
   expect_reject(dnn_gemm_skinny(p, 48, nullptr, p, 48, nullptr, p, 8, nullptr, nullptr, 0, 4, 24, 48, 3, 0, 0, st),
@@ -61,7 +63,8 @@ int main() {
   // norms / embedding
   expect_reject(dnn_layernorm(p, 12, f, f, p, 12, 4, 12, 1e-5f, 0, st), "layernorm N%8");
   expect_reject(dnn_layernorm(p, 16384, f, f, p, 16384, 4, 16384, 1e-5f, 1, st), "layernorm N>8192");
-  expect_reject(dnn_embed_gpt2(ip, p, p, p, 1, 1, 12, ip, st), "embed d%8");
+  expect_reject(dnn_embed_gpt2(ip, p, p, p, 1, 1, 12, ip, 8, 8, st), "embed d%8");
+  expect_reject(dnn_embed_gpt2(ip, p, p, p, 1, 1, 16, ip, 0, 8, st), "embed empty vocab");
   // attention
   expect_reject(dnn_qkv_split(p, p, p, p, 1, 1, 4, 4, 24, 16, ip, nullptr, nullptr, 0, st), "qkv_split hd%16");
   expect_reject(dnn_qkv_split(p, p, p, p, 1, 1, 6, 4, 64, 16, ip, nullptr, nullptr, 0, st), "qkv_split H%Hkv");

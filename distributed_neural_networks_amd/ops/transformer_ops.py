@@ -66,7 +66,8 @@ def embed(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], out
     d = wte.shape[1]
     if out.numel() < B * T * d:
         raise ValueError("embed: output too small")
-    check(lib().embed_gpt2(ptr(idx), ptr(wte), ptr(wpe), ptr(out), B, T, d, ptr(pos), stream_ptr()), "embed")
+    check(lib().embed_gpt2(ptr(idx), ptr(wte), ptr(wpe), ptr(out), B, T, d, ptr(pos), wte.shape[0],
+                           0 if wpe is None else wpe.shape[0], stream_ptr()), "embed")
     return out
 
 
