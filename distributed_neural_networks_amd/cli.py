@@ -160,8 +160,14 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
         else:
             from .runtime.transformer import build_device_stage
             n_seq, n_pos = kv_needs(ctx, args) if args is not None else (8, 1024)
+            # activation buffers hold the largest single stage call: a whole
+            # request over gRPC, else one microbatch x (prefill chunk | prompt)
+            if pipe.transport == "grpc":
+                ntok = n_seq * n_pos
+            else:
+                ntok = pipe.micro_batch_size * (min(pipe.prefill_chunk, n_pos) if pipe.prefill_chunk > 0 else n_pos)
             st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
-                                    max_batch=n_seq, max_seq=n_pos,
+                                    max_batch=n_seq, max_seq=n_pos, max_tokens=ntok,
                                     temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed)
     else:
         st = TorchStage(pipe.model, sd, a, b, first, last, device,

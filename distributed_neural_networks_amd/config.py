@@ -12,7 +12,7 @@ Behavioural contract (reference ``node.py:222-290``, ``config.json:1-18``):
 * Additive optional fields (absent in the reference file, so it still loads):
   top level ``model``, ``dtype``, ``transport``, ``micro_batch_size``,
   ``num_microbatches``, ``seq_len``, ``decode_steps``, ``prompt_len``, ``temperature``, ``top_k``,
-  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``; per node
+  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``; per node
   ``layers: [start, end]`` (inclusive, as in
   ``partitions/gpt_model_parts.py:12``) and ``device``.
 
@@ -66,6 +66,7 @@ class PipelineConfig:
     seq_len: int = 64
     prompt_len: Optional[int] = None
     decode_steps: int = 0
+    prefill_chunk: int = 0                    # > 0: chunked prefill, this many prompt tokens per stage call
     temperature: float = 0.0                  # 0 = greedy; > 0 = sampling (last stage)
     top_k: int = 0                            # 0 = whole vocabulary
     seed: int = 0                             # sampling seed (counter-based RNG, reproducible)
@@ -176,6 +177,7 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         transport=transport, micro_batch_size=int(cfg.get("micro_batch_size", 1)),
         num_microbatches=int(cfg.get("num_microbatches", 1)), seq_len=int(cfg.get("seq_len", 64)),
         prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),
+        prefill_chunk=int(cfg.get("prefill_chunk", 0)),
         temperature=float(cfg.get("temperature", 0.0)), top_k=int(cfg.get("top_k", 0)), seed=int(cfg.get("seed", 0)),
         rpc_timeout_s=cfg.get("rpc_timeout_s"), health_timeout_s=float(cfg.get("health_timeout_s", 120.0)),
         comm_timeout_s=float(cfg.get("comm_timeout_s", 300.0)),

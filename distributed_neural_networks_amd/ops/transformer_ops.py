@@ -117,18 +117,25 @@ def flash_attn_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: t
     return out
 
 
-def decode_splits(S: int, B: int, Hkv: int) -> int:
+DEC_LDS_SCORES = 160 * 1024 // 4  # fp32 scores one decode-attention workgroup can hold in LDS
+
+
+def decode_splits(S: int, B: int, Hkv: int, G: int = 1) -> int:
     """Split-K factor for decode attention: one split once B*Hkv alone gives 2
     workgroups per CU; else enough workgroups for ~4 per CU (1024), at most one
     split per 256 keys of cache capacity.  Each split takes
     ``ceil(len/splits)`` of the *runtime* length, so short contexts stay
-    balanced; with one split the kernel writes the output itself (no combine)."""
+    balanced; with one split the kernel writes the output itself (no combine).
+    Long contexts: a split keeps its G x chunk scores in LDS (160 KiB), so the
+    split count never drops below ceil(S / floor(40960 / G)) (14 for a 128 K-token
+    Llama-3 cache, G = 4), whatever the batch."""
+    lds_min = max(1, -(-S // (DEC_LDS_SCORES // max(1, G))))  # ceil(S/splits) * G <= 40960
     if os.environ.get("DNN_DECODE_SPLITS"):  # A/B override
-        return max(1, int(os.environ["DNN_DECODE_SPLITS"]))
+        return max(lds_min, int(os.environ["DNN_DECODE_SPLITS"]))
     if B * Hkv >= 512:  # >= 2 workgroups per CU already: the combine pass costs more than it hides
-        return 1          # (GPT-2 B=64: 0.754 -> 0.703 ms/step, profiles/r1_decode_benches_v6.jsonl)
+        return lds_min    # (GPT-2 B=64: 0.754 -> 0.703 ms/step, profiles/r1_decode_benches_v6.jsonl)
     want = max(1, -(-1024 // max(1, B * Hkv)))
-    return max(1, min(want, -(-S // 256)))  # >= 256 keys per split: short contexts skip the combine pass
+    return max(lds_min, min(want, -(-S // 256)))  # >= 256 keys per split: short contexts skip the combine
 
 
 def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, H: int, Hkv: int,

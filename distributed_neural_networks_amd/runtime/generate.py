@@ -77,9 +77,9 @@ def _report(nid: str, toks: torch.Tensor, prefill_s: float, decode_s: float, n_s
     log("METRICS " + json.dumps(m))
 
 
-def _timed_generate(ring: DecodeRing, prompts, T: int, steps: int, dev):
+def _timed_generate(ring: DecodeRing, prompts, T: int, steps: int, dev, chunk: int = 0):
     t0 = time.perf_counter()
-    ring.prefill(prompts, T)
+    ring.prefill(prompts, T, chunk)
     if steps > 1:
         ring.capture()
     _sync(dev)
@@ -101,7 +101,7 @@ def run_generate_colocated(ctx, args, stages: List, device) -> int:
     M, B = pipe.num_microbatches, pipe.micro_batch_size
     ring = DecodeRing(stages, RingLinks(), 1, M, B)
     prompts = [prompt[m * B:(m + 1) * B] for m in range(M)]
-    pf, dec = _timed_generate(ring, prompts, T, steps, device)
+    pf, dec = _timed_generate(ring, prompts, T, steps, device, pipe.prefill_chunk)
     _report(ctx.node_id, ring.tokens(), pf, dec, n_seq, T, steps, M, 1)
     return 0
 
@@ -133,7 +133,7 @@ def run_generate_dist(ctx, args, stage, info, progress=None) -> int:
         links.nxt.send_header(KIND_DATA, B, T, steps)
     check_capacity([stage], *kv_capacity(pipe, T))
     ring = DecodeRing([stage], links, S, M, B, progress=progress)
-    pf, dec = _timed_generate(ring, prompts, T, steps, dev)
+    pf, dec = _timed_generate(ring, prompts, T, steps, dev, pipe.prefill_chunk)
     if r == 0:
         _report(ctx.node_id, ring.tokens(), pf, dec, B * M, T, steps, M, S)
     return 0

@@ -368,41 +368,53 @@ class DecodeRing:
             self.toks[m].append(self.cur[m].view(self.B).clone())
 
     # -- prefill ----------------------------------------------------------------
-    def prefill(self, prompts: Optional[Sequence[torch.Tensor]], T: int) -> None:
+    def prefill(self, prompts: Optional[Sequence[torch.Tensor]], T: int, chunk: int = 0) -> None:
         """Run the T-token prompts of all M microbatches (group 0 passes
-        ``prompts[m]`` (B, T) int; other groups pass None)."""
+        ``prompts[m]`` (B, T) int; other groups pass None).  ``chunk`` > 0
+        prefills in pieces of that many tokens (chunked prefill: activation
+        buffers and stage hops stay bounded for long prompts; each piece
+        attends to the cache written by the previous ones)."""
         B, d = self.B, self.d
+        C = T if chunk <= 0 else min(chunk, T)
+        pieces = [(t0, min(C, T - t0)) for t0 in range(0, T, C)]
         for m in range(self.M):
             self.pos[m].zero_()
             self.toks[m] = []
-        xin_pf = torch.empty((B * T, d), dtype=_act_dtype(self.stages[0]), device=self.dev) if not self.first else None
+        in_dt, out_dt = _act_dtype(self.stages[0]), _act_dtype(self.stages[-1])
+        xin_pf = torch.empty((B * C, d), dtype=in_dt, device=self.dev) if not self.first else None
         out_pf = None
         pf_work: List[object] = [None, None]
         if not self.last:
-            out_pf = [torch.empty((B * T, d), dtype=_act_dtype(self.stages[-1]), device=self.dev) for _ in range(2)]
+            out_pf = [torch.empty((B * C, d), dtype=out_dt, device=self.dev) for _ in range(2)]
+        n_sent = 0
         for m in range(self.M):
             if self.first:
-                x = prompts[m].to(device=self.dev, dtype=torch.int32).contiguous()
-            else:
-                self.links.prev.recv(xin_pf)
-                x = xin_pf
-            k = m % 2
-            if not self.last and pf_work[k] is not None:
-                pf_work[k].wait()
+                ids = prompts[m].to(device=self.dev, dtype=torch.int32).contiguous()
             self._out_ready(m)
-            with trace.span("prefill", "compute", mb=m):
-                y = self._run(x, m, T, out=(self.out[m] if self.last else out_pf[k]))
-            self.pos[m].add_(T)
-            if self.last:
-                if self.G == 1:
-                    self.cur[m].copy_(self.out[m].view(B, 1))
-                    if self.record:
-                        self.toks[m].append(self.out[m].clone())
+            for t0, Tc in pieces:
+                final = t0 + Tc == T
+                if self.first:
+                    x = ids[:, t0:t0 + Tc].contiguous()
                 else:
-                    self._send(m)
-            else:
-                pf_work[k] = self.links.nxt.isend(out_pf[k])
-            self.progress()
+                    x = xin_pf[:B * Tc]
+                    self.links.prev.recv(x)
+                k = n_sent % 2
+                if not self.last and pf_work[k] is not None:
+                    pf_work[k].wait()
+                with trace.span("prefill", "compute", mb=m, t0=t0):
+                    y = self._run(x, m, Tc, out=(self.out[m] if self.last else out_pf[k][:B * Tc]))
+                self.pos[m].add_(Tc)
+                if not self.last:
+                    pf_work[k] = self.links.nxt.isend(out_pf[k][:B * Tc])
+                    n_sent += 1
+                elif final:
+                    if self.G == 1:
+                        self.cur[m].copy_(self.out[m].view(B, 1))
+                        if self.record:
+                            self.toks[m].append(self.out[m].clone())
+                    else:
+                        self._send(m)
+                self.progress()
         for w in pf_work:
             if w is not None:
                 w.wait()
@@ -459,10 +471,10 @@ class DecodeRing:
                 self.sorder.waited(m)
         self.sorder.drained()
 
-    def generate(self, prompts, T: int, steps: int) -> Optional[torch.Tensor]:
+    def generate(self, prompts, T: int, steps: int, chunk: int = 0) -> Optional[torch.Tensor]:
         """Prefill + ``steps - 1`` decode rounds (``steps`` tokens per sequence).
         Group 0 returns (M*B, steps) int32 on the host; other groups None."""
-        self.prefill(prompts, T)
+        self.prefill(prompts, T, chunk)
         if steps > 1:
             self.capture()
         for _ in range(steps - 1):

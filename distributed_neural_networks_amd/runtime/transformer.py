@@ -190,7 +190,7 @@ class TransformerStage(StageCompute):
         self.buf_att = torch.empty((ntok, H * hd), dtype=bf, device=dev)
         self.buf_f = torch.empty((ntok, ffn), dtype=bf, device=dev)
         self.lens = torch.zeros((self.max_batch,), dtype=torch.int32, device=dev)
-        self.splits = T_.decode_splits(self.max_seq, self.max_batch, Hkv)
+        self.splits = T_.decode_splits(self.max_seq, self.max_batch, Hkv, H // Hkv)
         G = H // Hkv
         self.ws = torch.empty((self.max_batch * Hkv * self.splits * G * (hd + 2),), dtype=torch.float32, device=dev)
         self.q8 = self.s8 = None

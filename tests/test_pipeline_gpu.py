@@ -98,13 +98,15 @@ def test_cli_transformer_colocated_greedy(tmp_path, model, n_layers):
     _check_greedy(_golden_model(model, n_layers, 3), [prompt], toks)
 
 
-def test_cli_colocated_decode_microbatches_gpu(tmp_path):
+@pytest.mark.parametrize("chunk", [0, 5])
+def test_cli_colocated_decode_microbatches_gpu(tmp_path, chunk):
     """Colocated CLI decode with M = 3 microbatches of 2 sequences (one HIP
-    graph per microbatch): tokens per sequence vs golden, tokens/s reported."""
+    graph per microbatch), whole or chunked prefill: tokens per sequence vs
+    golden, tokens/s reported."""
     from distributed_neural_networks_amd.config import load_node
     from distributed_neural_networks_amd.runtime.generate import make_prompts
     cfg = _colocated_cfg(tmp_path, 2, "gpt2-tiny", "synthetic:4", prompt_len=12, decode_steps=6,
-                         micro_batch_size=2, num_microbatches=3)
+                         micro_batch_size=2, num_microbatches=3, prefill_chunk=chunk)
     r = _node(cfg)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     toks = json.loads(r.stdout.split("generated tokens:")[1].strip().splitlines()[0])

@@ -256,3 +256,18 @@ def test_killed_middle_stage_aborts_pipeline_gloo(tmp_path):
             if q.poll() is None:
                 q.kill()
                 q.wait()
+
+
+def test_cli_chunked_prefill_gloo(tmp_path):
+    """Chunked prefill (prefill_chunk = 6 of a 20-token prompt, 2 microbatches,
+    2 ranks): the chunks attend to the cache written by the earlier ones, so
+    the greedy tokens equal the full-prompt golden."""
+    cfg = _cfg(tmp_path, "gloo", 2, model="gpt2-tiny", weights="synthetic:8", prompt_len=20, decode_steps=4,
+               micro_batch_size=2, num_microbatches=2, prefill_chunk=6)
+    r0, outs, rcs = _run_all(cfg, 2)
+    assert r0.returncode == 0 and all(rc == 0 for rc in rcs), r0.stdout[-3000:] + "".join(o[-1500:] for o in outs)
+    toks = json.loads(r0.stdout.split("generated tokens:")[1].strip().splitlines()[0])
+    from distributed_neural_networks_amd.config import load_node
+    from distributed_neural_networks_amd.runtime.generate import make_prompts
+    prompts = make_prompts(load_node(str(cfg), "node1").pipeline, None).tolist()
+    assert toks == _golden_tokens("gpt2-tiny", 4, 8, prompts, 4)

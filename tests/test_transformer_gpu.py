@@ -133,7 +133,9 @@ def test_flash_attn_spike_rescale():
 
 
 @pytest.mark.parametrize("B,H,Hkv,hd,S,lens", [(2, 12, 12, 64, 1024, [1, 700]), (3, 32, 8, 128, 2048, [5, 1000, 2048]),
-                                               (1, 4, 2, 128, 300, [299]), (4, 25, 25, 64, 512, [17, 64, 65, 512])])
+                                               (1, 4, 2, 128, 300, [299]), (4, 25, 25, 64, 512, [17, 64, 65, 512]),
+                                               (1, 32, 8, 128, 131072, [120001]),   # long context: LDS-bound splits
+                                               (2, 12, 12, 64, 65536, [65536, 9000])])
 def test_attn_decode(B, H, Hkv, hd, S, lens):
     from distributed_neural_networks_amd.ops import transformer_ops as T
     torch.manual_seed(2)
@@ -141,7 +143,8 @@ def test_attn_decode(B, H, Hkv, hd, S, lens):
     kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
     vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
     L = torch.tensor(lens, device=DEV, dtype=torch.int32)
-    splits = T.decode_splits(S, B, Hkv)
+    splits = T.decode_splits(S, B, Hkv, H // Hkv)
+    assert -(-S // splits) * (H // Hkv) <= 40960
     ws = torch.empty(B * Hkv * splits * (H // Hkv) * (hd + 2), device=DEV)
     out = torch.empty(B, H * hd, device=DEV, dtype=torch.bfloat16)
     T.attn_decode(q, kc, vc, out, B, H, Hkv, hd, L, ws, splits)
