@@ -325,6 +325,7 @@ def main():
     extra = {}
     if N == 1 and not args.no_extra and info.device.type == "cuda":
         extra = extra_keys(args, info)
+    hop_kib = 4 * (4 if args.precision == "fp32" else 2)
     if info.rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
@@ -336,15 +337,65 @@ def main():
                        "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
                        "stage0_spare_cus": spare,
-                       "stage_cut": {1: "conv|fc (reference split, 8 KiB/img hop)",
-                                     2: "conv+fc1|fc2 (1 KiB/img hop)"}[args._cut]},
+                       "stage_cut": {1: f"conv|fc (reference split, {hop_kib} KiB/img hop)",
+                                     2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},
         }
         out.update(extra)
+    if N > 1 and not args.no_extra:
+        # GPT-2 small 4-stage decode ring across the GPUs (BASELINE config 3 at
+        # N = 4: one stage per GPU, tokens back to stage 0 over RCCL).  Guarded:
+        # a failure or hang here only drops these keys, never the headline line.
+        g = guarded_multi_gpu_gpt(args, info, out if info.rank == 0 else None)
+        if info.rank == 0 and g:
+            out.update(g)
+    if info.rank == 0:
         print(json.dumps(out), flush=True)
     if N > 1:
         from distributed_neural_networks_amd.parallel import comm
         comm.shutdown()
     return 0
+
+
+def guarded_multi_gpu_gpt(args, info, line, limit_s: float = 150.0):
+    """Run bench/gpt_bench.py's decode ring on all ranks under a timer: on a
+    hang every rank exits 0 after ``limit_s`` (rank 0 first prints the CIFAR
+    line it already has), on an exception the keys are skipped."""
+    import threading
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+    import gpt_bench
+
+    def bail():
+        if line is not None:
+            line["gpt2_4stage_error"] = f"decode ring exceeded {limit_s:.0f} s; skipped"
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+    timer = threading.Timer(limit_s, bail)
+    timer.daemon = True
+    timer.start()
+    try:
+        if info.device.type == "cuda":
+            ga = gpt_bench.parse(["--gpus", str(info.world), "--steps", "32", "--warmup", "4", "--batch", "64",
+                                  "--prompt", "512", "--stages", "4", "--dtype", "bf16", "--prefill_iters", "3"])
+        else:  # schedule-test mode (gloo): the same ring on the tiny model
+            ga = gpt_bench.parse(["--gpus", str(info.world), "--cpu", "--model", "gpt2-tiny", "--steps", "3",
+                                  "--warmup", "1", "--batch", "2", "--prompt", "8", "--stages", "4",
+                                  "--prefill_iters", "1"])
+        g = gpt_bench.run(ga)
+    except Exception as e:  # noqa: BLE001
+        g = None
+        if line is not None:
+            line["gpt2_4stage_error"] = f"{type(e).__name__}: {e}"[:200]
+    finally:
+        timer.cancel()
+    if g is None:
+        return {}
+    return {"gpt2_4stage_decode_tok_s": g["value"], "gpt2_4stage_decode_ms_per_step": g["ms_per_step"],
+            "gpt2_4stage_prefill_tok_s": g["prefill_tokens_per_s"],
+            "gpt2_4stage_config": dict(g["config"], dtype="bf16" if info.device.type == "cuda" else "fp32",
+                                       model=("gpt2 (124M, random init)" if info.device.type == "cuda"
+                                              else "gpt2-tiny (schedule test)"),
+                                       placement=f"{g['config']['gpu_groups']} GPU groups x "
+                                                 f"{g['config']['replicas']} replicas, decode ring over RCCL")}
 
 
 if __name__ == "__main__":

@@ -213,6 +213,8 @@ def test_bench_distributed_schedule_cpu(placement, n):
     assert d["n_gpus"] == n and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
     assert d["dtype"] == "fp32" and d["scaling"] == "weak"
     assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
+    assert d["gpt2_4stage_decode_tok_s"] > 0 and "gpt2_4stage_error" not in d
+    assert d["gpt2_4stage_config"]["gpu_groups"] == min(n, 4)
     if placement == "linear":
         from distributed_neural_networks_amd.parallel.partition import linear_plan
         plan = linear_plan(n, "fp32")
