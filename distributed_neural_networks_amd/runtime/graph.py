@@ -26,7 +26,9 @@ class GraphedStep:
             for _ in range(warmup):
                 self.result = fn()
             s.synchronize()
-            with torch.cuda.graph(self.graph, stream=s, pool=pool):
+            # thread-local capture: ProcessGroupNCCL's watchdog thread keeps
+            # polling its events while a multi-GPU rank captures its decode step
+            with torch.cuda.graph(self.graph, stream=s, pool=pool, capture_error_mode="thread_local"):
                 self.result = fn()
         torch.cuda.current_stream(self.device).wait_stream(s)
 
