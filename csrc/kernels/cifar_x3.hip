@@ -350,6 +350,7 @@ __device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, in
 // A goes to registers one k-step ahead; a variant that moved A by DMA into a
 // 32 KiB fp32 staging area two k-steps ahead measured 5 % slower (A latency is
 // not the limiter; profiles/r2_cifar_fc1_fused_ab.jsonl) and was dropped.
+template <int MID>
 __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __restrict__ A, int lda,
                                                               const bf16_t* __restrict__ Wh,
                                                               const bf16_t* __restrict__ Wl, int ldw,
@@ -424,8 +425,8 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
   for (int t = 0; t < nk; ++t) {
     const int u = t & 1;
     if (t + 1 < nk) {
-      load_a(t + 1);
-      stage_w(u ^ 1, t + 1);
+      if (MID < 2) load_a(t + 1);
+      if (MID < 3) stage_w(u ^ 1, t + 1);
     }
     const char* ah_p = plane(u, 0);
     const char* al_p = plane(u, 1);
@@ -454,11 +455,18 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], a, 0, 0, 0);
         }
+      if (MID == 1 && h == 0 && t + 1 < nk) {
+        // split + store the next A tile between the MFMA halves: its VALU and
+        // ds_writes can issue in the second half's MFMA gaps
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_a(u ^ 1);
+      }
     }
-    if (t + 1 < nk) {
+    if (MID == 0 && t + 1 < nk) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       store_a(u ^ 1);
     }
+    if (MID == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // raw barrier (lgkmcnt for this step's LDS writes; the DMAs were waited
     // above): 6 % faster than __syncthreads here
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -576,13 +584,21 @@ extern "C" int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, 
   return (int)hipGetLastError();
 }
 
+static int g_fc1_mid = 1;
+extern "C" int dnn_cifar_fc1_x3_variant(int v) {
+  g_fc1_mid = v;
+  return 0;
+}
+
 extern "C" int dnn_cifar_fc1_x3(const float* A, int lda, const void* Wh, const void* Wl, int ldw, const float* bias,
                                 float* C, int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
   if (N % F1_T != 0 || K % F1_K != 0 || lda % 4 != 0 || ldw % 8 != 0 || ldc % 4 != 0) return -1;
   const int blocks = ((M + F1_T - 1) / F1_T) * (N / F1_T);
-  hipLaunchKernelGGL(cifar_fc1_x3_kernel, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
-                     (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
+#define F1V(v) if (g_fc1_mid == v) hipLaunchKernelGGL(cifar_fc1_x3_kernel<v>, dim3(blocks), dim3(512), 0, st, A, lda, \
+                       (const bf16_t*)Wh, (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
+  F1V(0) F1V(1) F1V(2) F1V(3)
+#undef F1V
   return (int)hipGetLastError();
 }
 
