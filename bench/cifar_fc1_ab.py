@@ -31,26 +31,9 @@ def main():
         check(lib().cifar_fc1_x3(ptr(h), 4096, ptr(w.w_fc1h), ptr(w.w_fc1l), 4096, ptr(w.b_fc1), ptr(out_b), 512,
                                  B, 512, 4096, stream_ptr()), "fc1_x3")
 
-    def b_end():
-        lib().cifar_fc1_x3_variant(0)
-        b()
-
-    def b_mid():
-        lib().cifar_fc1_x3_variant(1)
-        b()
-
-    def b_noa():
-        lib().cifar_fc1_x3_variant(2)
-        b()
-
-    def b_nold():
-        lib().cifar_fc1_x3_variant(3)
-        b()
-
     res = {"B": B}
     outs = {}
-    for name, fn in (("split3_concat_gemm", a), ("fused_fc1_x3", b_end), ("fused_fc1_x3_mid", b_mid),
-                     ("probe_no_A_loads", b_noa), ("probe_no_loads", b_nold)):
+    for name, fn in (("split3_concat_gemm", a), ("fused_fc1_x3", b)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -64,7 +47,6 @@ def main():
         res[name + "_ms"] = round(ms, 4)
         res[name + "_pflops"] = round(3 * 2 * B * 512 * 4096 / ms / 1e12, 3)
         outs[name] = (out_a if fn is a else out_b).clone()
-    res["max_abs_diff_mid"] = (outs["split3_concat_gemm"] - outs["fused_fc1_x3_mid"]).abs().max().item()
     res["max_abs_diff"] = (outs["split3_concat_gemm"] - outs["fused_fc1_x3"]).abs().max().item()
     print(json.dumps(res), flush=True)
 

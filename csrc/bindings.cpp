@@ -71,7 +71,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("cifar_split3", [](u64 a, int lda, u64 o, int ldo, int M, int K, u64 st) {
     return dnn_cifar_split3(CFP(a), lda, P(o), ldo, M, K, ST(st));
   });
-  m.def("cifar_fc1_x3_variant", [](int v) { return dnn_cifar_fc1_x3_variant(v); });
   m.def("cifar_fc1_x3", [](u64 a, int lda, u64 wh, u64 wl, int ldw, u64 bias, u64 c, int ldc, int M, int N, int K,
                            u64 st) {
     return dnn_cifar_fc1_x3(CFP(a), lda, CP(wh), CP(wl), ldw, CFP(bias), FP(c), ldc, M, N, K, ST(st));

@@ -32,6 +32,8 @@
 //    W' = [W_hi | W_lo | W_hi]) when the 256^2 tiles cannot fill the chip.
 //  * cifar_head_tail_x3_kernel: fc2 (512->10) + bias + softmax + per-row argmax
 //    on fp32 hidden rows, 3-term split on mfma_f32_16x16x32_bf16.
+#include <type_traits>
+
 #include "gemm_epilogue.h"
 
 namespace dnn {
@@ -347,10 +349,11 @@ __device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, in
   tn = r / gm;
 }
 
-// A goes to registers one k-step ahead; a variant that moved A by DMA into a
-// 32 KiB fp32 staging area two k-steps ahead measured 5 % slower (A latency is
-// not the limiter; profiles/r2_cifar_fc1_fused_ab.jsonl) and was dropped.
-template <int MID>
+// A goes to registers one k-step ahead.  Measured alternatives, dropped: A by
+// DMA into a 32 KiB fp32 staging area two k-steps ahead (5 % slower), the
+// split+store between the two MFMA halves (flat).  Probes
+// (profiles/r2_cifar_fc1_probes.jsonl): without the A stream the kernel runs
+// 0.51 ms, without any load 0.45 ms (1.8 PF/s), with both 0.80 ms.
 __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __restrict__ A, int lda,
                                                               const bf16_t* __restrict__ Wh,
                                                               const bf16_t* __restrict__ Wl, int ldw,
@@ -367,29 +370,33 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
   auto plane = [&](int u, int p) { return smem + (u * 4 + p) * F1_PLANE; };  // p: 0 A_hi, 1 A_lo, 2 W_hi, 3 W_lo
 
   // A: 2 chunks (8 fp32 each) per thread; chunk q = tid + 512 i -> row q >> 2, k-chunk q & 3
-  float4 ar[2][2];
+  // A: 2 chunks (8 fp32 each) per thread; chunk q = tid + 512 i -> row q >> 2, k-chunk q & 3.
+  // (A second register set prefetching A two steps ahead spills at 2 waves/SIMD.)
+  float4 ar[1][2][2];  // [set][i][half]
   auto a_src = [&](int t, int i) {
     const int q = tid + 512 * i, r = q >> 2, c = q & 3;
     const int row = min(m0 + r, M - 1);
     return A + (size_t)row * lda + t * F1_K + c * 8;
   };
-  auto load_a = [&](int t) {
+  auto load_a = [&](int t, auto scst) {
+    constexpr int S = decltype(scst)::value;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const float* p = a_src(t, i);
-      ar[i][0] = *reinterpret_cast<const float4*>(p);
-      ar[i][1] = *reinterpret_cast<const float4*>(p + 4);
+      ar[S][i][0] = *reinterpret_cast<const float4*>(p);
+      ar[S][i][1] = *reinterpret_cast<const float4*>(p + 4);
     }
   };
-  auto store_a = [&](int u) {
+  auto store_a = [&](int u, auto scst) {
+    constexpr int S = decltype(scst)::value;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + 512 * i, r = q >> 2, c = q & 3;
       uint4 hi, lo;
-      split2(ar[i][0].x, ar[i][0].y, hi.x, lo.x);
-      split2(ar[i][0].z, ar[i][0].w, hi.y, lo.y);
-      split2(ar[i][1].x, ar[i][1].y, hi.z, lo.z);
-      split2(ar[i][1].z, ar[i][1].w, hi.w, lo.w);
+      split2(ar[S][i][0].x, ar[S][i][0].y, hi.x, lo.x);
+      split2(ar[S][i][0].z, ar[S][i][0].w, hi.y, lo.y);
+      split2(ar[S][i][1].x, ar[S][i][1].y, hi.z, lo.z);
+      split2(ar[S][i][1].z, ar[S][i][1].w, hi.w, lo.w);
       const int o = r * 64 + ((c ^ f1_swz(r)) << 4);
       *reinterpret_cast<uint4*>(plane(u, 0) + o) = hi;
       *reinterpret_cast<uint4*>(plane(u, 1) + o) = lo;
@@ -415,19 +422,15 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_a(0);
+  using I0 = std::integral_constant<int, 0>;
+  load_a(0, I0{});
   stage_w(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  store_a(0);
+  store_a(0, I0{});
   __syncthreads();
 
   const int fr = lane & 15, fc = lane >> 4;
-  for (int t = 0; t < nk; ++t) {
-    const int u = t & 1;
-    if (t + 1 < nk) {
-      if (MID < 2) load_a(t + 1);
-      if (MID < 3) stage_w(u ^ 1, t + 1);
-    }
+  auto compute = [&](int u) {
     const char* ah_p = plane(u, 0);
     const char* al_p = plane(u, 1);
     const char* bh_p = plane(u, 2);
@@ -455,24 +458,28 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], a, 0, 0, 0);
         }
-      if (MID == 1 && h == 0 && t + 1 < nk) {
-        // split + store the next A tile between the MFMA halves: its VALU and
-        // ds_writes can issue in the second half's MFMA gaps
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        store_a(u ^ 1);
-      }
     }
-    if (MID == 0 && t + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store_a(u ^ 1);
-    }
-    if (MID == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // raw barrier (lgkmcnt for this step's LDS writes; the DMAs were waited
-    // above): 6 % faster than __syncthreads here
+  };
+  // raw barrier (lgkmcnt for this step's LDS writes; the DMAs were waited
+  // above): 6 % faster than __syncthreads here
+  auto barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int t = 0; t < nk; ++t) {
+    const int u = t & 1;
+    if (t + 1 < nk) {
+      load_a(t + 1, I0{});
+      stage_w(u ^ 1, t + 1);
+    }
+    compute(u);
+    if (t + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_a(u ^ 1, I0{});
+    }
+    barrier();
   }
 
   // epilogue (transposed accumulators): row m0 + wr*128 + i*16 + (lane & 15), cols n..n+3
@@ -584,21 +591,13 @@ extern "C" int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, 
   return (int)hipGetLastError();
 }
 
-static int g_fc1_mid = 1;
-extern "C" int dnn_cifar_fc1_x3_variant(int v) {
-  g_fc1_mid = v;
-  return 0;
-}
-
 extern "C" int dnn_cifar_fc1_x3(const float* A, int lda, const void* Wh, const void* Wl, int ldw, const float* bias,
                                 float* C, int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
   if (N % F1_T != 0 || K % F1_K != 0 || lda % 4 != 0 || ldw % 8 != 0 || ldc % 4 != 0) return -1;
   const int blocks = ((M + F1_T - 1) / F1_T) * (N / F1_T);
-#define F1V(v) if (g_fc1_mid == v) hipLaunchKernelGGL(cifar_fc1_x3_kernel<v>, dim3(blocks), dim3(512), 0, st, A, lda, \
-                       (const bf16_t*)Wh, (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
-  F1V(0) F1V(1) F1V(2) F1V(3)
-#undef F1V
+  hipLaunchKernelGGL(cifar_fc1_x3_kernel, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
+                     (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
   return (int)hipGetLastError();
 }
 
