@@ -351,7 +351,8 @@ __device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, in
 
 // A goes to registers one k-step ahead.  Measured alternatives, dropped: A by
 // DMA into a 32 KiB fp32 staging area two k-steps ahead (5 % slower), the
-// split+store between the two MFMA halves (flat).  Probes
+// split+store between the two MFMA halves (flat), a second register set for A
+// two k-steps ahead once the loads were coalesced (flat, 6 spilled VGPRs).  Probes
 // (profiles/r2_cifar_fc1_probes.jsonl): without the A stream the kernel runs
 // 0.51 ms, without any load 0.45 ms (1.8 PF/s), with both 0.80 ms.
 __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __restrict__ A, int lda,
@@ -370,36 +371,29 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
   auto plane = [&](int u, int p) { return smem + (u * 4 + p) * F1_PLANE; };  // p: 0 A_hi, 1 A_lo, 2 W_hi, 3 W_lo
 
   // A: 2 chunks (8 fp32 each) per thread; chunk q = tid + 512 i -> row q >> 2, k-chunk q & 3
-  // A: 2 chunks (8 fp32 each) per thread; chunk q = tid + 512 i -> row q >> 2, k-chunk q & 3.
-  // (A second register set prefetching A two steps ahead spills at 2 waves/SIMD.)
-  float4 ar[1][2][2];  // [set][i][half]
-  auto a_src = [&](int t, int i) {
-    const int q = tid + 512 * i, r = q >> 2, c = q & 3;
-    const int row = min(m0 + r, M - 1);
-    return A + (size_t)row * lda + t * F1_K + c * 8;
-  };
-  auto load_a = [&](int t, auto scst) {
-    constexpr int S = decltype(scst)::value;
+  // A: 4 pieces of 16 B per thread; piece k: row (tid >> 3) + 64 k, floats
+  // 4 (tid & 7) .. +3, so every wave load instruction reads 8 whole 128-B row
+  // segments and the split halves land as ds_write_b64 into half of a 16-B LDS
+  // chunk.  (The first mapping, 32 contiguous bytes per lane in two loads,
+  // touched every 128-B line twice per wave: 0.85 -> 0.68 ms.)
+  float4 ar[4];
+  auto load_a = [&](int t, auto) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float* p = a_src(t, i);
-      ar[S][i][0] = *reinterpret_cast<const float4*>(p);
-      ar[S][i][1] = *reinterpret_cast<const float4*>(p + 4);
+    for (int k = 0; k < 4; ++k) {
+      const int row = min(m0 + (tid >> 3) + 64 * k, M - 1);
+      ar[k] = *reinterpret_cast<const float4*>(A + (size_t)row * lda + t * F1_K + (tid & 7) * 4);
     }
   };
-  auto store_a = [&](int u, auto scst) {
-    constexpr int S = decltype(scst)::value;
+  auto store_a = [&](int u, auto) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + 512 * i, r = q >> 2, c = q & 3;
-      uint4 hi, lo;
-      split2(ar[S][i][0].x, ar[S][i][0].y, hi.x, lo.x);
-      split2(ar[S][i][0].z, ar[S][i][0].w, hi.y, lo.y);
-      split2(ar[S][i][1].x, ar[S][i][1].y, hi.z, lo.z);
-      split2(ar[S][i][1].z, ar[S][i][1].w, hi.w, lo.w);
-      const int o = r * 64 + ((c ^ f1_swz(r)) << 4);
-      *reinterpret_cast<uint4*>(plane(u, 0) + o) = hi;
-      *reinterpret_cast<uint4*>(plane(u, 1) + o) = lo;
+    for (int k = 0; k < 4; ++k) {
+      const int r = (tid >> 3) + 64 * k, c = (tid & 7) >> 1, half = tid & 1;
+      uint2 hi, lo;
+      split2(ar[k].x, ar[k].y, hi.x, lo.x);
+      split2(ar[k].z, ar[k].w, hi.y, lo.y);
+      const int o = r * 64 + ((c ^ f1_swz(r)) << 4) + half * 8;
+      *reinterpret_cast<uint2*>(plane(u, 0) + o) = hi;
+      *reinterpret_cast<uint2*>(plane(u, 1) + o) = lo;
     }
   };
   // W: per plane 16 pieces of 16 rows (1 KiB per wave instruction), 2 per wave
