@@ -166,6 +166,17 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         v = cfg.get(key, 1)
         if not isinstance(v, int) or v < 1:
             raise ConfigError(f"ERROR: '{key}' must be a positive integer, got {v!r}")
+    for key in ("prefill_chunk", "decode_steps", "top_k", "seed"):
+        v = cfg.get(key, 0)
+        if not isinstance(v, int) or isinstance(v, bool) or v < 0:
+            raise ConfigError(f"ERROR: '{key}' must be a non-negative integer, got {v!r}")
+    for key in ("heartbeat_timeout_s", "stall_timeout_s", "health_timeout_s", "comm_timeout_s", "rpc_timeout_s"):
+        v = cfg.get(key)
+        if v is not None and (not isinstance(v, (int, float)) or isinstance(v, bool) or v <= 0):
+            raise ConfigError(f"ERROR: '{key}' must be a positive number of seconds, got {v!r}")
+    t = cfg.get("temperature", 0.0)
+    if not isinstance(t, (int, float)) or t < 0:
+        raise ConfigError(f"ERROR: 'temperature' must be >= 0, got {t!r}")
     ret = cfg.get("return_to_node_id")
     if ret is not None and transport in ("rccl", "gloo"):
         rn = next((n for n in nodes if n.id == ret), None)

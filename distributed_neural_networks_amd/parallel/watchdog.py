@@ -61,6 +61,13 @@ class Watchdog:
         self._thread: Optional[threading.Thread] = None
         self._store = None
         self.aborted: Optional[str] = None
+        self._exited = threading.Lock()
+
+    def _exit(self) -> None:
+        # abort() from the schedule and the thread's own poll can both fire
+        if self._exited.acquire(blocking=False):
+            self._stop.set()
+            self.exit_fn(EXIT_ABORT)
 
     # -- called from the schedule (cheap) -----------------------------------
     def beat(self) -> None:
@@ -123,7 +130,7 @@ class Watchdog:
             self._store.set(f"{PREFIX}abort", f"rank {self.rank}: {reason}")
         except Exception:  # noqa: BLE001
             pass
-        self.exit_fn(EXIT_ABORT)
+        self._exit()
 
     # -- the thread --------------------------------------------------------------
     def _loop(self) -> None:
@@ -140,7 +147,7 @@ class Watchdog:
                     msg = st.get(f"{PREFIX}abort").decode()
                     _log(f"!!! {self.tag} peer reported a pipeline failure ({msg}); exiting (exit {EXIT_ABORT})")
                     self.aborted = msg
-                    self.exit_fn(EXIT_ABORT)
+                    self._exit()
                     return
                 for p in peers:
                     if done[p]:

@@ -92,3 +92,24 @@ def test_repo_configs_parse():
         d = json.load(open(f))
         for n in d["nodes"]:
             resolve_node(d, n["id"], f)
+
+
+@pytest.mark.parametrize("key,val", [("micro_batch_size", 0), ("num_microbatches", "4"), ("prefill_chunk", -1),
+                                     ("decode_steps", 1.5), ("heartbeat_timeout_s", 0), ("stall_timeout_s", "x"),
+                                     ("temperature", -0.1), ("top_k", True)])
+def test_extension_field_validation(key, val):
+    c = json.loads(json.dumps(REF))
+    c[key] = val
+    with pytest.raises(ConfigError, match=key):
+        resolve_node(c, "node1")
+
+
+def test_extension_field_defaults_and_values():
+    c = json.loads(json.dumps(REF))
+    assert resolve_node(c, "node1").pipeline.heartbeat_timeout_s == 15.0
+    c.update(prefill_chunk=128, heartbeat_timeout_s=2.5, stall_timeout_s=30, transport="gloo")
+    p = resolve_node(c, "node1").pipeline
+    assert (p.prefill_chunk, p.heartbeat_timeout_s, p.stall_timeout_s) == (128, 2.5, 30.0)
+    c["return_to_node_id"] = "node7"
+    with pytest.raises(ConfigError, match="return_to_node_id"):
+        resolve_node(c, "node1")
