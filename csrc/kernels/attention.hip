@@ -18,7 +18,25 @@
 // XOR-swizzled so the A-fragment ds_read_b128 reads are conflict-free.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dnn {
+
+// Phase timestamps of decode-attention block (0,0), thread 0: only in the
+// bench-only probe build (-DDNN_DEC_PROBE, bench/attn_probe.py).
+#ifdef DNN_DEC_PROBE
+__device__ unsigned long long dec_probe_ts[32];
+#define DEC_PROBE(i, dep)                                                             \
+  do {                                                                                \
+    asm volatile("" ::"v"(dep));                                                      \
+    if (threadIdx.x == 0 && (blockIdx.x | blockIdx.y) == 0) {                         \
+      dec_probe_ts[i] = __builtin_amdgcn_s_memrealtime();                             \
+      dec_probe_ts[16 + i] = __builtin_amdgcn_s_memtime();                             \
+    }                                                                                 \
+  } while (0)
+#else
+#define DEC_PROBE(i, dep) do { } while (0)
+#endif
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -296,29 +314,35 @@ constexpr int DEC_U = 8;  // key/value rows in flight per thread
 static_assert(DEC_U % 2 == 0, "P.V folds key pairs");
 
 // 8 consecutive head-dim elements [8*sub, 8*sub+8) of one head row, RoPE'd
-// (rotate-half: element i pairs with i +- hd/2) when cosT != nullptr, and
+// (rotate-half: element i pairs with i +- hd/2) when ROPE, and
 // rounded to bf16 exactly as qkv_split stores them.
-template <int HD>
+template <int HD, bool ROPE>
 __device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int sub, const float* __restrict__ cosT,
                                            const float* __restrict__ sinT, int p, float out[8]) {
+  // branch-free (ROPE is compile-time): every load of a caller's unrolled loop
+  // sits in one basic block, so the scheduler issues them all before the first
+  // wait instead of one dependent round trip per head
   const bf16x8 x = *reinterpret_cast<const bf16x8*>(row + sub * 8);
-  if (cosT == nullptr) {
+  if constexpr (!ROPE) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = bf2f_s(x[j]);
-    return;
-  }
-  constexpr int HALFC = HD / 16;  // 16-B chunks per half row
-  const bool lo = sub < HALFC;
-  const int psub = lo ? sub + HALFC : sub - HALFC;
-  const bf16x8 y = *reinterpret_cast<const bf16x8*>(row + psub * 8);
-  const int i0 = (lo ? sub : psub) * 8;
-  const float* cr = cosT + (size_t)p * (HD / 2) + i0;
-  const float* sr = sinT + (size_t)p * (HD / 2) + i0;
+  } else {
+    constexpr int HALFC = HD / 16;  // 16-B chunks per half row
+    const bool lo = sub < HALFC;
+    const int psub = lo ? sub + HALFC : sub - HALFC;
+    const bf16x8 y = *reinterpret_cast<const bf16x8*>(row + psub * 8);
+    const int i0 = (lo ? sub : psub) * 8;
+    const float4* cr = reinterpret_cast<const float4*>(cosT + (size_t)p * (HD / 2) + i0);
+    const float4* sr = reinterpret_cast<const float4*>(sinT + (size_t)p * (HD / 2) + i0);
+    const float4 c0 = cr[0], c1 = cr[1], s0 = sr[0], s1 = sr[1];
+    const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float a = bf2f_s(x[j]), c = bf2f_s(y[j]);
-    const float r = lo ? a * cr[j] - c * sr[j] : a * cr[j] + c * sr[j];
-    out[j] = bf2f(f2bf(r));
+    for (int j = 0; j < 8; ++j) {  // same expression as qkv_split (cache rows must match bit for bit)
+      const float a = bf2f_s(x[j]), c = bf2f_s(y[j]);
+      const float r = lo ? a * cv[j] - c * sv[j] : a * cv[j] + c * sv[j];
+      out[j] = bf2f(f2bf(r));
+    }
   }
 }
 
@@ -328,23 +352,36 @@ __device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int s
 // cache; its own scores use the register copy, so no other split touches that
 // row and there is no qkv_split launch.  Otherwise q is head-major (B,H,hd)
 // and lens[b] keys are cached.
-template <int HD, int G, bool FUSED, bool NT>
+// MF: scores on MFMA.  The LDS-score layout (LPK lanes per key, a 4-step DPP
+// row reduction per key and head) costs ~20 VALU ops per 4 keys and head; with
+// one wave per SIMD (small grids: Llama-3 batch 1 has 8 workgroups) nothing
+// hides that and the score loop, not memory, set the kernel time (~1.2 us per
+// 128 keys, profiles/r2_attn_decode_phase_probe.jsonl).  With MF a wave
+// computes S^T for a tile of 16 keys x 16 query-head columns (G used) as
+// HD/32 v_mfma_f32_16x16x32_bf16: lane l feeds key row l&15 (A, straight from
+// the cache) and head l&15 (B = q^T, RoPE'd once); C lands as 4 keys x 1 head
+// per lane.  Softmax, P.V and the reduction are unchanged.
+template <int HD, int G, int FM, bool NT, bool MF = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
                                                           bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                           float* __restrict__ ws, int H, int Hkv, int S,
                                                           const int* __restrict__ lens, const float* __restrict__ cosT,
                                                           const float* __restrict__ sinT, float scale_log2,
                                                           int chunk_cap, bf16_t* __restrict__ o_direct) {
+  constexpr bool FUSED = FM != 0;  // FM: 0 = q head-major + cached keys, 1 = fused QKV rows, 2 = fused + RoPE
+  constexpr bool ROPE = FM == 2;
   constexpr int LPK = HD / 8;           // lanes per key row (16 B each)
   constexpr int GPB = 256 / LPK;        // key groups per block
   extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk_cap] scores, then reduction scratch
   const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
+  DEC_PROBE(0, 0);
   const int b = bk / Hkv, kvh = bk % Hkv;
   const int p_new = FUSED ? lens[b] : 0;  // FUSED: lens = positions already cached
   const int len = FUSED ? min(p_new + 1, S) : min(lens[b], S);  // never read past the cache capacity
   // splits share the *runtime* length evenly (one captured graph serves every step)
   const int chunk = (len + NS - 1) / NS;
   const int k0 = split * chunk, k1 = min(len, k0 + chunk);
+  DEC_PROBE(1, k1);
   const int tid = threadIdx.x, sub = tid % LPK, grp = tid / LPK;
   float* wsp = ws + ((size_t)bk * NS + split) * G * (HD + 2);
   if (k0 >= k1) {
@@ -363,25 +400,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   if constexpr (FUSED) {
     const bf16_t* row = q + (size_t)b * ldq;
     const int pr = min(p_new, S - 1);  // RoPE table row (overflow is dropped, never read out of bounds)
+    if constexpr (!MF) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) load_head8<HD>(row + (kvh * G + g) * HD, sub, cosT, sinT, pr, qv[g]);
-    if (own_new) {
-      load_head8<HD>(row + (H + kvh) * HD, sub, cosT, sinT, pr, nk);
-      load_head8<HD>(row + (H + Hkv + kvh) * HD, sub, nullptr, nullptr, 0, nv);
-      if (grp == 0) {
-        uint4 wk, wv;
-        uint32_t* pk = reinterpret_cast<uint32_t*>(&wk);
-        uint32_t* pv = reinterpret_cast<uint32_t*>(&wv);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pk[j] = pack2bf(nk[2 * j], nk[2 * j + 1]);
-          pv[j] = pack2bf(nv[2 * j], nv[2 * j + 1]);
-        }
-        *reinterpret_cast<uint4*>(kb + (size_t)p_new * HD + sub * 8) = wk;
-        *reinterpret_cast<uint4*>(vb + (size_t)p_new * HD + sub * 8) = wv;
-      }
+      for (int g = 0; g < G; ++g) load_head8<HD, ROPE>(row + (kvh * G + g) * HD, sub, cosT, sinT, pr, qv[g]);
     }
-  } else {
+    // new key / value: loaded unconditionally (used only when own_new), no branch
+    load_head8<HD, ROPE>(row + (H + kvh) * HD, sub, cosT, sinT, pr, nk);
+    load_head8<HD, false>(row + (H + Hkv + kvh) * HD, sub, nullptr, nullptr, 0, nv);
+  } else if constexpr (!MF) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
@@ -393,10 +419,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   // q and the new key are bf16-exact (rounded after RoPE): pack them into bf16
   // pairs so a score is 4 v_dot2_f32_bf16 per lane instead of 8 converts + 8 FMAs.
   uint32_t qp[G][4], nkp[4];  // bf16 pairs, reinterpreted only at the dot2 call
+  if constexpr (!MF) {
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
+      for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) nkp[j] = pack2bf(nk[j * 2], nk[j * 2 + 1]);
   uint32_t nvp[4];
@@ -404,6 +432,68 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   for (int j = 0; j < 4; ++j) nvp[j] = pack2bf(nv[j * 2], nv[j * 2 + 1]);
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
+  DEC_PROBE(2, nvp[0]);
+  if constexpr (MF) {
+    static_assert(G <= 16, "MFMA score tile has 16 head columns");
+    constexpr int NKC = HD / 32;  // k-steps of 32 dims
+    constexpr int TB = 4;         // key tiles in flight per wave
+    const int lane = tid & 63, wave = tid >> 6, hj = lane & 15, c4 = lane >> 4;
+    bf16x8 qB[NKC], nkA[NKC];
+#pragma unroll
+    for (int m = 0; m < NKC; ++m) {
+      float t8[8];
+      const int hq = min(hj, G - 1);  // columns >= G load a valid head and are zeroed (no branch)
+      if constexpr (FUSED) {
+        load_head8<HD, ROPE>(q + (size_t)b * ldq + (kvh * G + hq) * HD, c4 + 4 * m, cosT, sinT, min(p_new, S - 1), t8);
+      } else {
+        const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + hq) * HD + (c4 + 4 * m) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t8[j] = bf2f_s(pq[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qB[m][j] = hj < G ? (short)f2bf(t8[j]) : (short)0;
+      if constexpr (FUSED) {  // the new key in A layout (rows of its tile come from registers)
+        load_head8<HD, ROPE>(q + (size_t)b * ldq + (H + kvh) * HD, c4 + 4 * m, cosT, sinT, min(p_new, S - 1), t8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nkA[m][j] = (short)f2bf(t8[j]);
+      }
+    }
+    const int ntile = (n + 15) / 16;
+    for (int t0 = 0; t0 < ntile; t0 += 4 * TB) {
+      bf16x8 ka[TB][NKC];
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) {
+        const int kk = min((t0 + tb * 4 + wave) * 16 + hj, n - 1);
+#pragma unroll
+        for (int m = 0; m < NKC; ++m) {
+          const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + (c4 + 4 * m) * 8);
+          ka[tb][m] = NT ? __builtin_nontemporal_load(kp) : *kp;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (t0 == 0) DEC_PROBE(8, ka[0][0][0]);
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) {
+        const int t = t0 + tb * 4 + wave;
+        if (t >= ntile) break;  // wave-uniform
+        if (FUSED && t * 16 + hj == knew) {
+#pragma unroll
+          for (int m = 0; m < NKC; ++m) ka[tb][m] = nkA[m];
+        }
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < NKC; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[tb][m], qB[m], acc, 0, 0, 0);
+        if (t0 == 0 && tb == 0) DEC_PROBE(9, acc[0]);
+        if (hj < G) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = t * 16 + c4 * 4 + r;
+            if (key < n) sc[hj * chunk_cap + key] = acc[r] * scale_log2;
+          }
+        }
+      }
+    }
+  } else {
   // Scores: batches of DEC_U key rows per thread, all loads issued before the
   // first use (memory-level parallelism is the whole game in decode).
   for (int kb0 = 0; kb0 < n; kb0 += GPB * DEC_U) {
@@ -440,7 +530,19 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       }
     }
   }
+  }
+  DEC_PROBE(10, 0);
+  // first batch of value rows: requested now, in flight across the barrier and
+  // the softmax (they depend only on the key range)
+  bf16x8 vr0[DEC_U];
+#pragma unroll
+  for (int u = 0; u < DEC_U; ++u) {
+    const int kk = min(u * GPB + grp, n - 1);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+    vr0[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+  }
   __syncthreads();
+  DEC_PROBE(3, 0);
   // per-head max and exp (one wave per head, strided)
   __shared__ float mh[DEC_MAXG], lh[DEC_MAXG];
   const int wave = tid >> 6, lane = tid & 63;
@@ -458,6 +560,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     if (lane == 0) { mh[g] = mx; lh[g] = s; }
   }
   __syncthreads();
+  DEC_PROBE(4, 0);
   // P.V: thread owns d chunk `sub` for key group `grp`
   float acc[G][8];
 #pragma unroll
@@ -466,11 +569,16 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   for (int kb0 = 0; kb0 < n; kb0 += GPB * DEC_U) {
     bf16x8 vr[DEC_U];
+    if (kb0 == 0) {
 #pragma unroll
-    for (int u = 0; u < DEC_U; ++u) {
-      const int kk = min(kb0 + u * GPB + grp, n - 1);
-      const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
-      vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+      for (int u = 0; u < DEC_U; ++u) vr[u] = vr0[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < DEC_U; ++u) {
+        const int kk = min(kb0 + u * GPB + grp, n - 1);
+        const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+        vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // Key pairs (u, u+1) of this thread share the d chunk: interleave their
@@ -511,6 +619,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       }
     }
   }
+  DEC_PROBE(5, acc[0][0]);
   __syncthreads();  // scores no longer needed: reuse dsm as [GPB][G][HD] reduction scratch
   float* red = dsm;
 #pragma unroll
@@ -532,6 +641,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     wsp[tid * (HD + 2) + HD] = mh[tid];
     wsp[tid * (HD + 2) + HD + 1] = lh[tid];
   }
+  // the new key / value row into the cache, last: a store issued before the
+  // K/V loads would sit in front of them in this wave's vmcnt queue
+  if (FUSED && own_new && grp == 0) {
+    uint4 wk, wv;
+    uint32_t* pk = reinterpret_cast<uint32_t*>(&wk);
+    uint32_t* pv = reinterpret_cast<uint32_t*>(&wv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pk[j] = nkp[j];
+      pv[j] = nvp[j];
+    }
+    *reinterpret_cast<uint4*>(kb + (size_t)p_new * HD + sub * 8) = wk;
+    *reinterpret_cast<uint4*>(vb + (size_t)p_new * HD + sub * 8) = wv;
+  }
+  DEC_PROBE(7, 0);
 }
 
 __global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H, int Hkv,
@@ -621,13 +745,26 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
   dim3 grid(B * Hkv, splits);
   // cache bytes this launch may stream (capacity bound): > 32 MB -> non-temporal
   const bool nt = (double)B * Hkv * S * hd * 4.0 > 32.0 * 1024 * 1024;
-#define DEC_NT(HDV, GV, NTV)                                                                                          \
-  if (fused)                                                                                                          \
-    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, true, NTV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,    \
+  // MFMA scores: GQA (G >= 2) by default; DNN_DECODE_MFMA=0/1 forces it off/on (A/B)
+  const char* mf_e = getenv("DNN_DECODE_MFMA");
+  const bool mf = mf_e ? atoi(mf_e) == 1 : G >= 2;
+  const int fm = fused ? (cosT != nullptr ? 2 : 1) : 0;
+#define DEC_FM(HDV, GV, NTV, MFV)                                                                                     \
+  if (fm == 2)                                                                                                        \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 2, NTV, MFV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,  \
                        (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, chunk_cap, (bf16_t*)o);        \
+  else if (fm == 1)                                                                                                   \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 1, NTV, MFV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,  \
+                       (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2, chunk_cap, (bf16_t*)o);  \
   else                                                                                                                \
-    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, false, NTV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,   \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 0, NTV, MFV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,  \
                        (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2, chunk_cap, (bf16_t*)o);
+#define DEC_NT(HDV, GV, NTV)                                                                                          \
+  if (mf) {                                                                                                           \
+    DEC_FM(HDV, GV, NTV, true)                                                                                        \
+  } else {                                                                                                            \
+    DEC_FM(HDV, GV, NTV, false)                                                                                       \
+  }
 #define DEC(HDV, GV)                                                                                                  \
   if (hd == HDV && G == GV) {                                                                                         \
     if (nt) {                                                                                                         \
@@ -639,10 +776,17 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
   DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(128, 1) DEC(128, 2) DEC(128, 4) DEC(128, 8) { return -2; }
 #undef DEC
 #undef DEC_NT
+#undef DEC_FM
   if (splits > 1)
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
   return (int)hipGetLastError();
 }
+
+#ifdef DNN_DEC_PROBE
+extern "C" int dnn_dec_probe_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dec_probe_ts), sizeof(unsigned long long) * 32);
+}
+#endif
 
 extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd,
                                int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {

@@ -136,8 +136,12 @@ def test_flash_attn_spike_rescale():
                                                (1, 4, 2, 128, 300, [299]), (4, 25, 25, 64, 512, [17, 64, 65, 512]),
                                                (1, 32, 8, 128, 131072, [120001]),   # long context: LDS-bound splits
                                                (2, 12, 12, 64, 65536, [65536, 9000])])
-def test_attn_decode(B, H, Hkv, hd, S, lens):
+@pytest.mark.parametrize("mfma", ["0", "1"])
+def test_attn_decode(B, H, Hkv, hd, S, lens, mfma, monkeypatch):
+    """Both score paths of the decode kernel: DPP row reductions and MFMA key
+    tiles (the GQA default), forced by DNN_DECODE_MFMA."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
+    monkeypatch.setenv("DNN_DECODE_MFMA", mfma)
     torch.manual_seed(2)
     q = torch.randn(B, H, hd, device=DEV).bfloat16()
     kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
@@ -469,13 +473,16 @@ def test_linear_norm_strided_rows():
 
 @pytest.mark.parametrize("B,H,Hkv,hd,S,pos,rope,splits", [
     (1, 32, 8, 128, 200, [150], True, 1), (3, 12, 12, 64, 300, [0, 17, 299], False, 2),
-    (2, 8, 2, 128, 1024, [700, 1023], True, 4), (2, 4, 4, 64, 64, [63, 64], False, 1)])
-def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits):
+    (2, 8, 2, 128, 1024, [700, 1023], True, 4), (2, 4, 4, 64, 64, [63, 64], False, 1),
+    (1, 32, 8, 128, 600, [140], True, 1), (1, 32, 8, 128, 600, [599], True, 3)])
+@pytest.mark.parametrize("mfma", ["0", "1"])
+def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits, mfma, monkeypatch):
     """Fused decode step (split + RoPE + cache write + attention) == qkv_split
     then attn_decode, and the cache row it wrote matches; pos >= S (overflow)
     writes nothing and attends to the S cached keys."""
     from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
     from distributed_neural_networks_amd.ops import transformer_ops as T
+    monkeypatch.setenv("DNN_DECODE_MFMA", mfma)
     torch.manual_seed(9)
     kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
     vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
