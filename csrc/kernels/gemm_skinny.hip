@@ -54,15 +54,15 @@ enum SkNorm { NORM_NONE = 0, NORM_RMS = 1, NORM_LN = 2 };
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // 16 OCP e4m3 weight bytes -> 16 bf16 (exact: every e4m3 value is a bf16
-// value; the hardware converter yields fp32 and bf16 is its upper half).
+// value).  gfx950's v_cvt_scalef32_pk_bf16_fp8 (scale 1.0) turns two bytes into
+// a packed bf16 pair in one op: 8 VALU per 16 B instead of 8 fp32 converts + 8
+// repacks — the decode weight stream is VALU-paced at batch 1.
 __device__ __forceinline__ void w8_to_bf16(const i32x4& w, bf16x8& lo, bf16x8& hi) {
-  uint32_t o[8];
+  bf16x2v o[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(w[i], false);
-    const f32x2 b = __builtin_amdgcn_cvt_pk_f32_fp8(w[i], true);
-    o[2 * i] = (__float_as_uint(a[0]) >> 16) | (__float_as_uint(a[1]) & 0xffff0000u);
-    o[2 * i + 1] = (__float_as_uint(b[0]) >> 16) | (__float_as_uint(b[1]) & 0xffff0000u);
+    o[2 * i] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)w[i], 1.0f, false);
+    o[2 * i + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)w[i], 1.0f, true);
   }
   __builtin_memcpy(&lo, &o[0], 16);
   __builtin_memcpy(&hi, &o[4], 16);
@@ -72,7 +72,16 @@ __device__ __forceinline__ void w8_to_bf16(const i32x4& w, bf16x8& lo, bf16x8& h
 // c = the row's first element, so var = E[(x-c)^2] - E[x-c]^2 does not cancel
 // catastrophically when |mean| >> std (the unshifted E[x^2] - mean^2 loses
 // every bit of the variance once mean^2 / var ~ 2^24).
+template <int NORM>
 __device__ __forceinline__ void sk_stats(const i32x4& a, float c, float& s1, float& s2) {
+  if constexpr (NORM == NORM_RMS) {  // sum of squares only: one v_dot2 per bf16 pair (products exact in fp32)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x2v v = __builtin_bit_cast(bf16x2v, (uint32_t)a[i]);
+      s2 = __builtin_amdgcn_fdot2_f32_bf16(v, v, s2, false);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float lo = __uint_as_float((uint32_t)a[i] << 16) - c;
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
-          for (int h = 0; h < AU; ++h) sk_stats(av[t][u * AU + h], shift[t], st1[t], st2[t]);
+          for (int h = 0; h < AU; ++h) sk_stats<NORM>(av[t][u * AU + h], shift[t], st1[t], st2[t]);
       }
       if constexpr (W8) {
         // the lane's 16 weight bytes are k = 16g..16g+15 of the chunk; its two A
@@ -403,6 +412,9 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     // row-major stream stayed as fast or faster in-graph (25.6 vs 26.3, 9.7 vs
     // 10.1 us) although the cold-cache sweep favoured the copy
     if (!FP8 && Wsh != nullptr && N > 4096 && N < 16384 && kbytes <= 8192) CFG(1, 1, 4, false, 4);
+    // fp8 vocabulary head (128K x 4K, fragment order): 2 column tiles per wave
+    // 83.3 -> 75.8 us, 6.9 TB/s (profiles/r2_skinny_sweep_w8_m1.jsonl)
+    if (W8 && Wsh != nullptr && N >= 65536) CFG(1, 2, 4, false, 8);
     CFG(1, 1, 4, false, 8);
   }
   if (M <= 16) {

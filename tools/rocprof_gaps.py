@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Kernel-boundary cost of a decode run from a rocprofv3 ``--kernel-trace``
+database: over the kernels after the last prefill attention launch (the decode
+graphs), the span, the summed kernel time, the idle gaps between consecutive
+kernels (the per-launch boundary the HIP graph does not hide), and the mean
+duration and gap per kernel name.
+
+    python tools/rocprof_gaps.py gpurun_out/prof_dir [--after flash_attn] > profiles/xxx.md
+"""
+import argparse
+import collections
+import glob
+import os
+import re
+import sqlite3
+
+
+def short(name: str) -> str:
+    return re.sub(r"\(.*", "", name).replace("void ", "")[:80]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--after", default="flash_attn", help="decode region starts after the last kernel matching this")
+    args = ap.parse_args()
+    db = glob.glob(os.path.join(args.dir, "**", "*results.db"), recursive=True)[0]
+    con = sqlite3.connect(db)
+    cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
+    cs = next(c for c in cols if c.lower() in ("start", "start_ns", "begin", "begin_ns"))
+    ce = next(c for c in cols if c.lower() in ("end", "end_ns"))
+    rows = con.execute(f"select name, {cs}, {ce} from kernels order by {cs}").fetchall()
+    last = max((i for i, r in enumerate(rows) if args.after in r[0]), default=-1)
+    dec = rows[last + 1:]
+    if len(dec) < 2:
+        raise SystemExit("no decode region")
+    span = dec[-1][2] - dec[0][1]
+    busy = sum(e - s for _, s, e in dec)
+    gaps = [max(0, dec[i + 1][1] - dec[i][2]) for i in range(len(dec) - 1)]
+    print(f"decode region: {len(dec)} kernels, span {span / 1e3:.1f} us, kernel time {busy / 1e3:.1f} us, "
+          f"idle between kernels {sum(gaps) / 1e3:.1f} us ({100 * sum(gaps) / span:.1f} %), "
+          f"mean gap {sum(gaps) / len(gaps) / 1e3:.2f} us")
+    print()
+    per = collections.defaultdict(lambda: [0, 0, 0])
+    for i, (n, s, e) in enumerate(dec[:-1]):
+        p = per[short(n)]
+        p[0] += 1
+        p[1] += e - s
+        p[2] += gaps[i]
+    print("| kernel | calls | mean us | mean gap after us |")
+    print("|---|---|---|---|")
+    for n, (c, d, g) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        print(f"| `{n}` | {c} | {d / c / 1e3:.2f} | {g / c / 1e3:.2f} |")
+
+
+if __name__ == "__main__":
+    main()
