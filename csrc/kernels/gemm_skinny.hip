@@ -106,7 +106,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   constexpr int AU = W8 ? 2 : 1;        // 16-B A loads per chunk per M tile (W8: a chunk is 64 k = 128 B of A)
   constexpr int ACH = W8 ? 128 : 64;    // A bytes per row per chunk
   extern __shared__ __attribute__((aligned(16))) f32x4 sk_red[];  // [KS][NT*MT][64], then [KS][MT][16] x2 stats
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, KS = blockDim.x >> 6;
+  // wave index via readfirstlane: the K-slice bounds and the surplus-chunk tests
+  // below are then scalar (s_cbranch), not exec-masked VALU branches
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), KS = blockDim.x >> 6;
   // MS (M split): one workgroup per (column tile, 16-row M tile), so M = 32..64
   // runs 2-4x the workgroups (narrow N, e.g. GPT-2's 768-wide projections, has
   // too few column tiles to fill 256 CUs otherwise).  The M tiles of a column
