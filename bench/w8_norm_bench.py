@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--m", type=int, default=1)
     ap.add_argument("--cases", default=",".join(c[0] for c in CASES))
+    ap.add_argument("--env", default="", help="NAME=v1,v2,...: repeat each case per value of an A/B env var")
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import attach_shuffled
@@ -42,8 +43,16 @@ def main():
         x = torch.randn(M, K, device=dev).bfloat16()
         out = torch.empty(M, N // 2 if act == 3 else N, device=dev, dtype=torch.bfloat16)
         res = {"case": name, "M": M, "N": N, "K": K, "MB": round(N * K / 1e6, 1)}
-        for shuf in (False, True):
-            if shuf:
+        envs = [None]
+        if args.env:
+            ename, vals = args.env.split("=")
+            envs = [(ename, v) for v in vals.split(",")]
+        for shuf, ev in [(s_, e_) for s_ in (False, True) for e_ in envs]:
+            if ev is not None:
+                if not shuf:
+                    continue
+                os.environ[ev[0]] = ev[1]
+            if shuf and ws[0].shuf is None:
                 for w in ws:
                     attach_shuffled(w)
 
@@ -66,7 +75,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             us = a.elapsed_time(b) / (3 * args.iters) * 1e3
-            key = "shuf" if shuf else "rowmajor"
+            key = ("shuf" if shuf else "rowmajor") + (f"_{ev[0]}{ev[1]}" if ev else "")
             res[f"{key}_us"] = round(us, 2)
             res[f"{key}_TBs"] = round(N * K / us / 1e6, 2)
         print(json.dumps(res), flush=True)

@@ -409,14 +409,16 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     CFG_MS(2, 2, false, 4);
   }
   if (M <= 8) {
-    // fragment-order weights at batch 1-8 only for the mid-size N (QKV): in the
-    // Llama-3 8B fp8 decode graph 12.25 -> 10.33 us; on gate|up, O and down the
-    // row-major stream stayed as fast or faster in-graph (25.6 vs 26.3, 9.7 vs
-    // 10.1 us) although the cold-cache sweep favoured the copy
+    // batch 1-8: the fragment-order copy (Wsh) is streamed whenever the layer
+    // attached one; per shape class: QKV-sized N 1 tile x 4 chunks on 4 waves
+    // (Llama-3 8B fp8 decode graph 12.25 -> 10.33 us), the rest below
     if (!FP8 && Wsh != nullptr && N > 4096 && N < 16384 && kbytes <= 8192) CFG(1, 1, 4, false, 4);
     // fp8 vocabulary head (128K x 4K, fragment order): 2 column tiles per wave
     // 83.3 -> 75.8 us, 6.9 TB/s (profiles/r2_skinny_sweep_w8_m1.jsonl)
     if (W8 && Wsh != nullptr && N >= 65536) CFG(1, 2, 4, false, 8);
+    // fp8 gate|up (28K x 4K) with the fused RMSNorm: 2 column tiles x 2 chunks
+    // on 2 waves 23.3 -> 21.3 us (profiles/r2_w8_decode_projections.jsonl)
+    if (W8 && Wsh != nullptr && N >= 16384) CFG(1, 2, 2, false, 2);
     CFG(1, 1, 4, false, 8);
   }
   if (M <= 16) {
