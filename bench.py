@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="images sourced per GPU per step")
+    ap.add_argument("--no_fill", action="store_true",
+                    help="linear N>1: stage-1 GPUs only serve received microbatches (no own images)")
+    ap.add_argument("--fill_rows", type=int, default=-1, help="linear N>1: own images per round on a stage-1 GPU "
+                                                               "(-1 = sized from timing, see receiver_fill_rows)")
     ap.add_argument("--microbatches", type=int, default=2,
                     help="microbatches per step on N>1 (2 x 32768 rows fill the fc1 GEMM's 256 tiles)")
     ap.add_argument("--placement", default="linear", choices=["linear", "interleaved"],
@@ -223,7 +227,12 @@ def bench_linear(args, info):
     direct xGMI links (``parallel/partition.py::linear_plan``): n0 stage-0 GPUs
     each source ``--batch`` images per step and stream them to one of n1
     stage-1 GPUs.  The K timed steps run as ONE stream of K x M microbatches
-    (fill and drain once, not per step)."""
+    (fill and drain once, not per step).  A stage-1 GPU spends ~2 % of a
+    round on fc2, so it also runs its own images through both stages between
+    rounds (``receiver_fill_rows``; measured on one MI355X at 32768-row
+    microbatches: stage 0 1.245 ms, stage 1 0.023 ms -> 27648 / 24576 / 19456
+    own rows per round at N = 2 / 4 / 8, i.e. 1.84 / 3.75 / 7.59 GPUs of work
+    instead of 1 / 3 / 7)."""
     from distributed_neural_networks_amd.parallel.links import P2PLink
     from distributed_neural_networks_amd.parallel.partition import linear_plan, linear_role
     from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
@@ -245,17 +254,72 @@ def bench_linear(args, info):
             run_gpipe(s0, steps * M, mb, None, nxt, source=lambda i: xs[i % M], depth=2)
     else:
         prevs = [P2PLink(p, dev) for p in role["recv_from"]]
+        # receiver fill: a stage-1 GPU is mostly idle (fc2 is ~1 % of the model),
+        # so between rounds of received microbatches it runs its own images
+        # through both stages, sized so a round still fits in a sender's period
+        fill = 0 if args.no_fill else (args.fill_rows if args.fill_rows >= 0 else
+                                       receiver_fill_rows(s0, s1, mb, len(prevs), dev))
+        if fill:
+            xl = torch.randn((fill, 3, 32, 32), device=dev, generator=g)
+            sh0, dt0 = s0.out_spec(fill)
+            sh1, dt1 = s1.out_spec(fill)
+            yl0 = torch.empty(sh0, dtype=dt0, device=dev)
+            yl1 = torch.empty(sh1, dtype=dt1, device=dev)
+        count = [0]
+
+        def local_fill():
+            count[0] += 1
+            if fill and count[0] % len(prevs) == 0:
+                s1.forward(s0.forward(xl, yl0), yl1)
 
         def stream(steps):
-            run_gpipe(s1, steps * M * len(prevs), mb, prevs, None, depth=2 * len(prevs))
+            run_gpipe(s1, steps * M * len(prevs), mb, prevs, None, depth=2 * len(prevs), progress=local_fill)
 
     stream(args.warmup)
     t0 = sync_time(info)
     stream(args.steps)
     t1 = sync_time(info)
-    imgs_total_per_step = plan["n0"] * mb * M
-    par = f"pp2-linear-{plan['n0']}x{plan['n1']}"
+    # images completed per step, job-wide: every sender's stream plus the receivers' own
+    local = torch.tensor([0.0 if role["stage"] == 0 else float(fill * M)], dtype=torch.float64,
+                         device=dev)
+    import torch.distributed as dist
+    dist.all_reduce(local)
+    imgs_total_per_step = plan["n0"] * mb * M + float(local.item())
+    args._fill_rows = float(local.item())
+    par = f"pp2-linear-{plan['n0']}x{plan['n1']}" + ("+fill" if local.item() > 0 else "")
     return t1 - t0, imgs_total_per_step / N, float("nan"), par
+
+
+RECV_ITEM_OVERHEAD_S = 30e-6  # host wait + launch per received microbatch (assumed, not measured here)
+
+
+def receiver_fill_rows(s0, s1, mb: int, n_prev: int, dev) -> int:
+    """Rows of its own images a stage-1 GPU can push through both stages per
+    round of ``n_prev`` received microbatches without slowing the senders:
+    (t_stage0 - n_prev (t_stage1 + overhead)) / t_both, 10 % margin, whole 1024-row
+    blocks (8-row blocks for the small CPU test batches).  Timed on this GPU before the stream (the senders run the same
+    stage-0 kernel on the same hardware)."""
+    x = torch.randn((mb, 3, 32, 32), device=dev)
+    sh0, dt0 = s0.out_spec(mb)
+    sh1, dt1 = s1.out_spec(mb)
+    y0 = torch.empty(sh0, dtype=dt0, device=dev)
+    y1 = torch.empty(sh1, dtype=dt1, device=dev)
+
+    def timed(fn, reps=3):
+        fn()
+        dsync(dev)
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        dsync(dev)
+        return (time.perf_counter() - t) / reps
+
+    t_s0 = timed(lambda: s0.forward(x, y0))
+    t_s1 = timed(lambda: s1.forward(y0, y1))
+    budget = t_s0 - n_prev * (t_s1 + RECV_ITEM_OVERHEAD_S)
+    frac = max(0.0, budget / (t_s0 + t_s1)) * 0.9
+    gran = 1024 if mb >= 8192 else 8
+    return int(mb * frac) // gran * gran
 
 
 def extra_keys(args, info):
@@ -336,6 +400,7 @@ def main():
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
+                       "receiver_fill_images_per_step": getattr(args, "_fill_rows", 0),
                        "stage0_spare_cus": spare,
                        "stage_cut": {1: f"conv|fc (reference split, {hop_kib} KiB/img hop)",
                                      2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},

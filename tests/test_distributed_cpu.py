@@ -195,16 +195,18 @@ def test_stream_schedule_gloo(world):
             assert torch.allclose(torch.from_numpy(out[i]), m(x), atol=1e-5)
 
 
-@pytest.mark.parametrize("placement,n", [("linear", 2), ("linear", 4), ("linear", 8), ("interleaved", 2)])
-def test_bench_distributed_schedule_cpu(placement, n):
+@pytest.mark.parametrize("placement,n,fill", [("linear", 2, 0), ("linear", 4, 0), ("linear", 8, 0), ("interleaved", 2, 0),
+                                              ("linear", 4, 8)])
+def test_bench_distributed_schedule_cpu(placement, n, fill):
     """bench.py's multi-GPU placements with gloo on CPU (the driver's N = 2/4/8
     scaling runs use the same schedule over RCCL); the JSON line has the same
-    metric / config / dtype keys as the N = 1 run."""
+    metric / config / dtype keys as the N = 1 run.  ``fill``: stage-1 ranks also
+    push that many of their own images per round through both stages."""
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--cpu",
            "--batch", "16", "--steps", "2", "--warmup", "1", "--microbatches", "2", "--latency_iters", "3",
-           "--placement", placement]
+           "--placement", placement, "--fill_rows", str(fill)]
     env = dict(ENV, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
@@ -218,8 +220,9 @@ def test_bench_distributed_schedule_cpu(placement, n):
     if placement == "linear":
         from distributed_neural_networks_amd.parallel.partition import linear_plan
         plan = linear_plan(n, "fp32")
-        assert d["config"]["parallelism"] == f"pp2-linear-{plan['n0']}x{plan['n1']}"
-        assert d["config"]["global_batch"] == plan["n0"] * 16
+        assert d["config"]["parallelism"] == f"pp2-linear-{plan['n0']}x{plan['n1']}" + ("+fill" if fill else "")
+        assert d["config"]["global_batch"] == plan["n0"] * 16 + plan["n1"] * fill * 2
+        assert d["config"]["receiver_fill_images_per_step"] == plan["n1"] * fill * 2
 
 
 @pytest.mark.parametrize("n", [4, 8])
