@@ -37,6 +37,8 @@ def parse(argv=None):
     ap.add_argument("--stages", type=int, default=4)
     ap.add_argument("--batch", type=int, default=64, help="sequences per microbatch")
     ap.add_argument("--microbatches", type=int, default=0, help="0 = number of GPU groups")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="one GPU group: HIP streams the microbatches of a decode round run on (0 = one, -1 = min(M, 4))")
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--prefill_iters", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
@@ -122,7 +124,8 @@ def run(args=None):
 
     from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
     links = RingLinks(prev=prev, nxt=nxt, back_out=back_to0, back_in=back_from)
-    ring = DecodeRing(stages, links, groups, M, B, use_graphs=not args.no_graph, record=False) if stages else None
+    ring = (DecodeRing(stages, links, groups, M, B, use_graphs=not args.no_graph, record=False,
+                      lanes=getattr(args, "lanes", 0)) if stages else None)
     prompts = [torch.randint(0, V, (B, T0), device=dev, dtype=torch.int32) for _ in range(M)] if grp == 0 else None
 
     def sync():
@@ -200,6 +203,7 @@ def run(args=None):
             "hip_graph_decode": bool(graphs),
             "config": {"model": model, "stages": S, "gpu_groups": groups, "replicas": replicas,
                        "micro_batch": B, "microbatches": M, "prompt_len": T0, "seq_len": max_seq,
+                       "decode_lanes": len(ring.lanes) if ring is not None and ring.lanes else 1,
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},
         }
     if N > 1:

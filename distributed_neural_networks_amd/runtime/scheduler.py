@@ -296,7 +296,14 @@ class DecodeRing:
     """
 
     def __init__(self, stages: Sequence, links: RingLinks, n_groups: int, M: int, B: int,
-                 use_graphs: bool = True, record: bool = True, progress: Progress = None):
+                 use_graphs: bool = True, record: bool = True, progress: Progress = None, lanes: int = 0):
+        """``lanes`` (one group, M > 1, GPU): the M microbatch steps of a round
+        replay on this many HIP streams (0 = one stream, -1 = min(M, 4));
+        scratch rows follow the KV rows (``TransformerStage.step``), so
+        concurrent microbatches share no buffer.  Off by default: measured on
+        GPT-2 4-stage (profiles/r2_decode_lanes_gpt2.jsonl) concurrent small
+        microbatches beat the same microbatches on one stream (16 x 4: 2.17 ->
+        0.88 ms/round) but not one large batch (64 x 1: 0.60 ms)."""
         self.stages = list(stages)
         self.links = links
         self.G, self.M, self.B = n_groups, M, B
@@ -326,6 +333,9 @@ class DecodeRing:
         self.use_graphs = use_graphs and dev.type == "cuda"
         self.graphs: Dict[int, object] = {}
         self.steps_done = 0
+        n_lanes = min(M, 4) if lanes < 0 else min(M, lanes)
+        self.lanes = ([torch.cuda.Stream(dev) for _ in range(n_lanes)]
+                      if n_groups == 1 and n_lanes > 1 and dev.type == "cuda" else [])
 
     # -- one microbatch through this rank's stages --------------------------
     def _run(self, x, m: int, T: int, out=None):
@@ -438,6 +448,8 @@ class DecodeRing:
 
     def decode_round(self) -> None:
         """Every microbatch advances one token on this rank's stages."""
+        if self.lanes:
+            return self._decode_round_lanes()
         G = self.G
         for m in range(self.M):
             if self.first and G > 1:
@@ -455,6 +467,28 @@ class DecodeRing:
             if self.first and G == 1 and self.record:
                 self.toks[m].append(self.cur[m].view(self.B).clone())
             self.progress()
+        self.steps_done += 1
+
+    def _decode_round_lanes(self) -> None:
+        """One group, M microbatches on ``len(self.lanes)`` streams: the round
+        forks from the current stream and joins back into it, so host-visible
+        state (recorded tokens, the next prefill) is ordered as on one stream."""
+        cur = torch.cuda.current_stream(self.dev)
+        for s in self.lanes:
+            s.wait_stream(cur)
+        for m in range(self.M):
+            s = self.lanes[m % len(self.lanes)]
+            with torch.cuda.stream(s):
+                with trace.span("decode", "compute", mb=m, step=self.steps_done, lane=m % len(self.lanes)):
+                    if m in self.graphs:
+                        self.graphs[m]()
+                    else:
+                        self._decode_body(m)
+                if self.record:
+                    self.toks[m].append(self.cur[m].view(self.B).clone())
+            self.progress()
+        for s in self.lanes:
+            cur.wait_stream(s)
         self.steps_done += 1
 
     def drain(self) -> None:

@@ -192,7 +192,8 @@ class TransformerStage(StageCompute):
         self.lens = torch.zeros((self.max_batch,), dtype=torch.int32, device=dev)
         self.splits = T_.decode_splits(self.max_seq, self.max_batch, Hkv, H // Hkv)
         G = H // Hkv
-        self.ws = torch.empty((self.max_batch * Hkv * self.splits * G * (hd + 2),), dtype=torch.float32, device=dev)
+        self.ws_per_seq = Hkv * self.splits * G * (hd + 2)  # decode-attention partials of one sequence
+        self.ws = torch.empty((self.max_batch * self.ws_per_seq,), dtype=torch.float32, device=dev)
         self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
@@ -237,26 +238,37 @@ class TransformerStage(StageCompute):
         if b0 + B > self.max_batch:
             raise ValueError("batch slice exceeds the KV cache")
         d = self.d
+        # decode scratch rows follow the KV rows (r0 = b0): microbatches on
+        # different cache rows share no buffer, so their steps may run
+        # concurrently on separate streams (DecodeRing lanes); prefill (T > 1)
+        # uses the rows from 0 and stays one-at-a-time
+        r0 = b0 if T == 1 else 0
+        r1 = r0 + ntok
         if self.first:
             if x.dtype != torch.int32 or tuple(x.shape) != (B, T):
                 raise ValueError(f"first stage expects int32 ids (B,T)=({B},{T}), got {x.dtype} {tuple(x.shape)}")
-            T_.embed(x, self.wte, self.wpe, self.buf_h, pos)
-            h_in = self.buf_h[:ntok]
+            T_.embed(x, self.wte, self.wpe, self.buf_h[r0:r1], pos)
+            h_in = self.buf_h[r0:r1]
         else:
             h_in = x.reshape(ntok, d)
-        h = self.buf_h[:ntok]
-        a = self.buf_a[:ntok]
+        h = self.buf_h[r0:r1]
+        a = self.buf_a[r0:r1]
+        q8, s8 = self.q8, self.s8
+        if self.fp8 and T == 1:
+            q8 = self.q8[r0 * (self.q8.numel() // self.max_tokens):]
+            s8 = self.s8[r0:]
+        ws = self.ws[r0 * self.ws_per_seq:] if T == 1 else self.ws
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
             if self.fuse_norm:
-                qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[:ntok], std_buf=a, ones=self.ones, q8=self.q8,
-                                  s8=self.s8)
+                qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[r0:r1], std_buf=a, ones=self.ones, q8=q8,
+                                  s8=s8)
             else:
                 T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
-                qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[:ntok])
-            att = self.buf_att[:ntok]
+                qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[r0:r1])
+            att = self.buf_att[r0:r1]
             if T == 1:  # decode: split/RoPE/cache write fused into the attention launch
-                T_.attn_decode_qkv(qkv, kc, vc, att, B, self.H, self.Hkv, self.hd, pos, self.ws, self.splits,
+                T_.attn_decode_qkv(qkv, kc, vc, att, B, self.H, self.Hkv, self.hd, pos, ws, self.splits,
                                    self.cos, self.sin)
             elif self.cos is None:  # no RoPE (GPT-2): attention reads the c_attn output directly
                 T_.flash_attn_qkv(qkv, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
@@ -266,11 +278,11 @@ class TransformerStage(StageCompute):
             self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
             if self.fuse_norm:
-                f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[:ntok], std_buf=a, ones=self.ones, q8=self.q8,
-                                s8=self.s8)
+                f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[r0:r1], std_buf=a, ones=self.ones, q8=q8,
+                                s8=s8)
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
-                f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[:ntok])
+                f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[r0:r1])
             self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s)
             h_in = h
         if not self.last:
@@ -282,19 +294,19 @@ class TransformerStage(StageCompute):
             rows, src, ldx = B, h[T - 1:], T * d
         else:
             rows, src, ldx = ntok, h, d
-        logits = self.logits[:rows]
+        logits = self.logits[r0:r0 + rows]
         if self.fuse_norm:
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
-            linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf, ones=self.ones,
-                        q8=self.q8, s8=self.s8)
+            linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf[r0:], ones=self.ones,
+                        q8=q8, s8=s8)
         else:
-            lnf = self.buf_lnf[:rows]
+            lnf = self.buf_lnf[r0:r0 + rows]
             T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)
             if self.fp8:
                 self._head_fp8(lnf, logits)
             else:
                 linear(lnf, self.w_head, None, out=logits[:, :self.V])
-        nxt = self.next_ids[:rows]
+        nxt = self.next_ids[r0:r0 + rows]
         if self.temperature > 0 and last_only:
             T_.sample_topk(logits, nxt, self.V, self.temperature, self.top_k, self.seed, step=pos)
         else:

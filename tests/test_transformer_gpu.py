@@ -685,3 +685,33 @@ def test_gpt2_small_4stage_vs_golden():
         x = h.pred.cpu().long().view(B, 1)
         p += Tn
         Tn = 1
+
+
+@pytest.mark.parametrize("model", ["gpt2-tiny", "llama3-tiny"])
+def test_decode_ring_lanes_match_one_stream(model):
+    """Colocated decode ring with 4 microbatches on 4 HIP streams (lanes):
+    the same greedy tokens as the same ring on one stream (scratch rows follow
+    the KV rows, so concurrent microbatches share no buffer), graphs on and off."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import model_info
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    n = model_info(model).num_layers
+    ranges = [(0, n // 2 - 1), (n // 2, n - 1)]
+    M, B, T, steps = 4, 3, 12, 6
+    sds = [ckpt.random_stage_state_dict(model, a, b, i == 0, i == 1, 5, nontrivial=True)
+           for i, (a, b) in enumerate(ranges)]
+    g = torch.Generator().manual_seed(11)
+    prompts = [torch.randint(0, model_info(model).cfg.vocab_size, (B, T), generator=g) for _ in range(M)]
+    toks = {}
+    for lanes, graphs in ((0, True), (4, True), (4, False)):
+        st = [TransformerStage(model, sds[i], a, b, i == 0, i == 1, DEV, max_batch=M * B, max_seq=T + steps + 2)
+              for i, (a, b) in enumerate(ranges)]
+        ring = DecodeRing(st, RingLinks(), 1, M, B, use_graphs=graphs, lanes=lanes)
+        assert len(ring.lanes) == (lanes if lanes > 1 else 0)
+        toks[(lanes, graphs)] = ring.generate(prompts, T, steps)
+        torch.cuda.synchronize()
+    ref = toks[(0, True)]
+    assert ref.shape == (M * B, steps)
+    for k, v in toks.items():
+        assert torch.equal(v, ref), k
