@@ -5,49 +5,69 @@
 
 namespace dnn {
 
-template <bool F32>
-__global__ __launch_bounds__(256) void argmax_rows_kernel(const void* __restrict__ xv, int ld, int M, int N,
-                                                          int* __restrict__ out) {
+// One workgroup per row.  bf16 rows: every thread issues all of its 16-B loads
+// before the first compare (NV per lane, unrolled), so a row costs one memory
+// round trip instead of one per 2048-element sweep (Llama-3's 128K vocabulary
+// at batch 1: one 1024-thread workgroup, 16 loads per lane).  Decode step tail
+// fused in: the token also goes to `out2` (the next step's input ids) and
+// `pos_inc[row]` advances by one, so the sampled id, the input-id copy and the
+// position update are one launch instead of three.
+__device__ __forceinline__ void argmax_merge(float& best, int& bi, float v, int i) {
+  if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+}
+
+template <bool F32, int TH, int NV>
+__global__ __launch_bounds__(TH) void argmax_rows_kernel(const void* __restrict__ xv, int ld, int M, int N,
+                                                         int* __restrict__ out, int* __restrict__ out2,
+                                                         int* __restrict__ pos_inc) {
   const int row = blockIdx.x;
   if (row >= M) return;
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  if (F32) {
+  if constexpr (F32) {
     const float* x = reinterpret_cast<const float*>(xv) + (size_t)row * ld;
-    for (int i = threadIdx.x; i < N; i += 256) {
-      const float v = x[i];
-      if (v > best || (v == best && i < bi)) { best = v; bi = i; }
-    }
+    for (int i = threadIdx.x; i < N; i += TH) argmax_merge(best, bi, x[i], i);
   } else {
     const bf16_t* x = reinterpret_cast<const bf16_t*>(xv) + (size_t)row * ld;
     const int n8 = (N / 8) * 8;
-    for (int i = threadIdx.x * 8; i < n8; i += 256 * 8) {
-      const bf16x8 p = *reinterpret_cast<const bf16x8*>(x + i);
+    // full sweeps of TH x 8 elements, NV at a time with every load in flight
+    for (int base = 0; base < n8; base += NV * TH * 8) {
+      bf16x8 p[NV];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = bf2f_s(p[j]);
-        if (v > best) { best = v; bi = i + j; }
+      for (int u = 0; u < NV; ++u) {
+        const int i = base + (u * TH + threadIdx.x) * 8;
+        p[u] = i < n8 ? *reinterpret_cast<const bf16x8*>(x + i) : bf16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int i = base + (u * TH + threadIdx.x) * 8;
+        if (i < n8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = bf2f_s(p[u][j]);
+            if (v > best) { best = v; bi = i + j; }  // ascending i per lane: strict > keeps the first
+          }
+        }
       }
     }
-    for (int i = n8 + threadIdx.x; i < N; i += 256) {
-      const float v = bf2f(x[i]);
-      if (v > best || (v == best && i < bi)) { best = v; bi = i; }
-    }
+    for (int i = n8 + threadIdx.x; i < N; i += TH) argmax_merge(best, bi, bf2f(x[i]), i);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ov = __shfl_xor(best, o, 64);
     const int oi = __shfl_xor(bi, o, 64);
-    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    argmax_merge(best, bi, ov, oi);
   }
-  __shared__ float sv[4];
-  __shared__ int si[4];
+  __shared__ float sv[TH / 64];
+  __shared__ int si[TH / 64];
   if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = best; si[threadIdx.x >> 6] = bi; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w)
-      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
+    for (int w = 1; w < TH / 64; ++w) argmax_merge(best, bi, sv[w], si[w]);
+    bi = bi == 0x7fffffff ? 0 : bi;  // all-NaN row: token 0
     out[row] = bi;
+    if (out2 != nullptr) out2[row] = bi;
+    if (pos_inc != nullptr) pos_inc[row] += 1;
   }
 }
 
@@ -187,10 +207,19 @@ extern "C" int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, fl
   return -2;  // vocabulary > 128K entries
 }
 
-extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st) {
+extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st,
+                               int* out2, int* pos_inc) {
   if (M <= 0) return 0;
   if (!f32in && (ld % 8) != 0) return -1;
-  if (f32in) hipLaunchKernelGGL((argmax_rows_kernel<true>), dim3(M), dim3(256), 0, st, x, ld, M, N, out);
-  else hipLaunchKernelGGL((argmax_rows_kernel<false>), dim3(M), dim3(256), 0, st, x, ld, M, N, out);
+  if (f32in) {
+    hipLaunchKernelGGL((argmax_rows_kernel<true, 256, 1>), dim3(M), dim3(256), 0, st, x, ld, M, N, out, out2, pos_inc);
+  } else if (M <= 16) {
+    // few rows: a wide workgroup per row (Llama-3 128K vocabulary: 16 loads per lane)
+    hipLaunchKernelGGL((argmax_rows_kernel<false, 1024, 16>), dim3(M), dim3(1024), 0, st, x, ld, M, N, out, out2,
+                       pos_inc);
+  } else {
+    hipLaunchKernelGGL((argmax_rows_kernel<false, 256, 8>), dim3(M), dim3(256), 0, st, x, ld, M, N, out, out2,
+                       pos_inc);
+  }
   return (int)hipGetLastError();
 }

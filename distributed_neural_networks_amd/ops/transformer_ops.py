@@ -177,11 +177,18 @@ def attn_decode_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: 
     return out
 
 
-def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
+def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None, also: Optional[torch.Tensor] = None,
+                advance: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row argmax (ties -> smallest index) into ``out`` (int32).  Decode
+    step tail in the same launch: ``also`` receives a copy of the ids and
+    ``advance[row] += 1`` (int32 positions)."""
     M = x.shape[0]
     N = n if n is not None else x.shape[1]
+    for t, nm in ((out, "out"), (also, "also"), (advance, "advance")):
+        if t is not None and (t.dtype != torch.int32 or t.numel() < M or not t.is_contiguous()):
+            raise ValueError(f"argmax_rows: {nm} must be contiguous int32 with >= {M} entries")
     check(lib().argmax_rows(ptr(x), x.stride(0), M, N, ptr(out), 1 if x.dtype == torch.float32 else 0,
-                            stream_ptr()), "argmax_rows")
+                            stream_ptr(), ptr(also), ptr(advance)), "argmax_rows")
     return out
 
 

@@ -338,16 +338,25 @@ class DecodeRing:
                       if n_groups == 1 and n_lanes > 1 and dev.type == "cuda" else [])
 
     # -- one microbatch through this rank's stages --------------------------
-    def _run(self, x, m: int, T: int, out=None):
+    def _run(self, x, m: int, T: int, out=None, advance=None):
         h = x
         n = len(self.stages)
         for j, s in enumerate(self.stages):
-            h = s.step(h, self.pos[m], self.B, T, b0=m * self.B, out=out if j == n - 1 else None)
+            if j == n - 1 and advance is not None:
+                h = s.step(h, self.pos[m], self.B, T, b0=m * self.B, out=out, advance=advance)
+            else:
+                h = s.step(h, self.pos[m], self.B, T, b0=m * self.B, out=out if j == n - 1 else None)
         return h
 
     def _decode_body(self, m: int):
         x = self.cur[m] if self.first else self.xin
-        y = self._run(x, m, 1, out=self.out[m])
+        # greedy last stage: the argmax launch also writes the next input ids
+        # (one group) and advances the positions — no separate copy / add kernels
+        if self.last and getattr(self.stages[-1], "fuses_step_tail", False):
+            ids = self.cur[m].view(self.B) if self.G == 1 else None
+            self._run(x, m, 1, out=self.out[m], advance=(ids, self.pos[m]))
+            return None
+        self._run(x, m, 1, out=self.out[m])
         self.pos[m].add_(1)
         if self.last and self.G == 1:
             self.cur[m].copy_(self.out[m].view(self.B, 1))

@@ -227,11 +227,22 @@ class TransformerStage(StageCompute):
         return (batch * T, self.d), torch.bfloat16
 
     # ------------------------------------------------------------------ forward
+    @property
+    def fuses_step_tail(self) -> bool:
+        """Greedy last stage: ``step(advance=...)`` folds the decode step's tail
+        (input-id copy, position update) into the argmax launch."""
+        return self.last and not self.temperature > 0
+
     def step(self, x: torch.Tensor, pos: torch.Tensor, B: int, T: int, b0: int = 0, out: Optional[torch.Tensor] = None,
-             last_only: bool = True):
+             last_only: bool = True, advance=None):
         """Run this stage for B sequences x T new tokens at cache rows
         [b0, b0+B) and positions ``pos`` (device int32 (B,), tokens already
-        cached).  Returns hidden (B*T, d) bf16, or StageOutput for the last stage."""
+        cached).  Returns hidden (B*T, d) bf16, or StageOutput for the last stage.
+        ``advance`` = (ids or None, positions): greedy last stage only
+        (``fuses_step_tail``): the sampled ids are also written to ``ids`` and
+        ``positions += 1``, in the argmax launch."""
+        if advance is not None and not (self.fuses_step_tail and last_only):
+            raise ValueError("step(advance=...) needs a greedy last stage with last_only")
         ntok = B * T
         if ntok > self.buf_h.shape[0]:
             raise ValueError(f"stage buffers hold {self.buf_h.shape[0]} tokens, got {ntok}")
@@ -309,11 +320,13 @@ class TransformerStage(StageCompute):
         nxt = self.next_ids[r0:r0 + rows]
         if self.temperature > 0 and last_only:
             T_.sample_topk(logits, nxt, self.V, self.temperature, self.top_k, self.seed, step=pos)
-        else:
-            T_.argmax_rows(logits, nxt, n=self.V)
-        if last_only and out is not None:
-            out.copy_(nxt)
-        return StageOutput(logits[:, :self.V], nxt)
+            if out is not None:
+                out.copy_(nxt)
+            return StageOutput(logits[:, :self.V], nxt)
+        dst = out if (last_only and out is not None) else nxt
+        also, adv = advance if advance is not None else (None, None)
+        T_.argmax_rows(logits, dst, n=self.V, also=also, advance=adv)
+        return StageOutput(logits[:, :self.V], dst)
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None):
         """Full-prefix forward of one request (the reference stage call,

@@ -194,6 +194,34 @@ def test_argmax_rows():
     assert torch.equal(out2.long().cpu(), xf.argmax(1).cpu())
 
 
+@pytest.mark.parametrize("M,N,ld", [(1, 128256, 128256), (3, 50257, 50304), (16, 1003, 1008), (64, 50257, 50304),
+                                    (100, 4096, 4096)])
+def test_argmax_rows_step_tail(M, N, ld):
+    """Wide-load argmax (1024-thread rows for M <= 16, 256 otherwise) with the
+    fused decode tail: ids to ``out`` and ``also``, ``advance`` += 1; ties go to
+    the smallest index (bf16 logits have many exact ties)."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    x = (torch.randn(M, ld, device=DEV, generator=g) * 4).round().bfloat16()  # coarse values: frequent ties
+    x[0, N - 1] = 100.0  # the maximum in the last (tail) element of row 0
+    if M > 2:
+        x[2, 5] = x[2, N // 2] = 99.0  # tie: the smaller index wins
+        x[2, 7:] = torch.minimum(x[2, 7:], torch.tensor(98.0, device=DEV).bfloat16())
+        x[2, N // 2] = 99.0
+    out = torch.full((M,), -1, dtype=torch.int32, device=DEV)
+    cur = torch.full((M,), -1, dtype=torch.int32, device=DEV)
+    pos = torch.arange(M, dtype=torch.int32, device=DEV)
+    T.argmax_rows(x, out, n=N, also=cur, advance=pos)
+    torch.cuda.synchronize()
+    xs = x[:, :N].float().cpu()
+    ref = torch.tensor([int((row == row.max()).nonzero()[0]) for row in xs])
+    assert torch.equal(out.long().cpu(), ref)
+    assert torch.equal(cur.cpu(), out.cpu())
+    assert torch.equal(pos.cpu(), torch.arange(M, dtype=torch.int32) + 1)
+    if M > 2:
+        assert int(out[2]) == 5
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 512, 1024), (77, 4800, 1600), (3, 1600, 6400), (64, 4800, 1600),
                                    (33, 200, 1000), (1, 50257, 1600)])
 def test_fp8_gemm(M, N, K):
