@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--shapes", default=DEFAULT)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--act", default="none")
+    ap.add_argument("--residual", action="store_true", help="residual epilogue (R = a separate (M,N) bf16 tensor)")
+    ap.add_argument("--inplace", action="store_true", help="residual epilogue in place (R = C, the decoder's h += ...)")
+    ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     dev = torch.device("cuda", 0)
@@ -48,21 +51,25 @@ def main():
         x = torch.randn(M, K, device=dev).bfloat16()
         w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
         bias = torch.randn(N, device=dev)
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        out = torch.randn(M, N, device=dev).bfloat16()
+        res = out if args.inplace else (torch.randn(M, N, device=dev).bfloat16() if args.residual else None)
         flop = 2.0 * M * N * K
         row = {"M": M, "N": N, "K": K}
         ref = None
         for tile in (128, 256):
             set_gemm_tile(tile)
-            ms = timeit(lambda: linear(x, w, bias, act=args.act, out=out), args.iters)
+            ms = timeit(lambda: linear(x, w, bias, act=args.act, residual=res, out=out), args.iters)
             row[f"tile{tile}_tflops"] = round(flop / ms / 1e9, 1)
-            if ref is None:
-                ref = out.clone()
-            else:
-                row[f"tile{tile}_maxdiff"] = (out.float() - ref.float()).abs().max().item()
+            if not args.inplace:
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    row[f"tile{tile}_maxdiff"] = (out.float() - ref.float()).abs().max().item()
         set_gemm_tile(0)
-        ms = timeit(lambda: torch.nn.functional.linear(x, w, bias.bfloat16()), args.iters)
-        row["torch_tflops"] = round(flop / ms / 1e9, 1)
+        if args.torch:
+            ms = timeit(lambda: torch.nn.functional.linear(x, w, bias.bfloat16()), args.iters)
+            row["torch_tflops"] = round(flop / ms / 1e9, 1)
+        row["epilogue"] = args.act + ("+residual_inplace" if args.inplace else "+residual" if args.residual else "")
         print(json.dumps(row), flush=True)
         del x, w, out
 

@@ -1,7 +1,10 @@
 #!/bin/bash
-# GEMM epilogue cost on the GPT-2 prefill shapes (bias / bias+GELU), ours vs torch
+# GEMM epilogue cost on the GPT-2 prefill shapes: bias / +GELU / +residual (separate, in place)
 set -o pipefail
-S=32768x2304x768,32768x768x768,32768x3072x768,32768x768x3072
-timeout -k 10 200 python bench/gemm_bench.py --shapes $S --act none > gpurun_out/gemm_epi_none.jsonl 2>&1 &&
-timeout -k 10 200 python bench/gemm_bench.py --shapes $S --act gelu > gpurun_out/gemm_epi_gelu.jsonl 2>&1
-rc=$?; cat gpurun_out/gemm_epi_*.jsonl | grep '^{'; exit $rc
+N768=32768x768x768,32768x768x3072
+timeout -k 10 120 python bench/gemm_bench.py --shapes 32768x3072x768,$N768 --act none --torch > gpurun_out/ge.jsonl 2>&1 &&
+timeout -k 10 120 python bench/gemm_bench.py --shapes 32768x3072x768 --act gelu >> gpurun_out/ge.jsonl 2>&1 &&
+timeout -k 10 120 python bench/gemm_bench.py --shapes $N768 --residual >> gpurun_out/ge.jsonl 2>&1 &&
+timeout -k 10 120 python bench/gemm_bench.py --shapes $N768 --inplace >> gpurun_out/ge.jsonl 2>&1 &&
+timeout -k 10 120 python bench/gemm_bench.py --shapes 32768x3072x768,$N768 --act none >> gpurun_out/ge.jsonl 2>&1
+rc=$?; grep '^{' gpurun_out/ge.jsonl; exit $rc
