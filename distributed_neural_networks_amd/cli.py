@@ -15,6 +15,9 @@ Transports (config ``transport``):
   move with ``torch.distributed`` P2P (RCCL over xGMI on MI355X, gloo on CPU);
   the last stage returns predictions over the back-edge to
   ``return_to_node_id`` (resolved but unused in the reference, ``node.py:272-277``).
+  With config ``replicas`` = R the pipeline runs as R data-parallel copies
+  (``--replica r``, rank = r * num_parts + part_index, one GPU each): copy r
+  serves requests r, r+R, ... (CIFAR) or its own batch of sequences (GPT/Llama).
 """
 from __future__ import annotations
 
@@ -49,6 +52,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--trace", default=None, help="write a Chrome trace (host + device spans) to this path")
     p.add_argument("--metrics", action="store_true", help="print one METRICS json line per stage at exit")
+    p.add_argument("--replica", type=int, default=None,
+                   help="data-parallel copy of the pipeline this process serves (config 'replicas'; "
+                        "default: $DNN_REPLICA, else RANK // num_parts under torchrun, else 0)")
     p.add_argument("--dump_result", default=None,
                    help="stage 0 (grpc): save the final result tensor of the last request as .npy")
     return p
@@ -117,8 +123,10 @@ def pick_device(ctx: NodeContext, override: Optional[str]) -> torch.device:
         return torch.device(override)
     if torch.cuda.is_available() and ctx.pipeline.transport != "gloo":
         idx = ctx.node.device if ctx.node.device is not None else 0
-        if ctx.pipeline.transport == "rccl" and ctx.node.device is None:
-            idx = ctx.part_index % torch.cuda.device_count()
+        if ctx.pipeline.transport == "rccl":
+            # one GPU per rank; replica r of a stage pinned to device d runs on d + r * num_parts
+            base = ctx.node.device if ctx.node.device is not None else ctx.part_index
+            idx = (base + ctx.replica * ctx.num_parts) % torch.cuda.device_count()
         return torch.device("cuda", idx)
     return torch.device("cpu")
 
@@ -358,7 +366,7 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     if backend == "gloo":
         device = torch.device("cpu")
     s0 = pipe.stage(0)
-    info = comm.init(backend, rank=ctx.part_index, world=ctx.num_parts, master_addr=s0.host,
+    info = comm.init(backend, rank=ctx.rank, world=ctx.world, master_addr=s0.host,
                      timeout_s=pipe.comm_timeout_s, master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
     ranges = stage_ranges(ctx)
     stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device, None, args)
@@ -367,7 +375,8 @@ def run_dist(ctx: NodeContext, args, device) -> int:
                   stall_timeout_s=pipe.stall_timeout_s, tag=f"[{nid}]")
     comm.barrier(info)
     wd.start()
-    log(f"[{nid}] rank {info.rank}/{info.world} ready on {info.device} (backend {backend})")
+    rep = f", replica {ctx.replica}" if pipe.replicas > 1 else ""
+    log(f"[{nid}] rank {info.rank}/{info.world} ready on {info.device} (backend {backend}{rep})")
     rc = 0
     try:
         wd.busy(True)
@@ -395,23 +404,26 @@ def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
     nid, pipe, dev = ctx.node_id, ctx.pipeline, info.device
     r, S = ctx.part_index, ctx.num_parts
     ret = pipe.by_id(pipe.return_to_node_id) if pipe.return_to_node_id else None
-    ret_rank = ret.part_index if ret is not None else 0
+    ret_part = ret.part_index if ret is not None else 0
     last = r == S - 1
-    links = ForwardLinks(prev=P2PLink(r - 1, dev) if r > 0 else None,
-                         nxt=P2PLink(r + 1, dev) if not last else None,
-                         ret_out=P2PLink(ret_rank, dev) if (last and ret_rank != r) else None,
-                         ret_in=P2PLink(S - 1, dev) if (r == ret_rank and not last) else None)
+    peer = ctx.peer  # ranks of this replica's stages
+    links = ForwardLinks(prev=P2PLink(peer(r - 1), dev) if r > 0 else None,
+                         nxt=P2PLink(peer(r + 1), dev) if not last else None,
+                         ret_out=P2PLink(peer(ret_part), dev) if (last and ret_part != r) else None,
+                         ret_in=P2PLink(peer(S - 1), dev) if (r == ret_part and not last) else None)
+    rep = f" (replica {ctx.replica})" if pipe.replicas > 1 else ""
 
     def on_result(role, tag, preds):
         if role == "last":
-            log(f"[{nid}] Final Prediction Index: {_fmt(preds)}")
+            log(f"[{nid}]{rep} Final Prediction Index: {_fmt(preds)}")
         else:
-            log(f"[{nid}] ***** FINAL PREDICTION (Index): {_fmt(preds)} *****")
+            log(f"[{nid}]{rep} ***** FINAL PREDICTION (Index): {_fmt(preds)} *****")
 
-    fp = ForwardPipeline(stage, links, r == 0, last, r == ret_rank, depth=2, progress=wd.beat, on_result=on_result)
+    fp = ForwardPipeline(stage, links, r == 0, last, r == ret_part, depth=2, progress=wd.beat, on_result=on_result)
     mbs, M = pipe.micro_batch_size, pipe.num_microbatches
     if r == 0:
-        for req in range(args.num_requests):
+        # data parallel: replica k serves requests k, k+R, k+2R, ... (the tag keeps the global number)
+        for req in range(ctx.replica, args.num_requests, pipe.replicas):
             x = cifar_request(args, nid, mbs * M, req).to(dev)
             fp.run_request(x, mbs, M, tag=req)
         fp.stop()
@@ -430,6 +442,22 @@ def _finish(args) -> None:
         log(f"[{args.node_id}] trace written to {p}")
 
 
+def _replica_arg(args) -> int:
+    """--replica, else $DNN_REPLICA, else (under torchrun) RANK // num_parts of the config, else 0."""
+    if args.replica is not None:
+        return args.replica
+    if os.environ.get("DNN_REPLICA"):
+        return int(os.environ["DNN_REPLICA"])
+    if "RANK" in os.environ:
+        try:
+            import json
+            n = int(json.load(open(args.config)).get("num_parts", 1))
+            return int(os.environ["RANK"]) // max(1, n)
+        except (OSError, ValueError):
+            return 0
+    return 0
+
+
 def main(argv=None) -> int:
     log("Script started...")
     args = build_parser().parse_args(argv)
@@ -440,7 +468,7 @@ def main(argv=None) -> int:
     nid = args.node_id
     log(f"Parsed Node ID: {nid}")
     try:
-        ctx = load_node(args.config, nid)
+        ctx = load_node(args.config, nid, _replica_arg(args))
         log(f"Loaded configuration from {args.config}")
         check_config_capacity(ctx, args)
     except ConfigError as e:

@@ -12,7 +12,7 @@ Behavioural contract (reference ``node.py:222-290``, ``config.json:1-18``):
 * Additive optional fields (absent in the reference file, so it still loads):
   top level ``model``, ``dtype``, ``transport``, ``micro_batch_size``,
   ``num_microbatches``, ``seq_len``, ``decode_steps``, ``prompt_len``, ``temperature``, ``top_k``,
-  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``; per node
+  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``, ``replicas``; per node
   ``layers: [start, end]`` (inclusive, as in
   ``partitions/gpt_model_parts.py:12``) and ``device``.
 
@@ -75,6 +75,7 @@ class PipelineConfig:
     comm_timeout_s: float = 300.0             # process-group (RCCL/gloo) op timeout
     heartbeat_timeout_s: float = 15.0         # parallel/watchdog.py: peer declared dead after this
     stall_timeout_s: Optional[float] = None   # parallel/watchdog.py: abort when this rank stops progressing
+    replicas: int = 1                         # data-parallel copies of the whole pipeline (rccl / gloo)
     raw: Dict[str, Any] = field(default_factory=dict)
 
     def stage(self, part_index: int) -> NodeSpec:
@@ -106,10 +107,24 @@ class NodeContext:
     next_address: Optional[str]
     return_address: Optional[str]
     pipeline: PipelineConfig
+    replica: int = 0  # which data-parallel copy of the pipeline this process serves
 
     @property
     def node(self) -> NodeSpec:
         return self.pipeline.stage(self.part_index)
+
+    @property
+    def rank(self) -> int:
+        """Process-group rank: replica-major, ``replica * num_parts + part_index``."""
+        return self.replica * self.num_parts + self.part_index
+
+    @property
+    def world(self) -> int:
+        return self.pipeline.replicas * self.num_parts
+
+    def peer(self, part_index: int) -> int:
+        """Rank of stage ``part_index`` of this process's own replica."""
+        return self.replica * self.num_parts + part_index
 
 
 def load_json(path: str) -> Dict[str, Any]:
@@ -174,6 +189,12 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         v = cfg.get(key)
         if v is not None and (not isinstance(v, (int, float)) or isinstance(v, bool) or v <= 0):
             raise ConfigError(f"ERROR: '{key}' must be a positive number of seconds, got {v!r}")
+    reps = cfg.get("replicas", 1)
+    if not isinstance(reps, int) or isinstance(reps, bool) or reps < 1:
+        raise ConfigError(f"ERROR: 'replicas' must be a positive integer, got {reps!r}")
+    if reps > 1 and transport not in ("rccl", "gloo"):
+        raise ConfigError(f"ERROR: 'replicas' > 1 needs transport 'rccl' or 'gloo' (one rank per stage and replica), "
+                          f"got '{transport}'")
     t = cfg.get("temperature", 0.0)
     if not isinstance(t, (int, float)) or t < 0:
         raise ConfigError(f"ERROR: 'temperature' must be >= 0, got {t!r}")
@@ -193,11 +214,13 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
         rpc_timeout_s=cfg.get("rpc_timeout_s"), health_timeout_s=float(cfg.get("health_timeout_s", 120.0)),
         comm_timeout_s=float(cfg.get("comm_timeout_s", 300.0)),
         heartbeat_timeout_s=float(cfg.get("heartbeat_timeout_s", 15.0)),
-        stall_timeout_s=(None if cfg.get("stall_timeout_s") is None else float(cfg["stall_timeout_s"])), raw=cfg)
+        stall_timeout_s=(None if cfg.get("stall_timeout_s") is None else float(cfg["stall_timeout_s"])),
+        replicas=int(reps), raw=cfg)
 
 
-def resolve_node(cfg: Dict[str, Any], node_id: str, path: str = "<config>") -> NodeContext:
-    """Own-node lookup + topology (``node.py:234-278``)."""
+def resolve_node(cfg: Dict[str, Any], node_id: str, path: str = "<config>", replica: int = 0) -> NodeContext:
+    """Own-node lookup + topology (``node.py:234-278``); ``replica`` selects the
+    data-parallel copy of the pipeline (config ``replicas``)."""
     mine = next((n for n in cfg.get("nodes", []) if n.get("id") == node_id), None)
     if not mine:
         raise ConfigError(f"ERROR: Node ID '{node_id}' not found in config file '{path}'")
@@ -226,13 +249,15 @@ def resolve_node(cfg: Dict[str, Any], node_id: str, path: str = "<config>") -> N
             ret = pipe.by_id(pipe.return_to_node_id)
             if ret is not None:
                 return_address = ret.address
+    if not (isinstance(replica, int) and 0 <= replica < pipe.replicas):
+        raise ConfigError(f"ERROR: replica {replica!r} out of range: the config has {pipe.replicas} replica(s)")
     return NodeContext(node_id=node_id, address=str(address), port=port, part_index=int(part_index),
                        num_parts=pipe.num_parts, model_weights=pipe.model_weights, is_last=is_last,
-                       next_address=next_address, return_address=return_address, pipeline=pipe)
+                       next_address=next_address, return_address=return_address, pipeline=pipe, replica=replica)
 
 
-def load_node(path: str, node_id: str) -> NodeContext:
-    return resolve_node(load_json(path), node_id, path)
+def load_node(path: str, node_id: str, replica: int = 0) -> NodeContext:
+    return resolve_node(load_json(path), node_id, path, replica)
 
 
 def banner(ctx: NodeContext, device: str) -> str:
@@ -248,6 +273,7 @@ def banner(ctx: NodeContext, device: str) -> str:
         f"  Return Node Addr: {ctx.return_address}",
         f"  Weights: {ctx.model_weights}",
         f"  Device: {device}",
-        f"  Model: {ctx.pipeline.model}  Transport: {ctx.pipeline.transport}",
+        f"  Model: {ctx.pipeline.model}  Transport: {ctx.pipeline.transport}"
+        + (f"  Replica: {ctx.replica} / {ctx.pipeline.replicas - 1}" if ctx.pipeline.replicas > 1 else ""),
         "-------------------------",
     ])

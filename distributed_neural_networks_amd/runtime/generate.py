@@ -29,15 +29,16 @@ from ..utils.log import log
 from .scheduler import DecodeRing, RingLinks
 
 
-def make_prompts(pipe, prompt: Optional[str]) -> torch.Tensor:
+def make_prompts(pipe, prompt: Optional[str], replica: int = 0) -> torch.Tensor:
     """(micro_batch_size * num_microbatches, T) int64 prompt ids: ``--prompt``
-    (comma-separated ids, replicated to every sequence) or seeded random ids."""
+    (comma-separated ids, replicated to every sequence) or seeded random ids
+    (each data-parallel replica draws its own batch)."""
     info = model_info(pipe.model)
     n = pipe.micro_batch_size * pipe.num_microbatches
     if prompt:
         ids = [int(v) for v in prompt.split(",") if v.strip()]
         return torch.tensor([ids], dtype=torch.int64).repeat(n, 1)
-    g = torch.Generator().manual_seed(1234)
+    g = torch.Generator().manual_seed(1234 + 7919 * replica)
     T = pipe.prompt_len or pipe.seq_len
     return torch.randint(0, info.cfg.vocab_size, (n, T), generator=g)
 
@@ -112,19 +113,20 @@ def run_generate_dist(ctx, args, stage, info, progress=None) -> int:
     from ..parallel.links import KIND_DATA, P2PLink
     pipe = ctx.pipeline
     S, r, dev = pipe.num_parts, ctx.part_index, info.device
+    peer = getattr(ctx, "peer", lambda p: p)  # ranks of this replica's stages
     if pipe.return_to_node_id and pipe.by_id(pipe.return_to_node_id) and \
             pipe.by_id(pipe.return_to_node_id).part_index != 0 and r == S - 1:
         log(f"[{ctx.node_id}] note: generated tokens feed the embedding, so they return to stage 0 "
             f"(return_to_node_id '{pipe.return_to_node_id}' is not stage 0)")
-    links = RingLinks(prev=P2PLink(r - 1, dev) if r > 0 else None,
-                      nxt=P2PLink(r + 1, dev) if r < S - 1 else None,
-                      back_out=P2PLink(0, dev) if (r == S - 1 and S > 1) else None,
-                      back_in=P2PLink(S - 1, dev) if (r == 0 and S > 1) else None)
+    links = RingLinks(prev=P2PLink(peer(r - 1), dev) if r > 0 else None,
+                      nxt=P2PLink(peer(r + 1), dev) if r < S - 1 else None,
+                      back_out=P2PLink(peer(0), dev) if (r == S - 1 and S > 1) else None,
+                      back_in=P2PLink(peer(S - 1), dev) if (r == 0 and S > 1) else None)
     M, B = pipe.num_microbatches, pipe.micro_batch_size
     steps = max(1, pipe.decode_steps or 1)
     prompts = None
     if r == 0:
-        prompt = make_prompts(pipe, args.prompt)
+        prompt = make_prompts(pipe, args.prompt, getattr(ctx, "replica", 0))
         T = prompt.shape[1]
         prompts = [prompt[m * B:(m + 1) * B] for m in range(M)]
     else:
@@ -135,5 +137,6 @@ def run_generate_dist(ctx, args, stage, info, progress=None) -> int:
     ring = DecodeRing([stage], links, S, M, B, progress=progress)
     pf, dec = _timed_generate(ring, prompts, T, steps, dev, pipe.prefill_chunk)
     if r == 0:
-        _report(ctx.node_id, ring.tokens(), pf, dec, B * M, T, steps, M, S)
+        nid = ctx.node_id + (f" replica {ctx.replica}" if getattr(pipe, "replicas", 1) > 1 else "")
+        _report(nid, ring.tokens(), pf, dec, B * M, T, steps, M, S)
     return 0

@@ -8,6 +8,10 @@ period), so a run never leaves orphan servers.
 
     python -m distributed_neural_networks_amd.tools.launch --config configs/cifar_2gpu_rccl.json \
         [--input_image img.png] [--num_requests N] [--prompt 1,2,3]
+
+With config ``replicas`` = R (rccl / gloo) it starts R copies of every stage
+(``--replica r``); copy 0's stage 0 is the process whose exit code is returned,
+the other copies' exit codes are checked too.
 """
 from __future__ import annotations
 
@@ -38,11 +42,24 @@ def main(argv=None) -> int:
     common = ["--config", a.config] + (["--quiet"] if a.quiet else [])
     transport = cfg.get("transport", "grpc")
     procs = []
+    reps = int(cfg.get("replicas", 1))
     if transport != "colocated":
         for n in nodes[1:]:
             extra = ["--serve_seconds", str(a.timeout)] if transport == "grpc" else []
             procs.append(subprocess.Popen([sys.executable, node_py, "--node_id", n["id"]] + common + extra, env=env))
     first = [sys.executable, node_py, "--node_id", nodes[0]["id"]] + common + ["--num_requests", str(a.num_requests)]
+    # data-parallel copies (config "replicas", rccl / gloo): every stage of copies 1..R-1, then copy 0 as below
+    for rep in range(1, reps):
+        for n in nodes[1:]:
+            procs.append(subprocess.Popen([sys.executable, node_py, "--node_id", n["id"], "--replica", str(rep)]
+                                          + common, env=env))
+        head = [sys.executable, node_py, "--node_id", nodes[0]["id"], "--replica", str(rep)] + common + \
+            ["--num_requests", str(a.num_requests)] + (["--input_image", a.input_image] if a.input_image else
+                                                      (["--input_image", "__dummy__.png"]
+                                                       if cfg.get("model", "cifar10") == "cifar10" else []))
+        if a.prompt:
+            head += ["--prompt", a.prompt]
+        procs.append(subprocess.Popen(head, env=env))
     if a.input_image:
         first += ["--input_image", a.input_image]
     elif cfg.get("model", "cifar10") == "cifar10":

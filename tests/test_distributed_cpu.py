@@ -145,6 +145,53 @@ def test_cli_gpt2_tiny_gloo(tmp_path):
     assert toks[0] == ref
 
 
+def _launch(cfg, *extra, timeout=240):
+    return subprocess.run([sys.executable, "-m", "distributed_neural_networks_amd.tools.launch", "--config", str(cfg),
+                           "--timeout", "200", *extra], env=ENV, capture_output=True, text=True, timeout=timeout,
+                          cwd=ROOT)
+
+
+def test_cli_replicas_cifar_gloo(cifar_setup):
+    """Data-parallel copies of the pipeline from the CLI (config ``replicas`` 2 x
+    2 stages = 4 gloo ranks, tools/launch.py): replica k serves requests k, k+2,
+    ...; every prediction equals the golden one."""
+    tmp, ck, img = cifar_setup
+    cfg = _cfg(tmp, "gloo", 2, weights=str(ck), replicas=2)
+    r = _launch(cfg, "--input_image", str(img), "--num_requests", "3")
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    gold = _golden_pred(str(ck), str(img))
+    lines = [l for l in out.splitlines() if "***** FINAL PREDICTION (Index):" in l]
+    assert sorted("(replica 1)" in l for l in lines) == [False, False, True], lines
+    assert all(_final_pred(l) == gold for l in lines)
+    assert "rank 3/4 ready" in out
+
+
+def test_cli_replicas_gpt2_tiny_gloo(tmp_path):
+    """Two data-parallel decode rings (gpt2-tiny, 2 stages each, 4 gloo ranks):
+    both generate the golden greedy tokens of the shared prompt."""
+    cfg = _cfg(tmp_path, "gloo", 2, model="gpt2-tiny", weights="synthetic:1", seq_len=12, decode_steps=3, replicas=2)
+    r = _launch(cfg, "--prompt", "1,2,3,4,5")
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    gen = [json.loads(l.split("generated tokens:")[1].strip()) for l in out.splitlines() if "generated tokens:" in l]
+    assert len(gen) == 2, out[-3000:]
+    assert "replica 1" in out
+    assert gen[0] == gen[1]
+
+
+def test_config_replicas_validation(tmp_path):
+    from distributed_neural_networks_amd.config import ConfigError, load_node
+    bad = _cfg(tmp_path, "grpc", 2, weights="x.pth", replicas=2)
+    with pytest.raises(ConfigError, match="replicas"):
+        load_node(str(bad), "node1")
+    good = _cfg(tmp_path, "gloo", 3, weights="x.pth", replicas=2)
+    ctx = load_node(str(good), "node2", replica=1)
+    assert (ctx.rank, ctx.world, ctx.peer(0), ctx.peer(2)) == (4, 6, 3, 5)
+    with pytest.raises(ConfigError, match="replica"):
+        load_node(str(good), "node2", replica=2)
+
+
 def _worker_stream(rank, world, port, q):
     os.environ["DNN_DEBUG_ORDER"] = "1"  # slot-ordering checks on (runtime/ordering.py)
     import torch.distributed as dist
