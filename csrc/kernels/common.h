@@ -45,6 +45,25 @@ __device__ __forceinline__ float gelu_erf(float x) {
   const float q = 0.5f * x * (p * t) * e;
   return x >= 0.f ? x - q : q;
 }
+// Two GELUs at once on packed fp32 math: the polynomial, the squares and the
+// products go through v_pk_fma_f32 / v_pk_mul_f32 (two lanes' worth per
+// instruction), only the reciprocal, the exponential, |x| and the sign select
+// stay per element — a GEMM epilogue applies it to 128 outputs per thread.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = f32x2{fabsf(x[0]), fabsf(x[1])} * 0.70710678118654752f;
+  const f32x2 d = z * 0.3275911f + 1.0f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 a = (z * z) * -1.44269504088896341f;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+  const f32x2 q = (x * 0.5f) * (p * t) * e;
+  return f32x2{x[0] >= 0.f ? x[0] - q[0] : q[0], x[1] >= 0.f ? x[1] - q[1] : q[1]};
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 // DPP lane moves (VALU, no LDS round trip — __shfl_xor lowers to

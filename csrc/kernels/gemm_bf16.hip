@@ -226,7 +226,8 @@ __device__ __forceinline__ void bg_read(bf16x8 (&f)[N][2], const char* half, int
 template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
-    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K) {
+    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
+    int res_pre) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
@@ -316,6 +317,32 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
+  // Residual epilogue: every residual load of the tile (32 x 8 B per lane, into
+  // the fragment registers the main loop no longer needs) is issued before the
+  // first output is computed, so the tile pays one memory round trip for R
+  // instead of one per output row group (-20..-25 % GEMM throughput otherwise,
+  // profiles/r2_gemm_epilogue_cost.jsonl).
+  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N) {
+    bf16x4 rr[2][2][4][2];
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          epi_pair_res_load(m0 + mq * 128 + arow + i * 16 + (lane & 15), n0 + nq * 128 + wc * 32, M, R, ldr, lane,
+                            rr[mq][nq][i][0], rr[mq][nq][i][1]);
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], m0 + mq * 128 + arow + i * 16 + (lane & 15),
+                                   n0 + nq * 128 + wc * 32, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, lane,
+                                   rr[mq][nq][i][0], rr[mq][nq][i][1]);
+    return;
+  }
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -519,6 +546,14 @@ using namespace dnn;
 // blocks), 128 / 256 force a tile (A/B benchmarking, tests).
 static int g_gemm_tile = 0;
 
+// 256^2 epilogue: residual rows loaded ahead of the outputs (1) or per output row group (0)
+static int g_res_prefetch = 1;
+
+extern "C" int dnn_gemm_set_res_prefetch(int on) {
+  g_res_prefetch = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int dnn_gemm_set_tile(int tile) {
   if (tile != 0 && tile != 128 && tile != 256) return -1;
   g_gemm_tile = tile;
@@ -550,7 +585,7 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
                    (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.4 * fill(tiles256, 256) > fill(tiles128, 512));
   if (big) {
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
-                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);
+                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch);
     return;
   }
   hipLaunchKernelGGL((gemm_bf16_tn_kernel<ACT, F32>), dim3(tiles128), dim3(256), 0, st, (const bf16_t*)A, lda,

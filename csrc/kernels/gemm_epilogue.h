@@ -26,10 +26,13 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
   if (vec && n + 3 < N) {
     if (colscale != nullptr) v *= *reinterpret_cast<const f32x4*>(colscale + n) * rowscale;
     if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + n);
+    if constexpr (ACT == ACT_GELU) {
+      const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+      v = f32x4{g0[0], g0[1], g1[0], g1[1]};
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (ACT == ACT_RELU) v[r] = fmaxf(v[r], 0.f);
-      if (ACT == ACT_GELU) v[r] = gelu_erf(v[r]);
     }
     if (R != nullptr) {
       const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
@@ -70,15 +73,32 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
 // stores (guide T21: the epilogue tail is store-issue bound).  Preconditions
 // (wave-uniform, checked by the caller): nb + 31 < N, 16-B aligned C/ldc and
 // bias, 8-B aligned R rows.  Every lane must call it (cross-lane swap).
-template <int ACT>
+// The residual rows of a pair, loaded ahead of the epilogue math (RES_PRE):
+// lane row q's 4 columns of each tile of the pair.
+__device__ __forceinline__ void epi_pair_res_load(int m, int nb, int M, const bf16_t* __restrict__ R, int ldr,
+                                                  int lane, bf16x4& r0, bf16x4& r1) {
+  const int n0 = nb + (lane >> 4) * 4;
+  const int mm = m < M ? m : M - 1;  // rows past M load a valid row (never stored)
+  r0 = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + n0);
+  r1 = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + n0 + 16);
+}
+
+template <int ACT, bool RES_PRE = false>
 __device__ __forceinline__ void epi_pair_bf16(f32x4 a0, f32x4 a1, int m, int nb, int M, bf16_t* __restrict__ C,
                                               int ldc, const float* __restrict__ bias,
-                                              const bf16_t* __restrict__ R, int ldr, int lane) {
+                                              const bf16_t* __restrict__ R, int ldr, int lane,
+                                              bf16x4 rp0 = bf16x4{}, bf16x4 rp1 = bf16x4{}) {
   const int q = lane >> 4;
   const int n0 = nb + q * 4, n1 = n0 + 16;
   if (bias != nullptr) {
     a0 += *reinterpret_cast<const f32x4*>(bias + n0);
     a1 += *reinterpret_cast<const f32x4*>(bias + n1);
+  }
+  if constexpr (ACT == ACT_GELU) {
+    const f32x2 g0 = gelu_erf2(f32x2{a0[0], a0[1]}), g1 = gelu_erf2(f32x2{a0[2], a0[3]});
+    const f32x2 g2 = gelu_erf2(f32x2{a1[0], a1[1]}), g3 = gelu_erf2(f32x2{a1[2], a1[3]});
+    a0 = f32x4{g0[0], g0[1], g1[0], g1[1]};
+    a1 = f32x4{g2[0], g2[1], g3[0], g3[1]};
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -86,14 +106,13 @@ __device__ __forceinline__ void epi_pair_bf16(f32x4 a0, f32x4 a1, int m, int nb,
       a0[r] = fmaxf(a0[r], 0.f);
       a1[r] = fmaxf(a1[r], 0.f);
     }
-    if (ACT == ACT_GELU) {
-      a0[r] = gelu_erf(a0[r]);
-      a1[r] = gelu_erf(a1[r]);
-    }
   }
-  if (R != nullptr && m < M) {
-    const bf16x4 r0 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n0);
-    const bf16x4 r1 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n1);
+  if (RES_PRE || (R != nullptr && m < M)) {
+    bf16x4 r0 = rp0, r1 = rp1;
+    if constexpr (!RES_PRE) {
+      r0 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n0);
+      r1 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n1);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       a0[r] += bf2f((bf16_t)r0[r]);
