@@ -1,0 +1,53 @@
+"""Interleaved in-process A/B of a decode-path switch (box-to-box clock
+differences cancel): bench/gpt_bench.py runs alternately with each variant's
+setting applied before the stages are built and captured.
+
+    python bench/decode_ab.py --switch skinny_max_m --values 32,64 [gpt_bench args...]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "bench"))
+
+
+def apply(switch: str, v: int) -> None:
+    from distributed_neural_networks_amd.ops import gemm
+    from distributed_neural_networks_amd.ops._lib import lib
+    if switch == "skinny_max_m":
+        gemm.set_skinny_max_m(v)
+    elif switch == "res_prefetch":
+        lib().gemm_set_res_prefetch(v)
+    else:
+        raise SystemExit(f"unknown switch {switch}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--switch", required=True)
+    ap.add_argument("--values", default="0,1")
+    ap.add_argument("--rounds", type=int, default=2)
+    a, rest = ap.parse_known_args()
+    import gpt_bench
+    vals = [int(v) for v in a.values.split(",")]
+    res = {v: [] for v in vals}
+    for _ in range(a.rounds):
+        for v in vals:
+            apply(a.switch, v)
+            g = gpt_bench.run(gpt_bench.parse(rest))
+            res[v].append((g["ms_per_step"], g["prefill_tokens_per_s"]))
+            torch.cuda.empty_cache()
+    out = {"switch": a.switch, "args": " ".join(rest)}
+    for v in vals:
+        out[f"{v}_decode_ms"] = min(r[0] for r in res[v])
+        out[f"{v}_prefill_tok_s"] = max(r[1] for r in res[v])
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

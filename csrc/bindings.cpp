@@ -56,6 +56,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
   m.def("gemm_set_res_prefetch", [](int on) { return dnn_gemm_set_res_prefetch(on); });
+  m.def("gemm_set_skinny_max_m", [](int m) { return dnn_gemm_set_skinny_max_m(m); });
   m.def("gemm_fp8_set_tile", [](int tile) { return dnn_gemm_fp8_set_tile(tile); });
   m.def("silu_mul_packed", [](u64 gu, int ld_in, u64 out, int ld_out, int M, int F, u64 st) {
     return dnn_silu_mul_packed(CP(gu), ld_in, P(out), ld_out, M, F, ST(st));

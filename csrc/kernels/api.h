@@ -10,6 +10,7 @@ int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int l
                   int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st, const void* Wsh = nullptr);
 int dnn_gemm_set_tile(int tile);
 int dnn_gemm_set_res_prefetch(int on);
+int dnn_gemm_set_skinny_max_m(int m);
 int dnn_gemm_fp8_set_tile(int tile);
 int dnn_gemm_fp8_256(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,
                      const void* R, int ldr, int M, int N, int Kb, int act, hipStream_t st);

@@ -489,6 +489,19 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
 
   const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
+  // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
+  const bool rpre = ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N;
+  bf16x4 rr[2][2][4][2];
+  if (rpre) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          epi_pair_res_load(m0 + mq * 128 + arow + i * 16 + (lane & 15), n0 + nq * 128 + wc * 32, M, R, ldr, lane,
+                            rr[mq][nq][i][0], rr[mq][nq][i][1]);
+  }
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -514,6 +527,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
         if (ACT == ACT_SILU_MUL) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) epi_silu_t4<false>(v[j], m, (nb + j * 16) / 2, M, N / 2, C, ldc, vec, lane);
+        } else if (rpre) {
+          epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane, rr[mq][nq][i][0],
+                                   rr[mq][nq][i][1]);
         } else if (pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane);
         } else {
@@ -546,6 +562,20 @@ using namespace dnn;
 // blocks), 128 / 256 force a tile (A/B benchmarking, tests).
 static int g_gemm_tile = 0;
 
+// Rows up to which every bf16 GEMM streams its weights on the skinny kernels
+// (A/B switch).  At M = 64 a wide-N head with warm weights runs faster on the
+// 128^2 MFMA tiles (GPT-2 50304 x 768: 28.3 -> 22.5 us, x 1600: 52.7 -> 33.6,
+// profiles/r2_head_probe.jsonl), but inside the decode step (weights cold behind
+// 1.27 GB of K/V) GPT-2 B=64 ran 0.588 -> 0.603 ms/step that way and GPT-2 XL
+// B=64 4.507 -> 4.493 (profiles/r2_decode_ab_skinny_max_m.jsonl): 64 stays.
+static int g_skinny_max_m = 64;
+
+extern "C" int dnn_gemm_set_skinny_max_m(int m) {
+  if (m < 0 || m > 64) return -1;
+  g_skinny_max_m = m;
+  return 0;
+}
+
 // 256^2 epilogue: residual rows loaded ahead of the outputs (1) or per output row group (0)
 static int g_res_prefetch = 1;
 
@@ -566,7 +596,7 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   // decode-sized: the weight-streaming skinny kernels (gemm_skinny.hip); medium
   // M (<= 256) too while the 128^2 tiles would not fill 3/4 of the CUs (same
   // rule as ops/gemm.py skinny_rows)
-  if (M <= 64 || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192)) {
+  if (M <= g_skinny_max_m || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192)) {
     dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh);
     return;
   }

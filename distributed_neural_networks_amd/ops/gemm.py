@@ -16,11 +16,25 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_SILU_MUL = 0, 1, 2, 3
 SKINNY_MAX_M = 256
 
 
-def skinny_rows(M: int, N: int) -> bool:
-    """Decode-sized GEMM -> the weight-streaming skinny kernels: M <= 64, or
-    medium M (<= 256, M split into 16-row tiles) while 128^2 tiles would not
-    fill 3/4 of the CUs (same rule as gemm_bf16.hip launch_gemm)."""
-    return M <= 64 or (M <= SKINNY_MAX_M and -(-M // 128) * -(-N // 128) < 192)
+SKINNY_ALWAYS_M = 64  # bf16: rows up to which the skinny kernels always run (gemm_bf16.hip g_skinny_max_m)
+
+
+def skinny_rows(M: int, N: int, w8: bool = False) -> bool:
+    """Decode-sized GEMM -> the weight-streaming skinny kernels: M <= 64 (always
+    for fp8 weights: W8A16 keeps bf16 activations in decode; bf16 per
+    ``set_skinny_max_m``), or medium M (<= 256, M split into 16-row tiles) while
+    128^2 tiles would not fill 3/4 of the CUs (same rule as gemm_bf16.hip
+    launch_gemm)."""
+    always = 64 if w8 else SKINNY_ALWAYS_M
+    return M <= always or (M <= SKINNY_MAX_M and -(-M // 128) * -(-N // 128) < 192)
+
+
+def set_skinny_max_m(m: int = 64) -> None:
+    """bf16 rows up to which every GEMM streams weights on the skinny kernels
+    (default 64, the maximum); lower values are A/B probes (bench/decode_ab.py)."""
+    global SKINNY_ALWAYS_M
+    check(lib().gemm_set_skinny_max_m(int(m)), "gemm_set_skinny_max_m")
+    SKINNY_ALWAYS_M = int(m)
 _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "silu_mul": ACT_SILU_MUL}
 
 
@@ -136,7 +150,7 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
     N = f.w.shape[0]
     if (not w8 and f.w.shape[1] != K) or x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise ValueError(f"linear_norm: x {tuple(x.shape)} {x.dtype} vs w {tuple(f.w.shape)}")
-    if not skinny_rows(M, N):
+    if not skinny_rows(M, N, w8):
         from .transformer_ops import layernorm, layernorm_q8
         if std_buf is None or ones is None:
             raise ValueError("linear_norm: large M needs std_buf and ones")

@@ -208,7 +208,7 @@ class TransformerStage(StageCompute):
     def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None):
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
-            if skinny_rows(x.shape[0], w.q.shape[0]):  # decode: weight-only fp8 (bf16 activations, no quantise launch)
+            if skinny_rows(x.shape[0], w.q.shape[0], w8=True):  # decode: weight-only fp8 (bf16 activations)
                 return linear_w8(x, w, b, act, residual, out)
             return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
         return linear(x, w, b, act, residual, out, w_shuf=w_shuf)
