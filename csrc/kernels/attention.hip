@@ -247,20 +247,41 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       const float m_new = fmaxf(m_i, mx * scale_log2);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
-      float rs = 0.f;
+      // exponent arguments, row sums and the O rescale on packed fp32 math
+      // (v_pk_fma / v_pk_add / v_pk_mul: two scores per instruction), only the
+      // exponentials per element — the softmax VALU work bounds hd 64
+      const f32x2 sl2 = f32x2{scale_log2, scale_log2}, negm = f32x2{-m_use, -m_use};
+      f32x2 rs2 = f32x2{0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[kt][g], scale_log2, -m_use));
-          sacc[kt][g] = pv;
-          rs += pv;
+        for (int g = 0; g < 16; g += 2) {
+          const f32x2 arg = f32x2{sacc[kt][g], sacc[kt][g + 1]} * sl2 + negm;
+          const f32x2 pv = f32x2{__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};
+          sacc[kt][g] = pv[0];
+          sacc[kt][g + 1] = pv[1];
+          rs2 += pv;
         }
+      float rs = rs2[0] + rs2[1];
       rs += __shfl_xor(rs, 32, 64);
       l_i = l_i * alpha + rs;
       m_i = m_new;
+      // hd 64 (VALU-bound): the running max rarely moves once the first blocks
+      // are in, so skip the rescale when it moved for no query of the wave
+      // (0.1120 -> 0.1104 ms on GPT-2 B=64 T=512); at hd 128 the branch costs
+      // more than it saves (1.174 -> 1.202 ms at T=4096), the rescale stays
+      // unconditional there (profiles/r2_flash_packed_softmax_ab.jsonl)
+      if (HD != 64 || !__all(alpha == 1.f)) {
+        const f32x2 a2 = f32x2{alpha, alpha};
 #pragma unroll
-      for (int i = 0; i < NDT; ++i) oacc[i] *= alpha;
+        for (int i = 0; i < NDT; ++i)
+#pragma unroll
+          for (int g = 0; g < 16; g += 2) {
+            const f32x2 o = f32x2{oacc[i][g], oacc[i][g + 1]} * a2;
+            oacc[i][g] = o[0];
+            oacc[i][g + 1] = o[1];
+          }
+      }
       // ---- O^T += V^T . P^T ----
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
