@@ -70,6 +70,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_cifar_stage0_x3(CFP(x), FP(out), CP(w1h), CP(w1l), CFP(b1), CP(w2h), CP(w2l), CFP(b2), B, grid,
                                ST(st));
   });
+  m.def("cifar_s0_set_wide_store", [](int on) { return dnn_cifar_s0_set_wide_store(on); });
   m.def("cifar_split3", [](u64 a, int lda, u64 o, int ldo, int M, int K, u64 st) {
     return dnn_cifar_split3(CFP(a), lda, P(o), ldo, M, K, ST(st));
   });

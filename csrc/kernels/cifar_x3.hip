@@ -109,6 +109,7 @@ __device__ __forceinline__ void resident_fence(const bf16x8 (&w)[N]) {
 
 using namespace x3;
 
+template <bool WIDE>
 __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
     const float* __restrict__ x, float* __restrict__ out, const bf16_t* __restrict__ w1h,
     const bf16_t* __restrict__ w1l, const float* __restrict__ b1, const bf16_t* __restrict__ w2h,
@@ -294,6 +295,29 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
         bf16x8 a0[4], a1[4];
         c2_issue<0>(b, a0);
         c2_step<0>(b, w2hf, w2lf, acc, a0, a1);
+        if constexpr (WIDE) {
+          // 16-B stores: lane half h holds pooled columns 4i+2h..+1 of both
+          // tiles; one v_permlane32_swap per dword gives half 0 columns 0-3
+          // (its own tile-0 pair + the other half's) and half 1 columns 4-7,
+          // so a row leaves as one dwordx4 per lane instead of two dwordx2
+#pragma unroll
+          for (int qy = 0; qy < 2; ++qy) {
+            const int g0 = (2 * qy) * 4;
+            float v[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              v[i][0] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
+              v[i][1] = fmaxf(fmaxf(fmaxf(acc[i][g0 + 2], acc[i][g0 + 3]), fmaxf(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
+                              0.f);
+            }
+            const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][0]), __float_as_uint(v[1][0]), false,
+                                                             false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][1]), __float_as_uint(v[1][1]), false,
+                                                             false);
+            const int PY = 2 * ty2 + qy;
+            *reinterpret_cast<uint4*>(ob + PY * 8 + 4 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          }
+        } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -306,6 +330,7 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
             const int PY = 2 * ty2 + qy, PX = 4 * i + 2 * h;
             *reinterpret_cast<float2*>(ob + PY * 8 + PX) = pv;
           }
+        }
         }
       }
     };
@@ -574,13 +599,26 @@ __global__ __launch_bounds__(256) void cifar_head_tail_x3_kernel(const float* __
 
 using namespace dnn;
 
+// stage-0 boundary stores: 16-B (permlane32-paired, 1) or 8-B (0); A/B switch
+static int g_s0_wide_store = 1;
+
+extern "C" int dnn_cifar_s0_set_wide_store(int on) {
+  g_s0_wide_store = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, const void* w1l, const float* b1,
                                    const void* w2h, const void* w2l, const float* b2, int B, int grid,
                                    hipStream_t st) {
   if (B <= 0) return 0;
   if (grid <= 0) grid = 256;
   if (grid > B) grid = B;
-  hipLaunchKernelGGL(cifar_stage0_x3_kernel, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
+  if (g_s0_wide_store) {
+    hipLaunchKernelGGL(cifar_stage0_x3_kernel<true>, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
+                       (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(cifar_stage0_x3_kernel<false>, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
                      (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
   return (int)hipGetLastError();
 }
