@@ -23,6 +23,8 @@ def apply(switch: str, v: int) -> None:
         gemm.set_skinny_max_m(v)
     elif switch == "res_prefetch":
         lib().gemm_set_res_prefetch(v)
+    elif switch == "fold_norm":
+        gemm.FOLD_NORM_PREFILL = bool(v)
     else:
         raise SystemExit(f"unknown switch {switch}")
 

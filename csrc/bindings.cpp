@@ -25,12 +25,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("gemm_bf16", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N,
-                        int K, int act, int out_f32, u64 st, u64 wsh) {
+                        int K, int act, int out_f32, u64 st, u64 wsh, u64 rowstat, u64 colsum) {
     return dnn_gemm_bf16(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, out_f32, ST(st),
-                         CP(wsh));
+                         CP(wsh), CFP(rowstat), CFP(colsum));
   }, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
      py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"), py::arg("out_f32"),
-     py::arg("st"), py::arg("wsh") = 0);
+     py::arg("st"), py::arg("wsh") = 0, py::arg("rowstat") = 0, py::arg("colsum") = 0);
   m.def("gemm_skinny", [](u64 A, int lda, u64 sa, u64 W, int ldw, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr,
                           int M, int N, int K, int act, int out_f32, int fp8, u64 st) {
     return dnn_gemm_skinny(CP(A), lda, CFP(sa), CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act,
@@ -85,6 +85,9 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_cifar_head_tail(CP(hid), CP(w2p), CFP(b2), FP(probs), IP(pred), B, ST(st));
   });
 #ifdef DNN_HAVE_TRANSFORMER
+  m.def("row_stats", [](u64 x, int ldx, u64 stats, int M, int N, float eps, int rms, u64 st) {
+    return dnn_row_stats(CP(x), ldx, FP(stats), M, N, eps, rms, ST(st));
+  });
   m.def("layernorm", [](u64 x, int ldx, u64 w, u64 b, u64 y, int ldy, int M, int N, float eps, int rms, u64 st) {
     return dnn_layernorm(CP(x), ldx, CFP(w), CFP(b), P(y), ldy, M, N, eps, rms, ST(st));
   });

@@ -7,7 +7,9 @@
 
 extern "C" {
 int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias, const void* R,
-                  int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st, const void* Wsh = nullptr);
+                  int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st, const void* Wsh = nullptr,
+                  const float* rowstat = nullptr, const float* colsum = nullptr);
+int dnn_row_stats(const void* x, int ldx, float* stats, int M, int N, float eps, int rms, hipStream_t st);
 int dnn_gemm_set_tile(int tile);
 int dnn_gemm_set_res_prefetch(int on);
 int dnn_gemm_set_skinny_max_m(int m);

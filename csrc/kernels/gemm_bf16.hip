@@ -69,7 +69,8 @@ __device__ __forceinline__ void tile_coords(int logical, int ntm, int ntn, int& 
 template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
-    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K) {
+    int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
+    const float2* __restrict__ rowstat, const float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(16))) char smem[4 * G_TILE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + GB_N - 1) / GB_N, ntm = (M + GB_M - 1) / GB_M;
@@ -124,6 +125,14 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
 
   // Epilogue (transposed accumulators): lane holds row m = .. + (lane&15), cols n..n+3.
+  if (rowstat != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = epi_norm4(acc[i][j], m0 + wm * 64 + i * 16 + (lane & 15), n0 + wn * 64 + j * 16 + (lane >> 4) * 4,
+                              M, N, rowstat, colsum);
+  }
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
 #pragma unroll
@@ -227,7 +236,7 @@ template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
     int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
-    int res_pre) {
+    int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
@@ -315,6 +324,39 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   // Epilogue (transposed accumulators):
   //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
   //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
+  if (rowstat != nullptr) {  // folded pre-norm (prefill QKV / up projections)
+    // 8 row statistics and 4 column-sum vectors per lane, loaded once
+    float2 rs[2][4];
+    f32x4 cs[2][2];
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rs[mq][i] = rowstat[min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1)];
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
+        cs[nq][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (colsum != nullptr) {
+          if (n + 3 < N) {
+            cs[nq][j] = *reinterpret_cast<const f32x4*>(colsum + n);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[nq][j][r] = n + r < N ? colsum[n + r] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq][nq][i][j] = acc[mq][nq][i][j] * rs[mq][i].x + rs[mq][i].y * cs[nq][j];
+  }
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
   // Residual epilogue: every residual load of the tile (32 x 8 B per lane, into
@@ -592,11 +634,15 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
-                        const void* R, int ldr, int M, int N, int K, hipStream_t st, const void* Wsh) {
+                        const void* R, int ldr, int M, int N, int K, hipStream_t st, const void* Wsh,
+                        const float2* rowstat, const float* colsum) {
   // decode-sized: the weight-streaming skinny kernels (gemm_skinny.hip); medium
   // M (<= 256) too while the 128^2 tiles would not fill 3/4 of the CUs (same
   // rule as ops/gemm.py skinny_rows)
-  if (M <= g_skinny_max_m || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192)) {
+  // (a folded-norm GEMM (rowstat) always takes the tile kernels: the skinny
+  // path folds its norm itself, dnn_gemm_skinny_norm)
+  if (rowstat == nullptr &&
+      (M <= g_skinny_max_m || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192))) {
     dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh);
     return;
   }
@@ -615,22 +661,28 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
                    (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.4 * fill(tiles256, 256) > fill(tiles128, 512));
   if (big) {
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
-                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch);
+                       (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch, rowstat,
+                       colsum);
     return;
   }
   hipLaunchKernelGGL((gemm_bf16_tn_kernel<ACT, F32>), dim3(tiles128), dim3(256), 0, st, (const bf16_t*)A, lda,
-                     (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K);
+                     (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, rowstat, colsum);
 }
 
+// rowstat (M float2 {rstd, -mean rstd}) / colsum (N floats, LayerNorm only):
+// folded pre-norm epilogue, v = rstd acc - mean rstd colsum, before bias / act /
+// residual (ops/gemm.py linear_norm at prefill sizes); nullptr = plain GEMM.
 extern "C" int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                              const void* R, int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st,
-                             const void* Wsh) {
+                             const void* Wsh, const float* rowstat, const float* colsum) {
   if (K % 64 != 0 || M <= 0 || N <= 0) return -1;
-#define DISPATCH(a)                                                                     \
-  if (act == a) {                                                                       \
-    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh); \
-    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh);        \
-    return (int)hipGetLastError();                                                      \
+  if (colsum != nullptr && rowstat == nullptr) return -1;
+  const float2* rs = reinterpret_cast<const float2*>(rowstat);
+#define DISPATCH(a)                                                                                  \
+  if (act == a) {                                                                                    \
+    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum); \
+    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum);        \
+    return (int)hipGetLastError();                                                                   \
   }
   DISPATCH(ACT_NONE)
   DISPATCH(ACT_RELU)

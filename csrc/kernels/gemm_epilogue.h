@@ -15,6 +15,26 @@ __device__ __forceinline__ bool epi_vec_ok(const void* C, int ldc, const float* 
   return ((ldc | (R != nullptr ? ldr : 0)) & 3) == 0 && (p & 15) == 0;
 }
 
+// Folded pre-norm on an accumulator (prefill GEMMs after ops/gemm.py
+// fold_norm): v = rstd[m] * v - mean[m] rstd[m] * colsum[n..n+3], rowstat[m] =
+// {rstd, -mean * rstd} (RMSNorm: shift 0, no colsum) from row_stats_kernel.
+__device__ __forceinline__ f32x4 epi_norm4(f32x4 v, int m, int n, int M, int N, const float2* __restrict__ rowstat,
+                                           const float* __restrict__ colsum) {
+  const float2 st = rowstat[m < M ? m : M - 1];
+  v *= st.x;
+  if (colsum != nullptr) {
+    f32x4 cs;
+    if (n + 3 < N) {
+      cs = *reinterpret_cast<const f32x4*>(colsum + n);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[r] = n + r < N ? colsum[n + r] : 0.f;
+    }
+    v += st.y * cs;
+  }
+  return v;
+}
+
 //
 // Optional dequant scales (fp8 kernels): v *= rowscale * colscale[n..n+3].
 template <int ACT, bool OUT_F32>

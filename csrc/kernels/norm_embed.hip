@@ -90,6 +90,46 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x,
   }
 }
 
+// Row statistics only (prefill LayerNorm / RMSNorm folded into the next GEMM,
+// ops/gemm.py linear_norm): one wave per row, the row in registers, two-pass
+// mean / variance (no E[x^2] - mean^2 cancellation); writes {rstd, -mean rstd}
+// per row (RMS: {rstd, 0}).  Reads the activation once and writes 8 B per row
+// instead of the normalised copy the norm kernel writes and the GEMM re-reads.
+template <int NC, bool RMS>
+__global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict__ x, int ldx, float2* __restrict__ st,
+                                                        int M, int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  float v[NC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+      const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = RMS ? 0.f : wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / N + eps);
+  if (lane == 0) st[row] = make_float2(rstd, -mean * rstd);
+}
+
 // Normalise + quantise in one pass (fp8 prefill): the normalised row (fp32,
 // still in registers) is scaled by its own amax/448 and written as OCP e4m3
 // with the K padding zeroed, plus the per-row scale — the layout
@@ -208,6 +248,23 @@ extern "C" int dnn_layernorm(const void* x, int ldx, const float* w, const float
     else hipLaunchKernelGGL((norm_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b, (bf16_t*)y,   \
                             ldy, M, N, eps);                                                                        \
     return (int)hipGetLastError();                                                                                  \
+  }
+  L(1) L(2) L(4) L(8) L(16)
+#undef L
+  return -1;
+}
+
+extern "C" int dnn_row_stats(const void* x, int ldx, float* stats, int M, int N, float eps, int rms, hipStream_t st) {
+  if (N % 8 != 0 || N > 8192 || M <= 0) return M <= 0 ? 0 : -1;
+  const int nc = (N / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), blk(256);
+#define L(NCV)                                                                                                       \
+  if (nc <= NCV) {                                                                                                   \
+    if (rms) hipLaunchKernelGGL((row_stats_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx,             \
+                                reinterpret_cast<float2*>(stats), M, N, eps);                                        \
+    else hipLaunchKernelGGL((row_stats_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx,                \
+                            reinterpret_cast<float2*>(stats), M, N, eps);                                            \
+    return (int)hipGetLastError();                                                                                   \
   }
   L(1) L(2) L(4) L(8) L(16)
 #undef L

@@ -40,8 +40,12 @@ _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` on the skinny path (``skinny_rows``)."""
+           out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None,
+           rowstat: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` on the skinny path (``skinny_rows``).
+    ``rowstat`` ((M, 2) fp32 from ``transformer_ops.row_stats``) / ``colsum``: a
+    folded pre-norm applied in the epilogue, ``rstd (x W^T) - mean rstd colsum``
+    (MFMA tile kernels only)."""
     a = _ACTS[act] if not isinstance(act, int) else act
     x2 = x.reshape(-1, x.shape[-1]) if x.dim() != 2 else x
     M, K = x2.shape
@@ -65,9 +69,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         r2 = residual.reshape(-1, residual.shape[-1]) if residual.dim() != 2 else residual
     if w_shuf is not None and w_shuf.numel() * w_shuf.element_size() != -(-N // 16) * 16 * K * 2:
         raise ValueError("linear: w_shuf is not shuffle_weight(w)")
+    if rowstat is not None and (rowstat.dtype != torch.float32 or rowstat.numel() < 2 * M
+                                or not rowstat.is_contiguous()):
+        raise ValueError("linear: rowstat must be contiguous fp32 (M, 2)")
+    if colsum is not None and (rowstat is None or colsum.dtype != torch.float32 or colsum.numel() < N):
+        raise ValueError("linear: colsum needs rowstat and N fp32 entries")
     check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
                           ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
-                          1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf)), "gemm_bf16")
+                          1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf), ptr(rowstat),
+                          ptr(colsum)), "gemm_bf16")
     return out
 
 
@@ -90,6 +100,7 @@ def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
 
 
 NORM_RMS, NORM_LN = 1, 2
+FOLD_NORM_PREFILL = True  # prefill (non-skinny) folded norms: row statistics + GEMM epilogue (A/B switch)
 
 
 class FoldedLinear:
@@ -159,9 +170,18 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
             kp = f.w.q.shape[1]
             layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
             return linear_fp8(x, f.w, f.bias, a, residual, out, q8, s8, prequantized=True)
-        xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
         if w8:
+            xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
             return linear_fp8(xs[:M], f.w, f.bias, a, residual, out, q8, s8)
+        if FOLD_NORM_PREFILL:
+            # statistics only (8 B per row, carved from the front of std_buf), the
+            # norm applied in the GEMM epilogue on the raw activations: no
+            # normalised copy written and re-read (profiles/r2_prefill_fold_norm_ab.jsonl)
+            from .transformer_ops import row_stats
+            st = std_buf.reshape(-1)[:4 * M].view(torch.float32).view(M, 2)
+            row_stats(x, st, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+            return linear(x, f.w, f.bias, a, residual, out, rowstat=st, colsum=f.colsum)
+        xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
         return linear(xs[:M], f.w, f.bias, a, residual, out)
     if w8:
         return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps)

@@ -37,6 +37,22 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: 
     return out
 
 
+def row_stats(x: torch.Tensor, stats: torch.Tensor, eps: float = 1e-5, rms: bool = False, rows: Optional[int] = None,
+              ldx: Optional[int] = None) -> torch.Tensor:
+    """Per-row {rstd, -mean * rstd} (fp32 (M, 2); RMSNorm: {rstd, 0}) of a bf16
+    (M, N) activation: the statistics a folded-norm GEMM applies in its epilogue."""
+    _bf16_2d(x, "row_stats")
+    N = x.shape[-1]
+    M = rows if rows is not None else x.numel() // N
+    ldx = ldx if ldx is not None else N
+    if stats.dtype != torch.float32 or stats.numel() < 2 * M or not stats.is_contiguous():
+        raise ValueError("row_stats: stats must be contiguous fp32 with 2 * M entries")
+    if N % 8 or N > 8192:
+        raise ValueError(f"row_stats: unsupported width {N}")
+    check(lib().row_stats(ptr(x), ldx, ptr(stats), M, N, eps, 1 if rms else 0, stream_ptr()), "row_stats")
+    return stats
+
+
 def layernorm_q8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_out: torch.Tensor,
                  s_out: torch.Tensor, kpad: int, eps: float = 1e-5, rms: bool = False, rows: Optional[int] = None,
                  ldx: Optional[int] = None) -> torch.Tensor:

@@ -608,7 +608,7 @@ def test_stage_decode_with_and_without_shuffled_weights(monkeypatch):
     assert _rel(outs[1], outs[0]) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 16, 64, 100])
+@pytest.mark.parametrize("M", [1, 16, 64, 100, 1000])
 @pytest.mark.parametrize("w8", [False, True])
 def test_linear_norm_large_mean(M, w8):
     """LayerNorm folded into the GEMM on rows with |mean| / std >= 50: the fused
@@ -618,6 +618,7 @@ def test_linear_norm_large_mean(M, w8):
     from distributed_neural_networks_amd.ops.gemm import fold_norm, linear_norm
     if w8 and M > 64:
         pytest.skip("W8 fused norm is the decode (M <= 64) path")
+    # M = 1000: the prefill path (row statistics + folded-norm GEMM epilogue)
     torch.manual_seed(9)
     K, N = 768, 1024
     x = (64.0 + torch.randn(M, K, device=DEV)).bfloat16()  # mean 64, std ~1 (ratio 64)
@@ -743,3 +744,44 @@ def test_decode_ring_lanes_match_one_stream(model):
     assert ref.shape == (M * B, steps)
     for k, v in toks.items():
         assert torch.equal(v, ref), k
+
+
+@pytest.mark.parametrize("M,N,K,rms,act", [(1000, 2304, 768, False, "none"), (700, 3072, 768, False, "gelu"),
+                                           (600, 2 * 1024, 512, True, "silu_mul"), (4096, 768, 768, False, "none")])
+def test_linear_norm_prefill_fold_vs_normalised_copy(M, N, K, rms, act):
+    """Prefill linear_norm: the folded path (row statistics + GEMM epilogue) vs
+    the normalised-copy path (norm kernel + plain GEMM), both vs fp32 torch."""
+    from distributed_neural_networks_amd.ops import gemm as G
+    torch.manual_seed(M + N)
+    x = (torch.randn(M, K, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = None if rms else torch.randn(K, device=DEV) * 0.1
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = None if act == "silu_mul" else torch.randn(N, device=DEV) * 0.1
+    xf = x.float()
+    if rms:
+        xn = xf * torch.rsqrt(xf.pow(2).mean(1, keepdim=True) + 1e-5) * gamma
+    else:
+        xn = F.layer_norm(xf, (K,), gamma, beta, 1e-5)
+    y = xn @ W.t() + (bias if bias is not None else 0)
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "silu_mul":
+        from distributed_neural_networks_amd.ops.gemm import pack_gate_up
+        Wp = pack_gate_up(W[:N // 2].cpu(), W[N // 2:].cpu()).to(DEV)
+        g, u = (xn @ W[:N // 2].t()), (xn @ W[N // 2:].t())
+        y = F.silu(g) * u
+        W = Wp
+    f = G.fold_norm(W, gamma, beta, bias, rms, 1e-5, DEV)
+    std = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    ones = torch.ones(K, device=DEV)
+    outs = {}
+    for fold in (True, False):
+        G.FOLD_NORM_PREFILL = fold
+        try:
+            outs[fold] = G.linear_norm(x, f, act=act, std_buf=std, ones=ones).float()
+        finally:
+            G.FOLD_NORM_PREFILL = True
+    torch.cuda.synchronize()
+    assert _rel(outs[True], y) < 1.5e-2, _rel(outs[True], y)
+    assert _rel(outs[False], y) < 1.5e-2
