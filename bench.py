@@ -15,8 +15,9 @@ fresh launches; nothing is cached across steps.
 
 Placements:
 * N = 1: both stages colocated on the GPU, one HIP graph per step; extra keys:
-  the bf16 pipeline and the GPT-2 small 4-stage pipeline (decode / prefill
-  tokens/s, p50 per-token latency; bench/gpt_bench.py).
+  the bf16 pipeline, the GPT-2 small 4-stage pipeline (decode / prefill
+  tokens/s, p50 per-token latency; bench/gpt_bench.py) and BASELINE configs 4
+  and 5 colocated (Llama-3 8B bf16 8-stage B=32, GPT-2 XL fp8 8-stage B=64).
 * N > 1 (one process per GPU, RCCL): ``linear`` (default) — the reference
   topology, one stage per GPU, isend/irecv over the direct xGMI links; the
   bottleneck stage is replicated (``parallel/partition.py::linear_plan``: n0
@@ -61,6 +62,8 @@ def parse():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="compute precision of the headline (fp32 = the reference's)")
     ap.add_argument("--no_extra", action="store_true", help="skip the extra bf16 / GPT-2 keys")
+    ap.add_argument("--no_big", action="store_true",
+                    help="skip the Llama-3 8B / GPT-2 XL extra keys (BASELINE configs 4 and 5)")
     ap.add_argument("--model", default="cifar10")
     ap.add_argument("--latency_iters", type=int, default=200)
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
@@ -349,6 +352,30 @@ def extra_keys(args, info):
         g = gpt_bench.run(ga)
         out["gpt2_4stage_b256_decode_tok_s"] = g["value"]
         out["gpt2_4stage_b256_decode_ms_per_step"] = g["ms_per_step"]
+    if getattr(args, "gpt", True) and not args.no_big:
+        # BASELINE.json configs 4 and 5 on this GPU (all stages colocated): Llama-3
+        # 8B bf16 8-stage microbatched decode and GPT-2 XL 8-stage with fp8
+        # weights; a failure only drops these keys
+        for key, argv, cfg in (
+                ("llama3_8b_8stage_b32", ["--model", "llama3-8b", "--stages", "8", "--batch", "32", "--prompt", "512",
+                                          "--dtype", "bf16"],
+                 {"model": "llama3-8b (random init)", "stages": 8, "dtype": "bf16", "micro_batch": 32,
+                  "prompt_len": 512}),
+                ("gpt2xl_fp8_8stage_b64", ["--model", "gpt2-xl", "--stages", "8", "--batch", "64", "--prompt", "512",
+                                           "--dtype", "fp8"],
+                 {"model": "gpt2-xl (random init)", "stages": 8,
+                  "dtype": "fp8-e4m3 weights (W8A16 decode, W8A8 prefill), bf16 activations", "micro_batch": 64,
+                  "prompt_len": 512})):
+            try:
+                g = gpt_bench.run(gpt_bench.parse(["--gpus", "1", "--steps", "16", "--warmup", "2",
+                                                   "--prefill_iters", "1"] + argv))
+                out[key + "_decode_tok_s"] = g["value"]
+                out[key + "_decode_ms_per_step"] = g["ms_per_step"]
+                out[key + "_prefill_tok_s"] = g["prefill_tokens_per_s"]
+                out[key + "_config"] = dict(cfg, decode_steps_timed=16, placement="8 stages colocated on 1 GPU")
+            except Exception as e:  # noqa: BLE001
+                out[key + "_error"] = f"{type(e).__name__}: {e}"[:200]
+            torch.cuda.empty_cache()
     if args.precision == "fp32":
         import copy
         a = copy.copy(args)
