@@ -66,6 +66,57 @@ def test_gemm_bf16_256_tile(M, N, K, act):
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(4400, 4208, 192), (4352, 4352, 768), (8192, 768, 768)])
+@pytest.mark.parametrize("epi", ["res", "gelu", "silu_mul", "norm"])
+def test_gemm_bf16_256_persistent(M, N, K, epi):
+    """More 256^2 tiles than CUs: the persistent grid (each workgroup walks several
+    tiles, the next tile's prologue DMA issued before this tile's epilogue) vs the
+    fp32 reference, and bit-identical to one workgroup per tile."""
+    from distributed_neural_networks_amd.ops._lib import lib
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    rowstat = colsum = None
+    kw = {}
+    if epi == "norm":  # folded pre-norm epilogue: v = rstd acc - mean rstd colsum
+        mean, rstd = torch.randn(M, device=DEV), torch.rand(M, device=DEV) + 0.5
+        rowstat = torch.stack([rstd, -mean * rstd], 1).contiguous()
+        colsum = torch.randn(N, device=DEV)
+        kw = dict(rowstat=rowstat, colsum=colsum)
+    outs = []
+    set_gemm_tile(256)
+    try:
+        for persist in (2, 0):  # always persistent, never
+            lib().gemm_set_persist(persist)
+            if epi == "silu_mul":
+                outs.append(linear(x, w, act="silu_mul"))
+            elif epi == "gelu":
+                outs.append(linear(x, w, b, act="gelu"))
+            elif epi == "res":
+                outs.append(linear(x, w, b, residual=r))
+            else:
+                outs.append(linear(x, w, b, **kw))
+        torch.cuda.synchronize()
+    finally:
+        lib().gemm_set_persist(1)
+        set_gemm_tile(0)
+    assert torch.equal(outs[0], outs[1])
+    ref = x.float() @ w.float().t()
+    if epi == "silu_mul":
+        g = ref.view(M, N // 16, 2, 8)
+        ref = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, N // 2)
+    elif epi == "gelu":
+        ref = torch.nn.functional.gelu(ref + b)
+    elif epi == "res":
+        ref = ref + b + r.float()
+    else:
+        ref = ref * rowstat[:, :1] + rowstat[:, 1:] * colsum + b
+    assert _rel(outs[0], ref) < 1e-2
+
+
 def test_gemm_256_asymmetric_layout():
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     n = 512
