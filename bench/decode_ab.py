@@ -25,6 +25,9 @@ def apply(switch: str, v: int) -> None:
         lib().gemm_set_res_prefetch(v)
     elif switch == "fold_norm":
         gemm.FOLD_NORM_PREFILL = bool(v)
+    elif switch == "argmax_split":
+        from distributed_neural_networks_amd.ops import transformer_ops
+        transformer_ops.ARGMAX_SPLIT = bool(v)
     else:
         raise SystemExit(f"unknown switch {switch}")
 

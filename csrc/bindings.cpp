@@ -126,10 +126,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_sample_topk(CP(x), ld, M, N, reinterpret_cast<int*>(out), temperature, topk, seed,
                            reinterpret_cast<const int*>(step), ST(st));
   });
-  m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st, u64 out2, u64 pos_inc) {
-    return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st), IP(out2), IP(pos_inc));
+  m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st, u64 out2, u64 pos_inc, u64 part) {
+    return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st), IP(out2), IP(pos_inc), reinterpret_cast<void*>(static_cast<uintptr_t>(part)));
   }, py::arg("x"), py::arg("ld"), py::arg("M"), py::arg("N"), py::arg("out"), py::arg("f32in"), py::arg("st"),
-     py::arg("out2") = 0, py::arg("pos_inc") = 0);
+     py::arg("out2") = 0, py::arg("pos_inc") = 0, py::arg("part") = 0);
   m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, int kpad, u64 st) {
     return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, kpad, ST(st));
   });

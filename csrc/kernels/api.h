@@ -62,7 +62,7 @@ int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int 
 int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float temperature, int topk, unsigned seed,
                     const int* step, hipStream_t st);
 int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st, int* out2 = nullptr,
-                    int* pos_inc = nullptr);
+                    int* pos_inc = nullptr, void* part = nullptr);
 int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, int kpad, hipStream_t st);
 int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,
                  const void* R, int ldr, int M, int N, int K, int act, hipStream_t st);

@@ -193,18 +193,28 @@ def attn_decode_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: 
     return out
 
 
+ARGMAX_PART_PER_ROW = 64  # int2 partials per row of the row-split argmax workspace
+ARGMAX_SPLIT = True  # use the workspace when one is given (A/B switch, bench/decode_ab.py)
+
+
 def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None, also: Optional[torch.Tensor] = None,
-                advance: Optional[torch.Tensor] = None) -> torch.Tensor:
+                advance: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-row argmax (ties -> smallest index) into ``out`` (int32).  Decode
     step tail in the same launch: ``also`` receives a copy of the ids and
-    ``advance[row] += 1`` (int32 positions)."""
+    ``advance[row] += 1`` (int32 positions).  ``part`` (int32, >= 128 M
+    entries): workspace that lets small batches split each row over many
+    workgroups (a partial and a merge launch, sampler.hip)."""
     M = x.shape[0]
     N = n if n is not None else x.shape[1]
     for t, nm in ((out, "out"), (also, "also"), (advance, "advance")):
         if t is not None and (t.dtype != torch.int32 or t.numel() < M or not t.is_contiguous()):
             raise ValueError(f"argmax_rows: {nm} must be contiguous int32 with >= {M} entries")
+    if part is not None and (part.dtype != torch.int32 or part.numel() < 2 * ARGMAX_PART_PER_ROW * M
+                             or not part.is_contiguous()):
+        raise ValueError(f"argmax_rows: part must be contiguous int32 with >= {2 * ARGMAX_PART_PER_ROW * M} entries")
     check(lib().argmax_rows(ptr(x), x.stride(0), M, N, ptr(out), 1 if x.dtype == torch.float32 else 0,
-                            stream_ptr(), ptr(also), ptr(advance)), "argmax_rows")
+                            stream_ptr(), ptr(also), ptr(advance), ptr(part if ARGMAX_SPLIT else None)),
+          "argmax_rows")
     return out
 
 

@@ -194,6 +194,9 @@ class TransformerStage(StageCompute):
         G = H // Hkv
         self.ws_per_seq = Hkv * self.splits * G * (hd + 2)  # decode-attention partials of one sequence
         self.ws = torch.empty((self.max_batch * self.ws_per_seq,), dtype=torch.float32, device=dev)
+        # row-split argmax partials (last stage; rows offset by the microbatch like the logits)
+        self.amx_part = torch.empty((self.max_batch * 2 * T_.ARGMAX_PART_PER_ROW,),
+                                    dtype=torch.int32, device=dev)
         self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
@@ -325,7 +328,8 @@ class TransformerStage(StageCompute):
             return StageOutput(logits[:, :self.V], nxt)
         dst = out if (last_only and out is not None) else nxt
         also, adv = advance if advance is not None else (None, None)
-        T_.argmax_rows(logits, dst, n=self.V, also=also, advance=adv)
+        part = self.amx_part[r0 * 2 * T_.ARGMAX_PART_PER_ROW:] if last_only else None
+        T_.argmax_rows(logits, dst, n=self.V, also=also, advance=adv, part=part)
         return StageOutput(logits[:, :self.V], dst)
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None):

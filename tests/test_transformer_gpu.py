@@ -195,11 +195,13 @@ def test_argmax_rows():
 
 
 @pytest.mark.parametrize("M,N,ld", [(1, 128256, 128256), (3, 50257, 50304), (16, 1003, 1008), (64, 50257, 50304),
-                                    (100, 4096, 4096)])
-def test_argmax_rows_step_tail(M, N, ld):
-    """Wide-load argmax (1024-thread rows for M <= 16, 256 otherwise) with the
-    fused decode tail: ids to ``out`` and ``also``, ``advance`` += 1; ties go to
-    the smallest index (bf16 logits have many exact ties)."""
+                                    (100, 4096, 4096), (8, 50257, 50304), (2, 6000, 6000)])
+@pytest.mark.parametrize("split", [False, True])
+def test_argmax_rows_step_tail(M, N, ld, split):
+    """Wide-load argmax (1024-thread rows for M <= 16, 256 otherwise; ``split``:
+    rows over many workgroups + a merge launch) with the fused decode tail: ids
+    to ``out`` and ``also``, ``advance`` += 1; ties go to the smallest index
+    (bf16 logits have many exact ties, also across segment boundaries)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
     x = (torch.randn(M, ld, device=DEV, generator=g) * 4).round().bfloat16()  # coarse values: frequent ties
@@ -211,7 +213,8 @@ def test_argmax_rows_step_tail(M, N, ld):
     out = torch.full((M,), -1, dtype=torch.int32, device=DEV)
     cur = torch.full((M,), -1, dtype=torch.int32, device=DEV)
     pos = torch.arange(M, dtype=torch.int32, device=DEV)
-    T.argmax_rows(x, out, n=N, also=cur, advance=pos)
+    part = torch.full((2 * T.ARGMAX_PART_PER_ROW * M,), -7, dtype=torch.int32, device=DEV) if split else None
+    T.argmax_rows(x, out, n=N, also=cur, advance=pos, part=part)
     torch.cuda.synchronize()
     xs = x[:, :N].float().cpu()
     ref = torch.tensor([int((row == row.max()).nonzero()[0]) for row in xs])
