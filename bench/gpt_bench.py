@@ -42,12 +42,13 @@ def parse(argv=None):
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--prefill_iters", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--kv", default="bf16", choices=["bf16", "fp8"], help="KV cache dtype (fp8: OCP e4m3, GPT-2 family)")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     return ap.parse_args(argv)
 
 
-def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8):
+def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16"):
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import TorchStage
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
@@ -61,7 +62,7 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8):
             continue
         sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0, device=dev)
         out.append(TransformerStage(model, sd, a, b, s == 0, s == S - 1, dev, max_batch=max_batch,
-                                    max_seq=max_seq, fp8=fp8))
+                                    max_seq=max_seq, fp8=fp8, kv_dtype=kv))
         del sd
     return out
 
@@ -113,7 +114,8 @@ def run(args=None):
     total_steps = args.warmup + args.steps + 16 + 2  # + the 16 latency steps + graph-capture slack
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
-    stages = _build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8) if stage_ids else []
+    kv = getattr(args, "kv", "bf16")
+    stages = _build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv) if stage_ids else []
     base = rep * groups
     prev = P2PLink(base + grp - 1, dev) if grp > 0 else None
     nxt = P2PLink(base + grp + 1, dev) if 0 <= grp < groups - 1 else None
@@ -195,7 +197,7 @@ def run(args=None):
             "n_gpus": N, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(decode_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": ("fp8-e4m3 weights (decode: W8A16 on bf16 MFMA; prefill: W8A8 on fp8 MFMA), bf16 activations"
-                      if fp8 else "bf16"),
+                      if fp8 else "bf16") + ("; fp8-e4m3 KV cache" if kv == "fp8" else ""),
             "data": "synthetic prompts, random-init weights",
             "prefill_tokens_per_s": round(prefill_tok / prefill_s, 1),
             "prefill_ms_per_round": round(prefill_s * 1e3, 3),

@@ -105,22 +105,29 @@ PYBIND11_MODULE(_dnn_hip, m) {
                          ST(st));
   });
   m.def("flash_attn_qkv", [](u64 qkv, int ldqkv, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S,
-                             u64 pos, float scale, u64 st) {
-    return dnn_flash_attn_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));
-  });
+                             u64 pos, float scale, u64 st, int kv8) {
+    return dnn_flash_attn_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st), kv8);
+  }, py::arg("qkv"), py::arg("ldqkv"), py::arg("kc"), py::arg("vc"), py::arg("o"), py::arg("B"), py::arg("T"),
+     py::arg("H"), py::arg("Hkv"), py::arg("hd"), py::arg("S"), py::arg("pos"), py::arg("scale"), py::arg("st"),
+     py::arg("kv8") = 0);
   m.def("flash_attn", [](u64 q, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
                          float scale, u64 st) {
     return dnn_flash_attn(CP(q), CP(kc), CP(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));
   });
   m.def("attn_decode", [](u64 q, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S, u64 lens,
-                          float scale, int splits, u64 ws, u64 st) {
-    return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st));
-  });
+                          float scale, int splits, u64 ws, u64 st, int kv8) {
+    return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st),
+                           kv8);
+  }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("o"), py::arg("B"), py::arg("H"), py::arg("Hkv"),
+     py::arg("hd"), py::arg("S"), py::arg("lens"), py::arg("scale"), py::arg("splits"), py::arg("ws"), py::arg("st"),
+     py::arg("kv8") = 0);
   m.def("attn_decode_qkv", [](u64 qkv, int ldqkv, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S,
-                              u64 pos, u64 cos, u64 sin, float scale, int splits, u64 ws, u64 st) {
+                              u64 pos, u64 cos, u64 sin, float scale, int splits, u64 ws, u64 st, int kv8) {
     return dnn_attn_decode_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, H, Hkv, hd, S, CIP(pos), CFP(cos), CFP(sin),
-                               scale, splits, FP(ws), ST(st));
-  });
+                               scale, splits, FP(ws), ST(st), kv8);
+  }, py::arg("qkv"), py::arg("ldqkv"), py::arg("kc"), py::arg("vc"), py::arg("o"), py::arg("B"), py::arg("H"),
+     py::arg("Hkv"), py::arg("hd"), py::arg("S"), py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("scale"),
+     py::arg("splits"), py::arg("ws"), py::arg("st"), py::arg("kv8") = 0);
   m.def("sample_topk", [](u64 x, int ld, int M, int N, u64 out, float temperature, int topk, unsigned seed, u64 step,
                           u64 st) {
     return dnn_sample_topk(CP(x), ld, M, N, reinterpret_cast<int*>(out), temperature, topk, seed,

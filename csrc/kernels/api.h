@@ -51,14 +51,14 @@ int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, 
 int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
                   const int* pos, const float* cos, const float* sin, int rope, hipStream_t st);
 int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H, int Hkv,
-                       int hd, int S, const int* pos, float scale, hipStream_t st);
+                       int hd, int S, const int* pos, float scale, hipStream_t st, int kv8 = 0);
 int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv, int hd, int S,
                    const int* pos, float scale, hipStream_t st);
 int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd, int S,
                         const int* pos, const float* cosT, const float* sinT, float scale, int splits, float* ws,
-                        hipStream_t st);
+                        hipStream_t st, int kv8 = 0);
 int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd, int S,
-                    const int* lens, float scale, int splits, float* ws, hipStream_t st);
+                    const int* lens, float scale, int splits, float* ws, hipStream_t st, int kv8 = 0);
 int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float temperature, int topk, unsigned seed,
                     const int* step, hipStream_t st);
 int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st, int* out2 = nullptr,

@@ -115,7 +115,33 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
-template <int HD, bool QKV = false>
+// KV8 (QKV mode): the cache is e4m3 (decode attention's KV8 layout): new rows
+// are rounded once when copied in, cached rows are widened to bf16 as they are
+// fetched; this chunk's own keys/values come from the bf16 c_attn output.
+__device__ __forceinline__ uint2 kv8_pack8(const i32x4& x) {  // 8 bf16 -> 8 e4m3
+  int lo = 0, hi = 0;
+  float f[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] << 16), -448.f), 448.f);
+    f[2 * i + 1] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] & 0xffff0000u), -448.f), 448.f);
+  }
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return make_uint2((uint32_t)lo, (uint32_t)hi);
+}
+__device__ __forceinline__ i32x4 kv8_unpack8(const uint2 w) {  // 8 e4m3 -> 8 bf16
+  i32x4 r;
+  r[0] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false));
+  r[1] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true));
+  r[2] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false));
+  r[3] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true));
+  return r;
+}
+
+template <int HD, bool QKV = false, bool KV8 = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
@@ -143,6 +169,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
   const int kv_end = min(min(kv_len, blk_qmax + 1), S);  // never read past the cache
 
+  static_assert(!KV8 || QKV, "fp8 KV cache: QKV-mode prefill only");
   const bf16_t* krow_new = nullptr;  // QKV: this sequence's new-key rows (position p0 + t = row b*T + t)
   const bf16_t* vrow_new = nullptr;
   if constexpr (QKV) {
@@ -154,10 +181,19 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       for (int e = tid; e < FA_QB * CH; e += 256) {
         const int t = qb * FA_QB + e / CH, c = e % CH;
         if (t < T && p0 + t < S) {
-          *reinterpret_cast<uint4*>(kd + (size_t)(p0 + t) * HD + c * 8) =
-              *reinterpret_cast<const uint4*>(krow_new + (size_t)t * ldq + c * 8);
-          *reinterpret_cast<uint4*>(vd + (size_t)(p0 + t) * HD + c * 8) =
-              *reinterpret_cast<const uint4*>(vrow_new + (size_t)t * ldq + c * 8);
+          if constexpr (KV8) {
+            uint8_t* kd8 = reinterpret_cast<uint8_t*>(kc_out) + ((size_t)b * Hkv + kvh) * S * HD;
+            uint8_t* vd8 = reinterpret_cast<uint8_t*>(vc_out) + ((size_t)b * Hkv + kvh) * S * HD;
+            *reinterpret_cast<uint2*>(kd8 + (size_t)(p0 + t) * HD + c * 8) =
+                kv8_pack8(*reinterpret_cast<const i32x4*>(krow_new + (size_t)t * ldq + c * 8));
+            *reinterpret_cast<uint2*>(vd8 + (size_t)(p0 + t) * HD + c * 8) =
+                kv8_pack8(*reinterpret_cast<const i32x4*>(vrow_new + (size_t)t * ldq + c * 8));
+          } else {
+            *reinterpret_cast<uint4*>(kd + (size_t)(p0 + t) * HD + c * 8) =
+                *reinterpret_cast<const uint4*>(krow_new + (size_t)t * ldq + c * 8);
+            *reinterpret_cast<uint4*>(vd + (size_t)(p0 + t) * HD + c * 8) =
+                *reinterpret_cast<const uint4*>(vrow_new + (size_t)t * ldq + c * 8);
+          }
         }
       }
     }
@@ -193,6 +229,11 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       if (QKV && kk >= p0) {
         pk[it] = *reinterpret_cast<const i32x4*>(krow_new + (size_t)(kk - p0) * ldq + c * 8);
         pv[it] = *reinterpret_cast<const i32x4*>(vrow_new + (size_t)(kk - p0) * ldq + c * 8);
+      } else if constexpr (KV8) {
+        const uint8_t* kb8 = reinterpret_cast<const uint8_t*>(kc) + ((size_t)b * Hkv + kvh) * S * HD;
+        const uint8_t* vb8 = reinterpret_cast<const uint8_t*>(vc) + ((size_t)b * Hkv + kvh) * S * HD;
+        pk[it] = kv8_unpack8(*reinterpret_cast<const uint2*>(kb8 + (size_t)kk * HD + c * 8));
+        pv[it] = kv8_unpack8(*reinterpret_cast<const uint2*>(vb8 + (size_t)kk * HD + c * 8));
       } else {
         pk[it] = *reinterpret_cast<const i32x4*>(kbase + (size_t)kk * HD + c * 8);
         pv[it] = *reinterpret_cast<const i32x4*>(vbase + (size_t)kk * HD + c * 8);
@@ -367,6 +408,29 @@ __device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int s
   }
 }
 
+// e4m3 KV cache helpers: 16 floats -> 16 OCP e4m3 bytes (round to nearest,
+// saturated to +-448 first: the hardware convert does not clamp), and 16 e4m3
+// bytes -> 8 packed bf16 pairs (exact; v_cvt_scalef32_pk_bf16_fp8 at scale 1).
+__device__ __forceinline__ void kv8_pack(const float (&x)[16], i32x4& out) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = fminf(fmaxf(x[4 * w + j], -448.f), 448.f);
+    int v = 0;
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], v, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], v, true);
+    out[w] = v;
+  }
+}
+__device__ __forceinline__ void kv8_unpack(const i32x4& w, uint32_t (&p)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[2 * i] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)w[i], 1.0f, false));
+    p[2 * i + 1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)w[i], 1.0f, true));
+  }
+}
+
 // FUSED (decode steps): q, the new key (RoPE'd) and value are read straight
 // from the QKV projection row of each sequence, the key count is pos[b] + 1,
 // and the workgroup whose split holds the new position writes it into the
@@ -382,7 +446,13 @@ __device__ __forceinline__ void load_head8(const bf16_t* __restrict__ row, int s
 // HD/32 v_mfma_f32_16x16x32_bf16: lane l feeds key row l&15 (A, straight from
 // the cache) and head l&15 (B = q^T, RoPE'd once); C lands as 4 keys x 1 head
 // per lane.  Softmax, P.V and the reduction are unchanged.
-template <int HD, int G, int FM, bool NT, bool MF = false>
+// KV8: the cache holds OCP e4m3 (unit scale, range +-448; kc/vc are byte
+// arrays of the same [B][Hkv][S][HD] shape): a lane's 16-B load is 16 key
+// dims instead of 8, so a key row is HD/16 lanes and the K/V bytes per step
+// halve; entries are converted to bf16 in registers (exact) before the same
+// v_dot2 math, and the new key/value row is rounded to e4m3 once — its score
+// uses the rounded copy, so the current step sees what later steps will read.
+template <int HD, int G, int FM, bool NT, bool MF = false, bool KV8 = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
                                                           bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                           float* __restrict__ ws, int H, int Hkv, int S,
@@ -391,7 +461,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           int chunk_cap, bf16_t* __restrict__ o_direct) {
   constexpr bool FUSED = FM != 0;  // FM: 0 = q head-major + cached keys, 1 = fused QKV rows, 2 = fused + RoPE
   constexpr bool ROPE = FM == 2;
-  constexpr int LPK = HD / 8;           // lanes per key row (16 B each)
+  static_assert(!(KV8 && MF), "fp8 KV cache: VALU score path only");
+  constexpr int ELT = KV8 ? 16 : 8;     // head dims per 16-B lane load
+  constexpr int LPK = HD / ELT;         // lanes per key row (16 B each)
   constexpr int GPB = 256 / LPK;        // key groups per block
   extern __shared__ __attribute__((aligned(16))) float dsm[];   // [G][chunk_cap] scores, then reduction scratch
   const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
@@ -414,8 +486,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD;
   bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD;
-  float qv[G][8];
-  float nk[8] = {}, nv[8] = {};
+  constexpr int EB = KV8 ? 1 : 2;  // cache bytes per element
+  uint8_t* kb8 = reinterpret_cast<uint8_t*>(kc) + ((size_t)b * Hkv + kvh) * S * HD * EB;
+  uint8_t* vb8 = reinterpret_cast<uint8_t*>(vc) + ((size_t)b * Hkv + kvh) * S * HD * EB;
+  float qv[G][ELT];
+  float nk[ELT] = {}, nv[ELT] = {};
   // FUSED: is the new key inside this split (and inside the cache)?
   const bool own_new = FUSED && p_new < S && p_new >= k0 && p_new < k1;
   if constexpr (FUSED) {
@@ -423,34 +498,50 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     const int pr = min(p_new, S - 1);  // RoPE table row (overflow is dropped, never read out of bounds)
     if constexpr (!MF) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) load_head8<HD, ROPE>(row + (kvh * G + g) * HD, sub, cosT, sinT, pr, qv[g]);
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int h8 = 0; h8 < ELT / 8; ++h8)
+          load_head8<HD, ROPE>(row + (kvh * G + g) * HD, sub * (ELT / 8) + h8, cosT, sinT, pr, qv[g] + 8 * h8);
     }
     // new key / value: loaded unconditionally (used only when own_new), no branch
-    load_head8<HD, ROPE>(row + (H + kvh) * HD, sub, cosT, sinT, pr, nk);
-    load_head8<HD, false>(row + (H + Hkv + kvh) * HD, sub, nullptr, nullptr, 0, nv);
+#pragma unroll
+    for (int h8 = 0; h8 < ELT / 8; ++h8) {
+      load_head8<HD, ROPE>(row + (H + kvh) * HD, sub * (ELT / 8) + h8, cosT, sinT, pr, nk + 8 * h8);
+      load_head8<HD, false>(row + (H + Hkv + kvh) * HD, sub * (ELT / 8) + h8, nullptr, nullptr, 0, nv + 8 * h8);
+    }
   } else if constexpr (!MF) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qv[g][j] = bf2f_s(pq[j]);
-    }
+      for (int h8 = 0; h8 < ELT / 8; ++h8) {
+        const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * ELT + 8 * h8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qv[g][8 * h8 + j] = bf2f_s(pq[j]);
+      }
   }
   const int knew = own_new ? p_new - k0 : -1;  // split-relative index of the register-held key
   // q and the new key are bf16-exact (rounded after RoPE): pack them into bf16
   // pairs so a score is 4 v_dot2_f32_bf16 per lane instead of 8 converts + 8 FMAs.
-  uint32_t qp[G][4], nkp[4];  // bf16 pairs, reinterpreted only at the dot2 call
+  uint32_t qp[G][ELT / 2], nkp[ELT / 2];  // bf16 pairs, reinterpreted only at the dot2 call
   if constexpr (!MF) {
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
+      for (int j = 0; j < ELT / 2; ++j) qp[g][j] = pack2bf(qv[g][2 * j], qv[g][2 * j + 1]);
   }
+  uint32_t nvp[ELT / 2];
+  i32x4 nk8 = {0, 0, 0, 0}, nv8 = {0, 0, 0, 0};  // KV8: the new row as stored (e4m3)
+  if constexpr (KV8) {
+    kv8_pack(nk, nk8);
+    kv8_pack(nv, nv8);
+    kv8_unpack(nk8, nkp);  // the register copy = what the cache will hold
+    kv8_unpack(nv8, nvp);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) nkp[j] = pack2bf(nk[j * 2], nk[j * 2 + 1]);
-  uint32_t nvp[4];
+    for (int j = 0; j < ELT / 2; ++j) nkp[j] = pack2bf(nk[j * 2], nk[j * 2 + 1]);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) nvp[j] = pack2bf(nv[j * 2], nv[j * 2 + 1]);
+    for (int j = 0; j < ELT / 2; ++j) nvp[j] = pack2bf(nv[j * 2], nv[j * 2 + 1]);
+  }
   float* sc = dsm;  // [G][chunk]
   const int n = k1 - k0;
   DEC_PROBE(2, nvp[0]);
@@ -526,7 +617,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       // per step, so stream them non-temporally (GPT-2 B=64: 0.658 -> 0.590 ms
       // per decode step); small caches (batch 1) stay cacheable: they live in
       // the MALL from one step to the next
-      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + sub * 8);
+      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb8 + ((size_t)(k0 + kk) * HD + sub * ELT) * EB);
       kr[u] = NT ? __builtin_nontemporal_load(kp) : *kp;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -534,18 +625,22 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int u = 0; u < DEC_U; ++u) {
       if (kb0 + u * GPB >= n) break;  // workgroup-uniform: the rest of the batch is past the context
       const int kk = kb0 + u * GPB + grp;
-      uint32_t kp[4];
+      uint32_t kp[ELT / 2];
+      if constexpr (KV8) {
+        kv8_unpack(__builtin_bit_cast(i32x4, kr[u]), kp);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) kp[j] = (uint32_t)(uint16_t)kr[u][2 * j] | ((uint32_t)(uint16_t)kr[u][2 * j + 1] << 16);
+        for (int j = 0; j < 4; ++j) kp[j] = (uint32_t)(uint16_t)kr[u][2 * j] | ((uint32_t)(uint16_t)kr[u][2 * j + 1] << 16);
+      }
       if (FUSED && kk == knew) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) kp[j] = nkp[j];
+        for (int j = 0; j < ELT / 2; ++j) kp[j] = nkp[j];
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qp[g][j]), __builtin_bit_cast(bf16x2v, kp[j]), d, false);
+        for (int j = 0; j < ELT / 2; ++j) d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qp[g][j]), __builtin_bit_cast(bf16x2v, kp[j]), d, false);
         d = group_sum<LPK>(d);  // DPP row reduction over the LPK lanes of this key
         if (sub == 0 && kk < n) sc[g * chunk_cap + kk] = d * scale_log2;
       }
@@ -559,7 +654,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
   for (int u = 0; u < DEC_U; ++u) {
     const int kk = min(u * GPB + grp, n - 1);
-    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb8 + ((size_t)(k0 + kk) * HD + sub * ELT) * EB);
     vr0[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
   }
   __syncthreads();
@@ -583,11 +678,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   __syncthreads();
   DEC_PROBE(4, 0);
   // P.V: thread owns d chunk `sub` for key group `grp`
-  float acc[G][8];
+  float acc[G][ELT];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+    for (int j = 0; j < ELT; ++j) acc[g][j] = 0.f;
   for (int kb0 = 0; kb0 < n; kb0 += GPB * DEC_U) {
     bf16x8 vr[DEC_U];
     if (kb0 == 0) {
@@ -597,7 +692,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
       for (int u = 0; u < DEC_U; ++u) {
         const int kk = min(kb0 + u * GPB + grp, n - 1);
-        const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)(k0 + kk) * HD + sub * 8);
+        const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb8 + ((size_t)(k0 + kk) * HD + sub * ELT) * EB);
         vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
       }
     }
@@ -609,23 +704,28 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int u = 0; u < DEC_U; u += 2) {
       if (kb0 + u * GPB >= n) break;  // workgroup-uniform, as in the score loop
       const int ka = kb0 + u * GPB + grp, kz = ka + GPB;
-      uint32_t wa[4], wz[4];
+      uint32_t wa[ELT / 2], wz[ELT / 2];
+      if constexpr (KV8) {
+        kv8_unpack(__builtin_bit_cast(i32x4, vr[u]), wa);
+        kv8_unpack(__builtin_bit_cast(i32x4, vr[u + 1]), wz);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
-        wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
+        for (int j = 0; j < 4; ++j) {
+          wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
+          wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
+        }
       }
       if (FUSED && ka == knew) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wa[j] = nvp[j];
+        for (int j = 0; j < ELT / 2; ++j) wa[j] = nvp[j];
       }
       if (FUSED && kz == knew) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wz[j] = nvp[j];
+        for (int j = 0; j < ELT / 2; ++j) wz[j] = nvp[j];
       }
-      uint32_t pr[8];  // element e of both rows: (row u, row u+1)
+      uint32_t pr[ELT];  // element e of both rows: (row u, row u+1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < ELT / 2; ++j) {
         pr[2 * j] = __builtin_amdgcn_perm(wz[j], wa[j], 0x05040100u);
         pr[2 * j + 1] = __builtin_amdgcn_perm(wz[j], wa[j], 0x07060302u);
       }
@@ -635,7 +735,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         const float pz = kz < n ? sc[g * chunk_cap + kz] : 0.f;
         const bf16x2v pp = __builtin_bit_cast(bf16x2v, pack2bf(pa, pz));
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < ELT; ++j)
           acc[g][j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2v, pr[j]), acc[g][j], false);
       }
     }
@@ -646,7 +746,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[((size_t)grp * G + g) * HD + sub * 8 + j] = acc[g][j];
+    for (int j = 0; j < ELT; ++j) red[((size_t)grp * G + g) * HD + sub * ELT + j] = acc[g][j];
   __syncthreads();
   for (int i = tid; i < G * HD; i += 256) {
     const int g = i / HD, d = i % HD;
@@ -664,7 +764,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   // the new key / value row into the cache, last: a store issued before the
   // K/V loads would sit in front of them in this wave's vmcnt queue
-  if (FUSED && own_new && grp == 0) {
+  if (KV8 && FUSED && own_new && grp == 0) {
+    *reinterpret_cast<i32x4*>(kb8 + (size_t)p_new * HD + sub * 16) = nk8;
+    *reinterpret_cast<i32x4*>(vb8 + (size_t)p_new * HD + sub * 16) = nv8;
+  } else if (FUSED && own_new && grp == 0) {
     uint4 wk, wv;
     uint32_t* pk = reinterpret_cast<uint32_t*>(&wk);
     uint32_t* pv = reinterpret_cast<uint32_t*>(&wv);
@@ -737,10 +840,23 @@ extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, voi
 
 // Prefill straight from the c_attn output (no RoPE): see flash_attn_kernel<HD, true>.
 extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H,
-                                  int Hkv, int hd, int S, const int* pos, float scale, hipStream_t st) {
+                                  int Hkv, int hd, int S, const int* pos, float scale, hipStream_t st, int kv8) {
   if (H % Hkv != 0 || ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
+  if (kv8) {  // e4m3 cache (unit scale)
+    if (hd == 64)
+      hipLaunchKernelGGL((flash_attn_kernel<64, true, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
+                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc,
+                         (bf16_t*)vc);
+    else if (hd == 128)
+      hipLaunchKernelGGL((flash_attn_kernel<128, true, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
+                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc,
+                         (bf16_t*)vc);
+    else
+      return -2;
+    return (int)hipGetLastError();
+  }
   if (hd == 64) {
     hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)kc,
                        (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc, (bf16_t*)vc);
@@ -755,21 +871,36 @@ extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc
 
 static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd,
                               int S, const int* lens, const float* cosT, const float* sinT, float scale, int splits,
-                              float* ws, bool fused, hipStream_t st) {
+                              float* ws, bool fused, hipStream_t st, bool kv8 = false) {
   const int G = H / Hkv;
   if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
+  if (kv8 && G != 1) return -4;  // e4m3 cache: MHA (the VALU score path) only
   const int chunk_cap = (S + splits - 1) / splits;
-  const int gpb = 256 / (hd / 8);
+  const int gpb = 256 / (hd / (kv8 ? 16 : 8));
   size_t smem = sizeof(float) * (size_t)G * (size_t)(chunk_cap > gpb * hd ? chunk_cap : gpb * hd);
   if (smem > 160 * 1024) return -3;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(B * Hkv, splits);
   // cache bytes this launch may stream (capacity bound): > 32 MB -> non-temporal
-  const bool nt = (double)B * Hkv * S * hd * 4.0 > 32.0 * 1024 * 1024;
+  const bool nt = (double)B * Hkv * S * hd * (kv8 ? 2.0 : 4.0) > 32.0 * 1024 * 1024;
   // MFMA scores: GQA (G >= 2) by default; DNN_DECODE_MFMA=0/1 forces it off/on (A/B)
   const char* mf_e = getenv("DNN_DECODE_MFMA");
   const bool mf = mf_e ? atoi(mf_e) == 1 : G >= 2;
   const int fm = fused ? (cosT != nullptr ? 2 : 1) : 0;
+  if (kv8) {
+#define DEC8(HDV, NTV, FMV)                                                                                          \
+  if (hd == HDV && nt == NTV && fm == FMV)                                                                            \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, 1, FMV, NTV, false, true>), grid, dim3(256), smem, st,                \
+                       (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens,                          \
+                       FMV == 2 ? cosT : nullptr, FMV == 2 ? sinT : nullptr, sl2, chunk_cap, (bf16_t*)o);            \
+  else
+    DEC8(64, true, 1) DEC8(64, false, 1) DEC8(128, true, 1) DEC8(128, false, 1) DEC8(64, true, 0) DEC8(64, false, 0)
+    DEC8(128, true, 0) DEC8(128, false, 0) { return -2; }
+#undef DEC8
+    if (splits > 1)
+      hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
+    return (int)hipGetLastError();
+  }
 #define DEC_FM(HDV, GV, NTV, MFV)                                                                                     \
   if (fm == 2)                                                                                                        \
     hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 2, NTV, MFV>), grid, dim3(256), smem, st, (const bf16_t*)q, ldq,  \
@@ -810,9 +941,9 @@ extern "C" int dnn_dec_probe_read(unsigned long long* out) {
 #endif
 
 extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int B, int H, int Hkv, int hd,
-                               int S, const int* lens, float scale, int splits, float* ws, hipStream_t st) {
+                               int S, const int* lens, float scale, int splits, float* ws, hipStream_t st, int kv8) {
   return attn_decode_launch(q, H * hd, const_cast<void*>(kc), const_cast<void*>(vc), o, B, H, Hkv, hd, S, lens,
-                            nullptr, nullptr, scale, splits, ws, false, st);
+                            nullptr, nullptr, scale, splits, ws, false, st, kv8 != 0);
 }
 
 // Decode step straight from the QKV projection: qkv rows (B, ldqkv) laid out
@@ -821,7 +952,9 @@ extern "C" int dnn_attn_decode(const void* q, const void* kc, const void* vc, vo
 // output (B, H*hd).
 extern "C" int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int H, int Hkv,
                                    int hd, int S, const int* pos, const float* cosT, const float* sinT, float scale,
-                                   int splits, float* ws, hipStream_t st) {
+                                   int splits, float* ws, hipStream_t st, int kv8) {
   if (ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
-  return attn_decode_launch(qkv, ldqkv, kc, vc, o, B, H, Hkv, hd, S, pos, cosT, sinT, scale, splits, ws, true, st);
+  if (kv8 && cosT != nullptr) return -4;  // e4m3 cache: no-RoPE (GPT-2 family) fused path
+  return attn_decode_launch(qkv, ldqkv, kc, vc, o, B, H, Hkv, hd, S, pos, cosT, sinT, scale, splits, ws, true, st,
+                            kv8 != 0);
 }

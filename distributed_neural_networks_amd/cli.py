@@ -176,7 +176,8 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
                 ntok = pipe.micro_batch_size * (min(pipe.prefill_chunk, n_pos) if pipe.prefill_chunk > 0 else n_pos)
             st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
                                     max_batch=n_seq, max_seq=n_pos, max_tokens=ntok,
-                                    temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed)
+                                    temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed,
+                                    kv_dtype=pipe.kv_cache_dtype)
     else:
         st = TorchStage(pipe.model, sd, a, b, first, last, device,
                         sampling=(pipe.temperature, pipe.top_k, pipe.seed))

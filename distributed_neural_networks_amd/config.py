@@ -60,6 +60,7 @@ class PipelineConfig:
     return_to_node_id: Optional[str] = None
     model: str = "cifar10"
     dtype: Optional[str] = None
+    kv_cache_dtype: str = "bf16"              # "fp8": OCP e4m3 KV cache (GPT-2 family)
     transport: str = "grpc"
     micro_batch_size: int = 1
     num_microbatches: int = 1
@@ -195,6 +196,11 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     if reps > 1 and transport not in ("rccl", "gloo"):
         raise ConfigError(f"ERROR: 'replicas' > 1 needs transport 'rccl' or 'gloo' (one rank per stage and replica), "
                           f"got '{transport}'")
+    kvd = cfg.get("kv_cache_dtype", "bf16")
+    if kvd not in ("bf16", "fp8"):
+        raise ConfigError(f"ERROR: 'kv_cache_dtype' must be 'bf16' or 'fp8', got {kvd!r}")
+    if kvd == "fp8" and not model.startswith("gpt2"):
+        raise ConfigError(f"ERROR: 'kv_cache_dtype' fp8 supports the GPT-2 family (MHA, no RoPE), not '{model}'")
     t = cfg.get("temperature", 0.0)
     if not isinstance(t, (int, float)) or t < 0:
         raise ConfigError(f"ERROR: 'temperature' must be >= 0, got {t!r}")
@@ -205,7 +211,7 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
             raise ConfigError(f"ERROR: return_to_node_id '{ret}' is not a node of this config")
     return PipelineConfig(
         nodes=nodes, model_weights=str(weights), num_parts=num_parts,
-        return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"),
+        return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"), kv_cache_dtype=kvd,
         transport=transport, micro_batch_size=int(cfg.get("micro_batch_size", 1)),
         num_microbatches=int(cfg.get("num_microbatches", 1)), seq_len=int(cfg.get("seq_len", 64)),
         prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),

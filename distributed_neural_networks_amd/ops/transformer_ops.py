@@ -113,6 +113,20 @@ def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.T
     return out
 
 
+KV8_DTYPES = (torch.float8_e4m3fn, torch.uint8)  # e4m3 KV cache storage (unit scale)
+
+
+def _kv8(kc: torch.Tensor, vc: torch.Tensor) -> int:
+    """1 for an OCP e4m3 KV cache (decode attention / QKV-mode prefill read and
+    write it as bytes, attention.hip KV8), 0 for bf16."""
+    k8, v8 = kc.dtype in KV8_DTYPES, vc.dtype in KV8_DTYPES
+    if k8 != v8:
+        raise TypeError("K and V caches must share a dtype")
+    if not k8 and kc.dtype != torch.bfloat16:
+        raise TypeError(f"KV cache dtype {kc.dtype}: bf16 or float8_e4m3fn")
+    return 1 if k8 else 0
+
+
 def flash_attn_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,
                    Hkv: int, hd: int, pos: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
     """Causal prefill straight from the c_attn output (no RoPE): qkv (B*T, ld)
@@ -129,7 +143,7 @@ def flash_attn_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: t
         raise ValueError("flash_attn_qkv: cache slices must be contiguous")
     scale = scale if scale is not None else 1.0 / math.sqrt(hd)
     check(lib().flash_attn_qkv(ptr(qkv), qkv.stride(0), ptr(kc), ptr(vc), ptr(out), B, T, H, Hkv, hd, S, ptr(pos),
-                               scale, stream_ptr()), "flash_attn_qkv")
+                               scale, stream_ptr(), kv8=_kv8(kc, vc)), "flash_attn_qkv")
     return out
 
 
@@ -163,7 +177,7 @@ def attn_decode(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.
         raise ValueError(f"attn_decode: workspace needs {need} fp32")
     scale = scale if scale is not None else 1.0 / math.sqrt(hd)
     check(lib().attn_decode(ptr(q), ptr(kc), ptr(vc), ptr(out), B, H, Hkv, hd, S, ptr(lens), scale, splits, ptr(ws),
-                            stream_ptr()), "attn_decode")
+                            stream_ptr(), kv8=_kv8(kc, vc)), "attn_decode")
     return out
 
 
@@ -189,7 +203,8 @@ def attn_decode_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: 
         raise ValueError(f"attn_decode_qkv: workspace needs {need} fp32")
     scale = scale if scale is not None else 1.0 / math.sqrt(hd)
     check(lib().attn_decode_qkv(ptr(qkv), qkv.stride(0), ptr(kc), ptr(vc), ptr(out), B, H, Hkv, hd, S, ptr(pos),
-                                ptr(cos), ptr(sin), scale, splits, ptr(ws), stream_ptr()), "attn_decode_qkv")
+                                ptr(cos), ptr(sin), scale, splits, ptr(ws), stream_ptr(), kv8=_kv8(kc, vc)),
+          "attn_decode_qkv")
     return out
 
 

@@ -68,7 +68,8 @@ class LayerW:
 class TransformerStage(StageCompute):
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
                  device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
-                 fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0):
+                 fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0,
+                 kv_dtype: str = "bf16"):
         info = model_info(model)
         # sampling (last stage): temperature 0 = greedy argmax; otherwise
         # Gumbel-max over the top_k logits (0 = all), seeded per (row, position)
@@ -118,7 +119,15 @@ class TransformerStage(StageCompute):
             self.cos, self.sin = _f32(cos, dev), _f32(sin, dev)
         # KV cache: [layer] -> (B, Hkv, S, hd)
         L = len(self.layers)
-        self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=torch.bfloat16, device=dev)
+        # KV cache: bf16, or OCP e4m3 ("fp8": half the bytes every decode step
+        # streams; MHA without RoPE, i.e. the GPT-2 family, attention.hip KV8)
+        if kv_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"kv_dtype {kv_dtype!r}: bf16 or fp8")
+        if kv_dtype == "fp8" and (self.Hkv != self.H or self.family != "gpt2"):
+            raise ValueError("fp8 KV cache: multi-head attention without RoPE (GPT-2 family) only")
+        self.kv_dtype = kv_dtype
+        kvt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
+        self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=kvt, device=dev)
         self.vc = torch.zeros_like(self.kc)
         self._alloc(self.max_tokens)
 
@@ -369,12 +378,12 @@ class TransformerStage(StageCompute):
 
 def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
                        max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
-                       temperature: float = 0.0, top_k: int = 0, seed: int = 0):
+                       temperature: float = 0.0, top_k: int = 0, seed: int = 0, kv_dtype: str = "bf16"):
     fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
     info = model_info(model)
     max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))
     return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8,
-                            temperature, top_k, seed)
+                            temperature, top_k, seed, kv_dtype=kv_dtype)
 
 
 # ---------------------------------------------------------------------- smoke / golden check
