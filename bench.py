@@ -352,6 +352,15 @@ def extra_keys(args, info):
         g = gpt_bench.run(ga)
         out["gpt2_4stage_b256_decode_tok_s"] = g["value"]
         out["gpt2_4stage_b256_decode_ms_per_step"] = g["ms_per_step"]
+        # fp8 (OCP e4m3) KV cache, reduced KV precision (weights/activations bf16):
+        # the decode K/V bytes halve (kv_cache_dtype "fp8")
+        for key, b in (("gpt2_4stage_kv8", "64"), ("gpt2_4stage_b256_kv8", "256")):
+            ga = gpt_bench.parse(["--gpus", "1", "--steps", "32", "--warmup", "4", "--batch", b, "--prompt", "512",
+                                  "--stages", "4", "--dtype", "bf16", "--kv", "fp8", "--prefill_iters", "1"])
+            g = gpt_bench.run(ga)
+            out[key + "_decode_tok_s"] = g["value"]
+            out[key + "_decode_ms_per_step"] = g["ms_per_step"]
+        out["gpt2_4stage_kv8_dtype"] = "bf16 weights/activations, fp8-e4m3 KV cache"
     if getattr(args, "gpt", True) and not args.no_big:
         # BASELINE.json configs 4 and 5 on this GPU (all stages colocated): Llama-3
         # 8B bf16 8-stage microbatched decode and GPT-2 XL 8-stage with fp8
@@ -365,7 +374,12 @@ def extra_keys(args, info):
                                            "--dtype", "fp8"],
                  {"model": "gpt2-xl (random init)", "stages": 8,
                   "dtype": "fp8-e4m3 weights (W8A16 decode, W8A8 prefill), bf16 activations", "micro_batch": 64,
-                  "prompt_len": 512})):
+                  "prompt_len": 512}),
+                ("gpt2xl_fp8_8stage_b64_kv8", ["--model", "gpt2-xl", "--stages", "8", "--batch", "64", "--prompt",
+                                               "512", "--dtype", "fp8", "--kv", "fp8"],
+                 {"model": "gpt2-xl (random init)", "stages": 8,
+                  "dtype": "fp8-e4m3 weights (W8A16 decode, W8A8 prefill), bf16 activations, fp8-e4m3 KV cache",
+                  "micro_batch": 64, "prompt_len": 512})):
             try:
                 g = gpt_bench.run(gpt_bench.parse(["--gpus", "1", "--steps", "16", "--warmup", "2",
                                                    "--prefill_iters", "1"] + argv))

@@ -25,6 +25,8 @@ def apply(switch: str, v: int) -> None:
         lib().gemm_set_res_prefetch(v)
     elif switch == "fold_norm":
         gemm.FOLD_NORM_PREFILL = bool(v)
+    elif switch == "kv8_u":  # fp8-KV decode attention rows in flight per thread (attention.hip KV8U)
+        os.environ["DNN_KV8_U"] = str(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

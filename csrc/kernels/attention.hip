@@ -452,7 +452,7 @@ __device__ __forceinline__ void kv8_unpack(const i32x4& w, uint32_t (&p)[8]) {
 // halve; entries are converted to bf16 in registers (exact) before the same
 // v_dot2 math, and the new key/value row is rounded to e4m3 once — its score
 // uses the rounded copy, so the current step sees what later steps will read.
-template <int HD, int G, int FM, bool NT, bool MF = false, bool KV8 = false>
+template <int HD, int G, int FM, bool NT, bool MF = false, bool KV8 = false, int KV8U = 10>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
                                                           bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                           float* __restrict__ ws, int H, int Hkv, int S,
@@ -462,6 +462,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   constexpr bool FUSED = FM != 0;  // FM: 0 = q head-major + cached keys, 1 = fused QKV rows, 2 = fused + RoPE
   constexpr bool ROPE = FM == 2;
   static_assert(!(KV8 && MF), "fp8 KV cache: VALU score path only");
+  // rows in flight per thread: KV8 rows are half the bytes, so KV8U (10) rows
+  // keep the same bytes in flight and one batch covers 640 keys at hd 64 (the
+  // 512-567-token benchmark contexts take one K and one V round trip, not two)
+  constexpr int DEC_U = KV8 ? KV8U : dnn::DEC_U;
+  static_assert(DEC_U % 2 == 0, "P.V folds key pairs");
   constexpr int ELT = KV8 ? 16 : 8;     // head dims per 16-B lane load
   constexpr int LPK = HD / ELT;         // lanes per key row (16 B each)
   constexpr int GPB = 256 / LPK;        // key groups per block
@@ -888,12 +893,20 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
   const bool mf = mf_e ? atoi(mf_e) == 1 : G >= 2;
   const int fm = fused ? (cosT != nullptr ? 2 : 1) : 0;
   if (kv8) {
+    // DNN_KV8_U=8: 8 rows in flight per thread instead of 10 (A/B)
+    const char* u_e = getenv("DNN_KV8_U");
+    const bool u8 = u_e != nullptr && atoi(u_e) == 8;
 #define DEC8(HDV, NTV, FMV)                                                                                          \
-  if (hd == HDV && nt == NTV && fm == FMV)                                                                            \
-    hipLaunchKernelGGL((attn_decode_kernel<HDV, 1, FMV, NTV, false, true>), grid, dim3(256), smem, st,                \
-                       (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens,                          \
-                       FMV == 2 ? cosT : nullptr, FMV == 2 ? sinT : nullptr, sl2, chunk_cap, (bf16_t*)o);            \
-  else
+  if (hd == HDV && nt == NTV && fm == FMV) {                                                                          \
+    if (u8)                                                                                                           \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, 1, FMV, NTV, false, true, 8>), grid, dim3(256), smem, st,           \
+                         (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2,  \
+                         chunk_cap, (bf16_t*)o);                                                                      \
+    else                                                                                                              \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, 1, FMV, NTV, false, true, 10>), grid, dim3(256), smem, st,          \
+                         (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2,  \
+                         chunk_cap, (bf16_t*)o);                                                                      \
+  } else
     DEC8(64, true, 1) DEC8(64, false, 1) DEC8(128, true, 1) DEC8(128, false, 1) DEC8(64, true, 0) DEC8(64, false, 0)
     DEC8(128, true, 0) DEC8(128, false, 0) { return -2; }
 #undef DEC8
