@@ -55,7 +55,6 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, M, N, K, nt, u, ks, pipe, w8, ST(st));
   });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
-  m.def("gemm_set_persist", [](int mode) { return dnn_gemm_set_persist(mode); });
   m.def("gemm_set_res_prefetch", [](int on) { return dnn_gemm_set_res_prefetch(on); });
   m.def("gemm_set_skinny_max_m", [](int m) { return dnn_gemm_set_skinny_max_m(m); });
   m.def("gemm_fp8_set_tile", [](int tile) { return dnn_gemm_fp8_set_tile(tile); });

@@ -232,69 +232,19 @@ __device__ __forceinline__ void bg_read(bf16x8 (&f)[N][2], const char* half, int
     for (int s = 0; s < 2; ++s) f[i][s] = lds_frag(half, row0 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
 }
 
-// Persistent mode (gridDim.x < tiles, launch_gemm g_gemm_persist): a workgroup
-// walks logical tiles blockIdx.x, +gridDim.x, ... (a multiple of 8 apart, so
-// every tile of a workgroup stays on its XCD's slice of the xcd_remap order).
-// Once a tile's main loop has drained (every wave past its last LDS read) the
-// NEXT tile's prologue DMA is issued before this tile's epilogue, so the
-// operand fetch latency hides under the epilogue math and stores instead of
-// stalling the start of every tile (at K = 768 a 256^2 tile has only 12
-// K-steps; its fixed prologue + epilogue cost is ~1/3 of the tile).
 template <int ACT, bool OUT_F32>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
     int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
     int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
-  int lane = tid & 63;  // laundered per tile (below)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
-  const int ntiles = ntm * ntn;
-  int virt = blockIdx.x;
-  int m0, n0;
-  auto coords = [&](int v) {
-    int tm, tn;
-    tile_coords(xcd_remap(v, ntiles), ntm, ntn, tm, tn);
-    m0 = tm * BG_M;
-    n0 = tn * BG_N;
-  };
-  coords(virt);
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
+  const int m0 = tm * BG_M, n0 = tn * BG_N;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / BG_K;
-
-  // half-tile h of buffer u: A0=0, A1=1, B0=2, B1=3
-  auto half = [&](int u, int h) { return smem + (u * 4 + h) * BG_HALF; };
-  auto stA = [&](int u, int h, int t) {
-    t = t < nk ? t : nk - 1;
-    stage_half(A, lda, m0 + h * 128, M, t * BG_K, half(u, h), wave, lane);
-  };
-  auto stB = [&](int u, int h, int t) {
-    t = t < nk ? t : nk - 1;
-    stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
-  };
-  // prologue DMA: tile 0 complete and A0/B1 of tile 1 (the 4 youngest loads)
-  auto prologue = [&]() {
-    stA(0, 0, 0);
-    stB(0, 1, 0);
-    stA(0, 1, 0);
-    stB(0, 0, 0);
-    stA(1, 0, 1);
-    stB(1, 1, 1);
-  };
-  prologue();
-  const int arow = wr * 64, brow = wc * 32;
-
-  for (;;) {
-  // lane-derived addresses are recomputed per tile instead of being hoisted to
-  // kernel entry and kept live (spilled) across the whole tile loop
-  asm volatile("" : "+v"(lane));
-  // the prologue of this tile is in flight (issued above, or before the
-  // previous tile's epilogue); in persistent mode that epilogue's stores are
-  // younger than it, so wait for everything
-  if (virt == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bg_barrier();
-  if (wr == 1) bg_barrier();
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -306,7 +256,30 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // half-tile h of buffer u: A0=0, A1=1, B0=2, B1=3
+  auto half = [&](int u, int h) { return smem + (u * 4 + h) * BG_HALF; };
+  auto stA = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(A, lda, m0 + h * 128, M, t * BG_K, half(u, h), wave, lane);
+  };
+  auto stB = [&](int u, int h, int t) {
+    t = t < nk ? t : nk - 1;
+    stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
+  };
+
+  // prologue: tile 0 complete, A0/B1 of tile 1 in flight
+  stA(0, 0, 0);
+  stB(0, 1, 0);
+  stA(0, 1, 0);
+  stB(0, 0, 0);
+  stA(1, 0, 1);
+  stB(1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bg_barrier();
+  if (wr == 1) bg_barrier();
+
   bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 64, brow = wc * 32;
   // One K-tile; the loop runs two per iteration so the buffer index u is a
   // compile-time constant and every LDS address an immediate offset.
   auto ktile = [&](const int t, auto ucst) {
@@ -347,39 +320,43 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
-  // every wave is past its last LDS read: the buffers are free for the next
-  // tile's prologue DMA, issued before this tile's epilogue (persistent mode)
-  const int em0 = m0, en0 = n0;
-  const int next = virt + (int)gridDim.x;
-  if (next < ntiles) {
-    coords(next);
-    prologue();
-  }
 
   // Epilogue (transposed accumulators):
   //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
   //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
-  // folded pre-norm (prefill QKV / up projections): v = rstd acc - mean rstd
-  // colsum, applied per row group right before its stores (a tile-wide pass
-  // ahead of the stores kept two copies of the accumulators live at its join)
-  auto norm = [&](int mq, int nq, int i) {
-    if (rowstat == nullptr) return;
-    const float2 st = rowstat[min(em0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1)];
+  if (rowstat != nullptr) {  // folded pre-norm (prefill QKV / up projections)
+    // 8 row statistics and 4 column-sum vectors per lane, loaded once
+    float2 rs[2][4];
+    f32x4 cs[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = en0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
-      f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (colsum != nullptr) {
-        if (n + 3 < N) {
-          cs = *reinterpret_cast<const f32x4*>(colsum + n);
-        } else {
+    for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) cs[r] = n + r < N ? colsum[n + r] : 0.f;
+      for (int i = 0; i < 4; ++i) rs[mq][i] = rowstat[min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1)];
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
+        cs[nq][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (colsum != nullptr) {
+          if (n + 3 < N) {
+            cs[nq][j] = *reinterpret_cast<const f32x4*>(colsum + n);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[nq][j][r] = n + r < N ? colsum[n + r] : 0.f;
+          }
         }
       }
-      acc[mq][nq][i][j] = acc[mq][nq][i][j] * st.x + st.y * cs;
-    }
-  };
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq][nq][i][j] = acc[mq][nq][i][j] * rs[mq][i].x + rs[mq][i].y * cs[nq][j];
+  }
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
   // Residual epilogue: every residual load of the tile (32 x 8 B per lane, into
@@ -387,7 +364,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   // first output is computed, so the tile pays one memory round trip for R
   // instead of one per output row group (-20..-25 % GEMM throughput otherwise,
   // profiles/r2_gemm_epilogue_cost.jsonl).
-  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && en0 + 255 < N) {
+  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N) {
     bf16x4 rr[2][2][4][2];
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
@@ -395,29 +372,27 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          epi_pair_res_load(em0 + mq * 128 + arow + i * 16 + (lane & 15), en0 + nq * 128 + wc * 32, M, R, ldr, lane,
+          epi_pair_res_load(m0 + mq * 128 + arow + i * 16 + (lane & 15), n0 + nq * 128 + wc * 32, M, R, ldr, lane,
                             rr[mq][nq][i][0], rr[mq][nq][i][1]);
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          norm(mq, nq, i);
-          epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], em0 + mq * 128 + arow + i * 16 + (lane & 15),
-                                   en0 + nq * 128 + wc * 32, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, lane,
+        for (int i = 0; i < 4; ++i)
+          epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], m0 + mq * 128 + arow + i * 16 + (lane & 15),
+                                   n0 + nq * 128 + wc * 32, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, lane,
                                    rr[mq][nq][i][0], rr[mq][nq][i][1]);
-        }
-  } else {
+    return;
+  }
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        norm(mq, nq, i);
-        const int m = em0 + mq * 128 + arow + i * 16 + (lane & 15);
-        const int nb = en0 + nq * 128 + wc * 32;
+        const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
+        const int nb = n0 + nq * 128 + wc * 32;
         if (ACT == ACT_SILU_MUL) {
 #pragma unroll
           for (int j = 0; j < 2; ++j)
@@ -432,10 +407,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
                                  vec);
         }
       }
-  }
-  if (next >= ntiles) break;
-  virt = next;
-  }  // persistent tile loop
 }
 
 // ---------------------------------------------------------------------------
@@ -655,42 +626,6 @@ extern "C" int dnn_gemm_set_res_prefetch(int on) {
   return 0;
 }
 
-// 256^2 kernel: persistent grid (one workgroup per CU walking the tiles, next
-// tile's prologue under this tile's epilogue) when the tiles exceed the CUs.
-// In-process A/B (bench/gemm_persist_ab.py, profiles/r2_gemm_persist_ab.jsonl):
-// bit-identical, +1.6 / +2.0 % on the GELU projections (GPT-2 / GPT-2 XL c_fc,
-// the longest epilogue), -1..-1.7 % on the residual ones, +-0.5 % elsewhere —
-// the per-tile overhead at K = 768 is not operand latency.  1 = GELU epilogues
-// only (default), 2 = always, 0 = never.
-static int g_gemm_persist = 1;
-
-extern "C" int dnn_gemm_set_persist(int mode) {
-  if (mode < 0 || mode > 2) return -1;
-  g_gemm_persist = mode;
-  return 0;
-}
-
-// Compute units of the current device (cached per device id).
-static int device_cus() {
-  static int cus[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
-
-// Persistent grid for a tile count: the CU count rounded down to a multiple
-// of 8 (tiles of one workgroup then stay on one XCD's xcd_remap slice).
-static int persistent_grid(int tiles, int act) {
-  const int g = device_cus() & ~7;
-  const bool on = g_gemm_persist == 2 || (g_gemm_persist == 1 && act == ACT_GELU);
-  return (on && g >= 8 && tiles > g) ? g : tiles;
-}
-
 extern "C" int dnn_gemm_set_tile(int tile) {
   if (tile != 0 && tile != 128 && tile != 256) return -1;
   g_gemm_tile = tile;
@@ -725,7 +660,7 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   const bool big = g_gemm_tile == 256 ||
                    (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.4 * fill(tiles256, 256) > fill(tiles128, 512));
   if (big) {
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(persistent_grid(tiles256, ACT)), dim3(512), 0, st, (const bf16_t*)A, lda,
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
                        (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch, rowstat,
                        colsum);
     return;
