@@ -452,7 +452,7 @@ __device__ __forceinline__ void kv8_unpack(const i32x4& w, uint32_t (&p)[8]) {
 // halve; entries are converted to bf16 in registers (exact) before the same
 // v_dot2 math, and the new key/value row is rounded to e4m3 once — its score
 // uses the rounded copy, so the current step sees what later steps will read.
-template <int HD, int G, int FM, bool NT, bool MF = false, bool KV8 = false, int KV8U = 10>
+template <int HD, int G, int FM, bool NT, bool MF = false, bool KV8 = false, int RU = 0>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int ldq,
                                                           bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                           float* __restrict__ ws, int H, int Hkv, int S,
@@ -462,10 +462,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   constexpr bool FUSED = FM != 0;  // FM: 0 = q head-major + cached keys, 1 = fused QKV rows, 2 = fused + RoPE
   constexpr bool ROPE = FM == 2;
   static_assert(!(KV8 && MF), "fp8 KV cache: VALU score path only");
-  // rows in flight per thread: KV8 rows are half the bytes, so KV8U (10) rows
-  // keep the same bytes in flight and one batch covers 640 keys at hd 64 (the
-  // 512-567-token benchmark contexts take one K and one V round trip, not two)
-  constexpr int DEC_U = KV8 ? KV8U : dnn::DEC_U;
+  // rows in flight per thread (RU > 0 overrides): KV8 rows are half the bytes,
+  // so 10 rows keep the same bytes in flight and one batch covers 640 keys at
+  // hd 64 (the 512-567-token benchmark contexts take one K and one V round
+  // trip, not two).  bf16 MHA with 10 or 12 rows measured neutral (GPT-2 B=64
+  // 0.585 / 0.584 / 0.590 ms, profiles/r2_decode_rows_in_flight_bf16_ab.jsonl):
+  // that path is bound by the K/V bytes, not by its round trips
+  constexpr int DEC_U = RU > 0 ? RU : (KV8 ? 10 : dnn::DEC_U);
   static_assert(DEC_U % 2 == 0, "P.V folds key pairs");
   constexpr int ELT = KV8 ? 16 : 8;     // head dims per 16-B lane load
   constexpr int LPK = HD / ELT;         // lanes per key row (16 B each)
