@@ -99,10 +99,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), V, Pn, ST(st));
   });
   m.def("qkv_split", [](u64 qkv, u64 q, u64 kc, u64 vc, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
-                        u64 cos, u64 sin, int rope, u64 st) {
+                        u64 cos, u64 sin, int rope, u64 st, int kv8) {
     return dnn_qkv_split(CP(qkv), P(q), P(kc), P(vc), B, T, H, Hkv, hd, S, CIP(pos), CFP(cos), CFP(sin), rope,
-                         ST(st));
-  });
+                         ST(st), kv8);
+  }, py::arg("qkv"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("B"), py::arg("T"), py::arg("H"),
+     py::arg("Hkv"), py::arg("hd"), py::arg("S"), py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("rope"),
+     py::arg("st"), py::arg("kv8") = 0);
   m.def("flash_attn_qkv", [](u64 qkv, int ldqkv, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S,
                              u64 pos, float scale, u64 st, int kv8) {
     return dnn_flash_attn_qkv(CP(qkv), ldqkv, P(kc), P(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st), kv8);
@@ -110,9 +112,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("H"), py::arg("Hkv"), py::arg("hd"), py::arg("S"), py::arg("pos"), py::arg("scale"), py::arg("st"),
      py::arg("kv8") = 0);
   m.def("flash_attn", [](u64 q, u64 kc, u64 vc, u64 o, int B, int T, int H, int Hkv, int hd, int S, u64 pos,
-                         float scale, u64 st) {
-    return dnn_flash_attn(CP(q), CP(kc), CP(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st));
-  });
+                         float scale, u64 st, int kv8) {
+    return dnn_flash_attn(CP(q), CP(kc), CP(vc), P(o), B, T, H, Hkv, hd, S, CIP(pos), scale, ST(st), kv8);
+  }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("o"), py::arg("B"), py::arg("T"), py::arg("H"),
+     py::arg("Hkv"), py::arg("hd"), py::arg("S"), py::arg("pos"), py::arg("scale"), py::arg("st"), py::arg("kv8") = 0);
   m.def("attn_decode", [](u64 q, u64 kc, u64 vc, u64 o, int B, int H, int Hkv, int hd, int S, u64 lens,
                           float scale, int splits, u64 ws, u64 st, int kv8) {
     return dnn_attn_decode(CP(q), CP(kc), CP(vc), P(o), B, H, Hkv, hd, S, CIP(lens), scale, splits, FP(ws), ST(st),

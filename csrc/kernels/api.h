@@ -48,11 +48,11 @@ int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* 
 int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d, const int* pos,
                    int V, int P, hipStream_t st);
 int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
-                  const int* pos, const float* cos, const float* sin, int rope, hipStream_t st);
+                  const int* pos, const float* cos, const float* sin, int rope, hipStream_t st, int kv8 = 0);
 int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H, int Hkv,
                        int hd, int S, const int* pos, float scale, hipStream_t st, int kv8 = 0);
 int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv, int hd, int S,
-                   const int* pos, float scale, hipStream_t st);
+                   const int* pos, float scale, hipStream_t st, int kv8 = 0);
 int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd, int S,
                         const int* pos, const float* cosT, const float* sinT, float scale, int splits, float* ws,
                         hipStream_t st, int kv8 = 0);

@@ -40,6 +40,33 @@ __device__ unsigned long long dec_probe_ts[32];
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// e4m3 KV cache (KV8) conversions of 8 entries: bf16 -> OCP e4m3 (RNE,
+// saturated to +-448 first: the hardware convert does not clamp) and back
+// (exact: v_cvt_scalef32_pk_bf16_fp8 at scale 1).
+__device__ __forceinline__ uint2 kv8_pack8(const i32x4& x) {  // 8 bf16 -> 8 e4m3
+  int lo = 0, hi = 0;
+  float f[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] << 16), -448.f), 448.f);
+    f[2 * i + 1] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] & 0xffff0000u), -448.f), 448.f);
+  }
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return make_uint2((uint32_t)lo, (uint32_t)hi);
+}
+__device__ __forceinline__ i32x4 kv8_unpack8(const uint2 w) {  // 8 e4m3 -> 8 bf16
+  i32x4 r;
+  r[0] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false));
+  r[1] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true));
+  r[2] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false));
+  r[3] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true));
+  return r;
+}
+
+
 // ---------------------------------------------------------------------------
 // QKV split: qkv rows r = b*T + t, columns [q H*hd | k Hkv*hd | v Hkv*hd].
 // q -> q_out[b][h][t][:] (RoPE'd when rope), k/v -> cache[b][hkv][pos[b]+t][:].
@@ -50,7 +77,7 @@ __global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict
                                                         bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int B, int T,
                                                         int H, int Hkv, int hd, int S, const int* __restrict__ pos,
                                                         const float* __restrict__ cosT, const float* __restrict__ sinT,
-                                                        int rope) {
+                                                        int rope, int kv8) {
   const int half = hd / 2, groups = half / 8;
   const int heads = H + 2 * Hkv;
   const long total = (long)B * T * heads * groups;
@@ -77,6 +104,13 @@ __global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict
         y1[j] = (short)f2bf(a * co - c * si);
         y2[j] = (short)f2bf(c * co + a * si);
       }
+    }
+    if (kv8 && hh >= H) {  // e4m3 cache rows: 8 + 8 bytes
+      uint8_t* d8 = reinterpret_cast<uint8_t*>(hh < H + Hkv ? kc : vc) +
+                    (((size_t)b * Hkv + (hh < H + Hkv ? hh - H : hh - H - Hkv)) * S + p) * hd;
+      *reinterpret_cast<uint2*>(d8 + i0) = kv8_pack8(__builtin_bit_cast(i32x4, y1));
+      *reinterpret_cast<uint2*>(d8 + half + i0) = kv8_pack8(__builtin_bit_cast(i32x4, y2));
+      continue;
     }
     bf16_t* dst;
     if (hh < H) {
@@ -115,32 +149,6 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
-// KV8 (QKV mode): the cache is e4m3 (decode attention's KV8 layout): new rows
-// are rounded once when copied in, cached rows are widened to bf16 as they are
-// fetched; this chunk's own keys/values come from the bf16 c_attn output.
-__device__ __forceinline__ uint2 kv8_pack8(const i32x4& x) {  // 8 bf16 -> 8 e4m3
-  int lo = 0, hi = 0;
-  float f[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] << 16), -448.f), 448.f);
-    f[2 * i + 1] = fminf(fmaxf(__uint_as_float((uint32_t)x[i] & 0xffff0000u), -448.f), 448.f);
-  }
-  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
-  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
-  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
-  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
-  return make_uint2((uint32_t)lo, (uint32_t)hi);
-}
-__device__ __forceinline__ i32x4 kv8_unpack8(const uint2 w) {  // 8 e4m3 -> 8 bf16
-  i32x4 r;
-  r[0] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false));
-  r[1] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true));
-  r[2] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false));
-  r[3] = __builtin_bit_cast(int, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true));
-  return r;
-}
-
 template <int HD, bool QKV = false, bool KV8 = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
@@ -169,7 +177,6 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const int blk_qmax = p0 + min(qb * FA_QB + FA_QB - 1, T - 1);
   const int kv_end = min(min(kv_len, blk_qmax + 1), S);  // never read past the cache
 
-  static_assert(!KV8 || QKV, "fp8 KV cache: QKV-mode prefill only");
   const bf16_t* krow_new = nullptr;  // QKV: this sequence's new-key rows (position p0 + t = row b*T + t)
   const bf16_t* vrow_new = nullptr;
   if constexpr (QKV) {
@@ -461,7 +468,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           int chunk_cap, bf16_t* __restrict__ o_direct) {
   constexpr bool FUSED = FM != 0;  // FM: 0 = q head-major + cached keys, 1 = fused QKV rows, 2 = fused + RoPE
   constexpr bool ROPE = FM == 2;
-  static_assert(!(KV8 && MF), "fp8 KV cache: VALU score path only");
   // rows in flight per thread (RU > 0 overrides): KV8 rows are half the bytes,
   // so 10 rows keep the same bytes in flight and one batch covers 640 keys at
   // hd 64 (the 512-567-token benchmark contexts take one K and one V round
@@ -576,6 +582,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         load_head8<HD, ROPE>(q + (size_t)b * ldq + (H + kvh) * HD, c4 + 4 * m, cosT, sinT, min(p_new, S - 1), t8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) nkA[m][j] = (short)f2bf(t8[j]);
+        if constexpr (KV8)  // the register copy = the stored e4m3 row
+          nkA[m] = __builtin_bit_cast(bf16x8, kv8_unpack8(kv8_pack8(__builtin_bit_cast(i32x4, nkA[m]))));
       }
     }
     const int ntile = (n + 15) / 16;
@@ -586,8 +594,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         const int kk = min((t0 + tb * 4 + wave) * 16 + hj, n - 1);
 #pragma unroll
         for (int m = 0; m < NKC; ++m) {
-          const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + (c4 + 4 * m) * 8);
-          ka[tb][m] = NT ? __builtin_nontemporal_load(kp) : *kp;
+          if constexpr (KV8) {  // 8 e4m3 entries -> the same bf16 A fragment
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2* kp8 = reinterpret_cast<const u32x2*>(kb8 + (size_t)(k0 + kk) * HD + (c4 + 4 * m) * 8);
+            const u32x2 w = NT ? __builtin_nontemporal_load(kp8) : *kp8;
+            ka[tb][m] = __builtin_bit_cast(bf16x8, kv8_unpack8(make_uint2(w[0], w[1])));
+          } else {
+            const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)(k0 + kk) * HD + (c4 + 4 * m) * 8);
+            ka[tb][m] = NT ? __builtin_nontemporal_load(kp) : *kp;
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -819,21 +834,32 @@ __global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __re
 using namespace dnn;
 
 extern "C" int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B, int T, int H, int Hkv, int hd, int S,
-                             const int* pos, const float* cos, const float* sin, int rope, hipStream_t st) {
+                             const int* pos, const float* cos, const float* sin, int rope, hipStream_t st, int kv8) {
   if (hd % 16 != 0 || H % Hkv != 0) return -1;
   const long total = (long)B * T * (H + 2 * Hkv) * (hd / 16);
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(qkv_split_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)q, (bf16_t*)kc,
-                     (bf16_t*)vc, B, T, H, Hkv, hd, S, pos, cos, sin, rope);
+                     (bf16_t*)vc, B, T, H, Hkv, hd, S, pos, cos, sin, rope, kv8);
   return (int)hipGetLastError();
 }
 
 extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,
-                              int hd, int S, const int* pos, float scale, hipStream_t st) {
+                              int hd, int S, const int* pos, float scale, hipStream_t st, int kv8) {
   if (H % Hkv != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
+  if (kv8) {  // e4m3 cache: every key / value row widened as it is fetched
+    if (hd == 64)
+      hipLaunchKernelGGL((flash_attn_kernel<64, false, true>), grid, dim3(256), 0, st, (const bf16_t*)q,
+                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+    else if (hd == 128)
+      hipLaunchKernelGGL((flash_attn_kernel<128, false, true>), grid, dim3(256), 0, st, (const bf16_t*)q,
+                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+    else
+      return -2;
+    return (int)hipGetLastError();
+  }
   if (hd == 64) {
     hipLaunchKernelGGL((flash_attn_kernel<64>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
                        (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
@@ -882,7 +908,7 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
                               float* ws, bool fused, hipStream_t st, bool kv8 = false) {
   const int G = H / Hkv;
   if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
-  if (kv8 && G != 1) return -4;  // e4m3 cache: MHA (the VALU score path) only
+  if (kv8 && G != 1 && hd != 128) return -4;  // e4m3 cache: MHA, or GQA at hd 128 (Llama-3)
   const int chunk_cap = (S + splits - 1) / splits;
   const int gpb = 256 / (hd / (kv8 ? 16 : 8));
   size_t smem = sizeof(float) * (size_t)G * (size_t)(chunk_cap > gpb * hd ? chunk_cap : gpb * hd);
@@ -910,6 +936,18 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
                          (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, nullptr, nullptr, sl2,  \
                          chunk_cap, (bf16_t*)o);                                                                      \
   } else
+    if (G > 1) {  // GQA: MFMA key tiles (hd 128: Llama-3 G = 4, llama3-tiny G = 2)
+#define DEC8G(GV, NTV, FMV)                                                                                           \
+  if (G == GV && nt == NTV && fm == FMV)                                                                              \
+    hipLaunchKernelGGL((attn_decode_kernel<128, GV, FMV, NTV, true, true>), grid, dim3(256), smem, st,                \
+                       (const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2,         \
+                       chunk_cap, (bf16_t*)o);                                                                        \
+  else
+      DEC8G(4, true, 2) DEC8G(4, false, 2) DEC8G(4, true, 1) DEC8G(4, false, 1) DEC8G(4, true, 0) DEC8G(4, false, 0)
+      DEC8G(2, true, 2) DEC8G(2, false, 2) DEC8G(2, true, 1) DEC8G(2, false, 1) DEC8G(2, true, 0) DEC8G(2, false, 0)
+      { return -2; }
+#undef DEC8G
+    } else
     DEC8(64, true, 1) DEC8(64, false, 1) DEC8(128, true, 1) DEC8(128, false, 1) DEC8(64, true, 0) DEC8(64, false, 0)
     DEC8(128, true, 0) DEC8(128, false, 0) { return -2; }
 #undef DEC8
@@ -970,7 +1008,6 @@ extern "C" int dnn_attn_decode_qkv(const void* qkv, int ldqkv, void* kc, void* v
                                    int hd, int S, const int* pos, const float* cosT, const float* sinT, float scale,
                                    int splits, float* ws, hipStream_t st, int kv8) {
   if (ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
-  if (kv8 && cosT != nullptr) return -4;  // e4m3 cache: no-RoPE (GPT-2 family) fused path
   return attn_decode_launch(qkv, ldqkv, kc, vc, o, B, H, Hkv, hd, S, pos, cosT, sinT, scale, splits, ws, true, st,
                             kv8 != 0);
 }

@@ -87,32 +87,6 @@ def embed(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], out
     return out
 
 
-def qkv_split(qkv: torch.Tensor, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, B: int, T: int, H: int,
-              Hkv: int, hd: int, pos: torch.Tensor, cos: Optional[torch.Tensor] = None,
-              sin: Optional[torch.Tensor] = None) -> None:
-    S = kc.shape[2]
-    if kc.shape[:2] != (B, Hkv) or kc.shape[3] != hd or vc.shape != kc.shape:
-        raise ValueError(f"qkv_split: cache {tuple(kc.shape)} does not match B={B} Hkv={Hkv} hd={hd}")
-    if qkv.numel() < B * T * (H + 2 * Hkv) * hd or q.numel() < B * T * H * hd:
-        raise ValueError("qkv_split: buffers too small")
-    rope = cos is not None
-    check(lib().qkv_split(ptr(qkv), ptr(q), ptr(kc), ptr(vc), B, T, H, Hkv, hd, S, ptr(pos), ptr(cos), ptr(sin),
-                          1 if rope else 0, stream_ptr()), "qkv_split")
-
-
-def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,
-               Hkv: int, hd: int, pos: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
-    """Causal attention of T new queries per sequence against the cache
-    (positions 0..pos[b]+T-1). q (B,H,T,hd); out (B*T, H*hd)."""
-    if hd not in (64, 128):
-        raise ValueError(f"flash_attn: head_dim {hd} unsupported (64/128)")
-    S = kc.shape[2]
-    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
-    check(lib().flash_attn(ptr(q), ptr(kc), ptr(vc), ptr(out), B, T, H, Hkv, hd, S, ptr(pos), scale, stream_ptr()),
-          "flash_attn")
-    return out
-
-
 KV8_DTYPES = (torch.float8_e4m3fn, torch.uint8)  # e4m3 KV cache storage (unit scale)
 
 
@@ -125,6 +99,32 @@ def _kv8(kc: torch.Tensor, vc: torch.Tensor) -> int:
     if not k8 and kc.dtype != torch.bfloat16:
         raise TypeError(f"KV cache dtype {kc.dtype}: bf16 or float8_e4m3fn")
     return 1 if k8 else 0
+
+
+def qkv_split(qkv: torch.Tensor, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, B: int, T: int, H: int,
+              Hkv: int, hd: int, pos: torch.Tensor, cos: Optional[torch.Tensor] = None,
+              sin: Optional[torch.Tensor] = None) -> None:
+    S = kc.shape[2]
+    if kc.shape[:2] != (B, Hkv) or kc.shape[3] != hd or vc.shape != kc.shape:
+        raise ValueError(f"qkv_split: cache {tuple(kc.shape)} does not match B={B} Hkv={Hkv} hd={hd}")
+    if qkv.numel() < B * T * (H + 2 * Hkv) * hd or q.numel() < B * T * H * hd:
+        raise ValueError("qkv_split: buffers too small")
+    rope = cos is not None
+    check(lib().qkv_split(ptr(qkv), ptr(q), ptr(kc), ptr(vc), B, T, H, Hkv, hd, S, ptr(pos), ptr(cos), ptr(sin),
+                          1 if rope else 0, stream_ptr(), kv8=_kv8(kc, vc)), "qkv_split")
+
+
+def flash_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,
+               Hkv: int, hd: int, pos: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
+    """Causal attention of T new queries per sequence against the cache
+    (positions 0..pos[b]+T-1). q (B,H,T,hd); out (B*T, H*hd)."""
+    if hd not in (64, 128):
+        raise ValueError(f"flash_attn: head_dim {hd} unsupported (64/128)")
+    S = kc.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    check(lib().flash_attn(ptr(q), ptr(kc), ptr(vc), ptr(out), B, T, H, Hkv, hd, S, ptr(pos), scale, stream_ptr(),
+                           kv8=_kv8(kc, vc)), "flash_attn")
+    return out
 
 
 def flash_attn_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor, B: int, T: int, H: int,

@@ -120,11 +120,11 @@ class TransformerStage(StageCompute):
         # KV cache: [layer] -> (B, Hkv, S, hd)
         L = len(self.layers)
         # KV cache: bf16, or OCP e4m3 ("fp8": half the bytes every decode step
-        # streams; MHA without RoPE, i.e. the GPT-2 family, attention.hip KV8)
+        # streams; attention.hip KV8: MHA, or GQA at head dim 128)
         if kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype {kv_dtype!r}: bf16 or fp8")
-        if kv_dtype == "fp8" and (self.Hkv != self.H or self.family != "gpt2"):
-            raise ValueError("fp8 KV cache: multi-head attention without RoPE (GPT-2 family) only")
+        if kv_dtype == "fp8" and self.Hkv != self.H and (self.hd != 128 or self.H // self.Hkv not in (2, 4)):
+            raise ValueError("fp8 KV cache: MHA, or GQA with head dim 128 and 2 or 4 query heads per kv head")
         self.kv_dtype = kv_dtype
         kvt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
         self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=kvt, device=dev)

@@ -116,7 +116,7 @@ def test_extension_field_defaults_and_values():
 
 
 def test_kv_cache_dtype():
-    """``kv_cache_dtype``: bf16 (default) or fp8 (OCP e4m3, GPT-2 family only)."""
+    """``kv_cache_dtype``: bf16 (default) or fp8 (OCP e4m3)."""
     c = json.loads(json.dumps(REF))
     assert resolve_node(c, "node1").pipeline.kv_cache_dtype == "bf16"
     c.update(model="gpt2", kv_cache_dtype="fp8")
@@ -125,5 +125,4 @@ def test_kv_cache_dtype():
     with pytest.raises(ConfigError, match="kv_cache_dtype"):
         resolve_node(c, "node1")
     c.update(model="llama3-8b", kv_cache_dtype="fp8")
-    with pytest.raises(ConfigError, match="kv_cache_dtype"):
-        resolve_node(c, "node1")
+    assert resolve_node(c, "node1").pipeline.kv_cache_dtype == "fp8"

@@ -1,4 +1,4 @@
-"""OCP e4m3 KV cache (attention.hip KV8): decode attention and QKV-mode prefill
+"""OCP e4m3 KV cache (attention.hip KV8): decode attention (MHA and GQA) and prefill
 against fp32 references over the dequantised cache (MI355X only)."""
 import pytest
 import torch
@@ -112,3 +112,111 @@ def test_gpt2_decode_kv8_close_to_bf16():
     assert torch.equal(t16[:, 0], t8[:, 0])
     assert (t16 == t8).float().mean().item() >= 0.75
     assert _rel(l8, l16) < 5e-2
+
+
+def _rope(x, cos, sin, p):
+    """Rotate-half RoPE of x (..., hd) at positions p (broadcast over heads), fp32."""
+    h2 = x.shape[-1] // 2
+    c, s_ = cos[p][:, None], sin[p][:, None]
+    x1, x2 = x[..., :h2], x[..., h2:]
+    return torch.cat([x1 * c - x2 * s_, x2 * c + x1 * s_], -1)
+
+
+@pytest.mark.parametrize("B,H,Hkv,S,pos,splits,rope", [(3, 32, 8, 400, [0, 200, 399], 1, True),
+                                                       (2, 8, 4, 300, [150, 17], 2, True),
+                                                       (2, 32, 8, 300, [5, 250], 1, False)])
+def test_attn_decode_qkv_kv8_gqa(B, H, Hkv, S, pos, splits, rope):
+    """GQA (MFMA key tiles, hd 128) on an e4m3 cache, with the fused RoPE: the new
+    row is stored as torch's e4m3 rounding of the RoPE'd bf16 key, and the output
+    matches fp32 attention over the dequantised cache."""
+    import dataclasses
+    from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(8)
+    hd, G = 128, H // Hkv
+    kc, vc = _q8(torch.randn(B, Hkv, S, hd, device=DEV) * 2), _q8(torch.randn(B, Hkv, S, hd, device=DEV))
+    qkv = torch.randn(B, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    p = torch.tensor(pos, device=DEV, dtype=torch.int32)
+    cos = sin = None
+    if rope:
+        cfg = LLAMA_CONFIGS["llama3-tiny"]
+        cos, sin = rope_tables(dataclasses.replace(cfg, n_embd=hd * cfg.n_head), S)
+        cos, sin = cos.to(DEV), sin.to(DEV)
+    ws = torch.empty(B * Hkv * splits * G * (hd + 2), device=DEV)
+    out = torch.empty(B, H * hd, device=DEV, dtype=torch.bfloat16)
+    T.attn_decode_qkv(qkv, kc, vc, out, B, H, Hkv, hd, p, ws, splits, cos, sin)
+    torch.cuda.synchronize()
+    x = qkv.float()
+    q = x[:, :H * hd].view(B, H, hd)
+    kn = x[:, H * hd:(H + Hkv) * hd].view(B, Hkv, hd)
+    vn = x[:, (H + Hkv) * hd:].view(B, Hkv, hd)
+    if rope:
+        q = _rope(q, cos, sin, p.long()).bfloat16().float()
+        kn = _rope(kn, cos, sin, p.long()).bfloat16().float()
+    for b, pb in enumerate(pos):
+        assert torch.equal(kc[b, :, pb].float(), _q8(kn[b]).float()), "new key row"
+        assert torch.equal(vc[b, :, pb].float(), _q8(vn[b]).float()), "new value row"
+    ref = torch.empty(B, H, hd, device=DEV)
+    for b, pb in enumerate(pos):
+        k = kc[b, :, :pb + 1].float().repeat_interleave(G, 0)
+        v = vc[b, :, :pb + 1].float().repeat_interleave(G, 0)
+        s = torch.einsum("hd,hkd->hk", q[b], k) / hd ** 0.5
+        ref[b] = torch.einsum("hk,hkd->hd", torch.softmax(s, -1), v)
+    assert _rel(out.view(B, H, hd), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,Tn,H,Hkv,hd,pos0", [(2, 77, 8, 2, 128, 0), (1, 33, 4, 1, 128, 40), (3, 130, 4, 4, 64, 17)])
+def test_qkv_split_flash_kv8(B, Tn, H, Hkv, hd, pos0):
+    """qkv_split into an e4m3 cache (rows = torch's e4m3 rounding) and flash
+    attention reading every key/value from it, vs fp32 over the dequantised cache."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(10)
+    S = pos0 + Tn + 16
+    kc, vc = _q8(torch.randn(B, Hkv, S, hd, device=DEV)), _q8(torch.randn(B, Hkv, S, hd, device=DEV))
+    qkv = torch.randn(B * Tn, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    q = torch.empty(B * H * Tn * hd, device=DEV, dtype=torch.bfloat16)
+    pos = torch.full((B,), pos0, device=DEV, dtype=torch.int32)
+    T.qkv_split(qkv, q, kc, vc, B, Tn, H, Hkv, hd, pos)
+    out = torch.empty(B * Tn, H * hd, device=DEV, dtype=torch.bfloat16)
+    T.flash_attn(q, kc, vc, out, B, Tn, H, Hkv, hd, pos)
+    torch.cuda.synchronize()
+    x = qkv.view(B, Tn, H + 2 * Hkv, hd)
+    assert torch.equal(q.view(B, H, Tn, hd), x[:, :, :H].transpose(1, 2))
+    assert torch.equal(kc[:, :, pos0:pos0 + Tn].float(), _q8(x[:, :, H:H + Hkv].transpose(1, 2)).float())
+    assert torch.equal(vc[:, :, pos0:pos0 + Tn].float(), _q8(x[:, :, H + Hkv:].transpose(1, 2)).float())
+    k = kc[:, :, :pos0 + Tn].float().repeat_interleave(H // Hkv, 1)
+    v = vc[:, :, :pos0 + Tn].float().repeat_interleave(H // Hkv, 1)
+    mask = torch.ones(Tn, pos0 + Tn, dtype=torch.bool, device=DEV).tril(diagonal=pos0)
+    ref = F.scaled_dot_product_attention(q.view(B, H, Tn, hd).float(), k, v, attn_mask=mask)
+    assert _rel(out, ref.transpose(1, 2).reshape(B * Tn, H * hd)) < 2e-2
+
+
+def test_llama_tiny_decode_kv8_close_to_bf16():
+    """llama3-tiny (GQA G = 2, hd 128, RoPE), 2 stages on the decode ring with the
+    e4m3 cache vs the bf16 cache: most tokens identical, last logits within 12 %
+    (measured 8 %: unlike the GPT-2 QKV-mode prefill, qkv_split stores the
+    prompt's own keys at e4m3 too, and the unit scale leaves this model's small
+    K/V entries few mantissa bits; the kernels themselves are pinned exactly
+    against the dequantised cache above)."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import model_info
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "llama3-tiny"
+    n = model_info(model).num_layers
+    ranges = [(0, n // 2 - 1), (n // 2, n - 1)]
+    V = model_info(model).cfg.vocab_size
+    B, T0, steps = 4, 48, 8
+    prompt = torch.randint(0, V, (B, T0), generator=torch.Generator().manual_seed(5))
+    res = {}
+    for kv in ("bf16", "fp8"):
+        stages = [TransformerStage(model, ckpt.random_stage_state_dict(model, a, b, i == 0, i == 1, 7, nontrivial=True),
+                                   a, b, i == 0, i == 1, DEV, max_batch=B, max_seq=T0 + steps + 2, kv_dtype=kv)
+                  for i, (a, b) in enumerate(ranges)]
+        toks = DecodeRing(stages, RingLinks(), 1, 1, B).generate([prompt], T0, steps)
+        torch.cuda.synchronize()
+        res[kv] = (toks.cpu().clone(), stages[-1].logits[:B, :V].float().cpu().clone())
+        del stages
+    (t16, l16), (t8, l8) = res["bf16"], res["fp8"]
+    assert (t16 == t8).float().mean().item() >= 0.75
+    assert _rel(l8, l16) < 0.12
