@@ -27,6 +27,8 @@ def apply(switch: str, v: int) -> None:
         gemm.FOLD_NORM_PREFILL = bool(v)
     elif switch == "kv8_u":  # fp8-KV decode attention rows in flight per thread (attention.hip KV8U)
         os.environ["DNN_KV8_U"] = str(v)
+    elif switch == "qkv_scatter":  # prefill c_attn straight into q / the KV caches (ops/gemm.py QKV_SCATTER)
+        gemm.QKV_SCATTER = bool(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

@@ -232,11 +232,36 @@ __device__ __forceinline__ void bg_read(bf16x8 (&f)[N][2], const char* half, int
     for (int s = 0; s < 2; ++s) f[i][s] = lds_frag(half, row0 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
 }
 
-template <int ACT, bool OUT_F32>
+// QKV scatter epilogue (prefill c_attn, no RoPE): output column c of row
+// m = b*T + t lands head-major — q -> q[b][h][t][:], k / v -> the KV caches at
+// position pos[b] + t — instead of in a (M, (H+2Hkv) hd) qkv row, so the flash
+// prefill reads contiguous K/V from the cache and no longer copies them there
+// (bench/flash_copy_probe.py: 21 us of a 116 us GPT-2 attention layer).
+struct QkvScatter {
+  bf16_t* q;
+  bf16_t* k;
+  bf16_t* v;
+  const int* pos;
+  int T, H, Hkv, hd, S;
+};
+
+// 8 consecutive output columns c..c+7 (one head) of row m -> destination.
+__device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c) {
+  const int b = m / sc.T, t = m - b * sc.T;
+  const int qw = sc.H * sc.hd, kw = sc.Hkv * sc.hd;
+  if (c < qw) return sc.q + (((size_t)b * sc.H + c / sc.hd) * sc.T + t) * sc.hd + c % sc.hd;
+  const int p = sc.pos[b] + t;
+  if (p >= sc.S) return nullptr;  // past the cache capacity: dropped, as in qkv_split
+  const bool isk = c < qw + kw;
+  const int cc = isk ? c - qw : c - qw - kw;
+  return (isk ? sc.k : sc.v) + (((size_t)b * sc.Hkv + cc / sc.hd) * sc.S + p) * sc.hd + cc % sc.hd;
+}
+
+template <int ACT, bool OUT_F32, bool SCATTER = false>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
     int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
-    int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum) {
+    int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum, QkvScatter scat = {}) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
@@ -397,6 +422,25 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             epi_silu_t4<OUT_F32>(acc[mq][nq][i][j], m, (nb + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
+        } else if (SCATTER) {
+          // widened 16-B stores as in epi_pair_bf16, to the head-major / cache
+          // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
+          // residual, N % 256 == 0, hd % 8 == 0 -> every pair is whole)
+          f32x4 a0 = acc[mq][nq][i][0], a1 = acc[mq][nq][i][1];
+          const int q = lane >> 4;
+          if (bias != nullptr) {
+            a0 += *reinterpret_cast<const f32x4*>(bias + nb + q * 4);
+            a1 += *reinterpret_cast<const f32x4*>(bias + nb + 16 + q * 4);
+          }
+          const uint32_t x0 = pack2bf(a0[0], a0[1]), x1 = pack2bf(a0[2], a0[3]);
+          const uint32_t y0 = pack2bf(a1[0], a1[1]), y1 = pack2bf(a1[2], a1[3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+          if (m < M) {
+            const int c = nb + ((q & 1) << 4) + ((q >> 1) << 3);
+            bf16_t* d = qkv_dest(scat, m, c);
+            if (d != nullptr) *reinterpret_cast<uint4*>(d) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
         } else if (!OUT_F32 && pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
                              bias, R, ldr, lane);
@@ -696,6 +740,26 @@ extern "C" int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_
   const int n = M * F;
   hipLaunchKernelGGL(silu_mul_packed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, (const bf16_t*)gu, ld_in,
                      (bf16_t*)out, ld_out, M, F);
+  return (int)hipGetLastError();
+}
+
+// Prefill c_attn with the QKV scatter epilogue (gemm_bf16_256_kernel SCATTER):
+// y = x W^T + bias (folded pre-norm when rowstat) written head-major: q ->
+// (B, H, T, hd), k / v -> the (B, Hkv, S, hd) caches at rows pos[b] + t.  M =
+// B*T.  Returns -3 when the shape does not fit the 256^2 path (the caller then
+// uses the qkv row output + qkv_split).
+extern "C" int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, int ldw, const float* bias,
+                                         const float* rowstat, const float* colsum, void* q, void* kc, void* vc,
+                                         const int* pos, int B, int T, int H, int Hkv, int hd, int S, int K,
+                                         hipStream_t st) {
+  const int M = B * T, N = (H + 2 * Hkv) * hd;
+  if (K % 64 != 0 || M <= 0 || hd % 8 != 0 || (colsum != nullptr && rowstat == nullptr)) return -1;
+  if (N % 256 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
+  const int tiles = ((M + BG_M - 1) / BG_M) * (N / BG_N);
+  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, hd, S};
+  hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(tiles), dim3(512), 0, st, (const bf16_t*)A,
+                     lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, N, K, 0,
+                     reinterpret_cast<const float2*>(rowstat), colsum, sc);
   return (int)hipGetLastError();
 }
 

@@ -73,7 +73,7 @@ int main() {
   expect_reject(dnn_attn_decode(p, p, p, p, 1, 4, 4, 64, 16, ip, 0.1f, 0, f, st), "decode splits=0");
   expect_reject(dnn_attn_decode(p, p, p, p, 1, 32, 2, 64, 16, ip, 0.1f, 1, f, st), "decode G>8");
   expect_reject(dnn_attn_decode(p, p, p, p, 1, 4, 4, 96, 16, ip, 0.1f, 1, f, st), "decode hd=96");
-  expect_reject(dnn_attn_decode(p, p, p, p, 1, 8, 2, 64, 16, ip, 0.1f, 1, f, st, 1), "decode fp8 KV with GQA");
+  expect_reject(dnn_attn_decode(p, p, p, p, 1, 8, 2, 64, 16, ip, 0.1f, 1, f, st, 1), "decode fp8 KV, GQA at hd 64");
   expect_reject(dnn_attn_decode_qkv(p, 100, p, p, p, 1, 4, 4, 64, 16, ip, nullptr, nullptr, 0.1f, 1, f, st),
                 "decode_qkv ldqkv too small");
   // sampling

@@ -201,6 +201,37 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
                                  ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws)), "gemm_skinny_norm")
     return out
 
+QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)
+
+
+def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q: torch.Tensor, kc: torch.Tensor,
+                     vc: torch.Tensor, pos: torch.Tensor, B: int, T: int, H: int, Hkv: int, hd: int) -> bool:
+    """Prefill c_attn (folded pre-norm, no RoPE) with the QKV scatter epilogue
+    (gemm_bf16.hip ``dnn_gemm_bf16_qkv_scatter``): q lands in ``q`` as (B, H, T,
+    hd) and K / V straight in the bf16 caches at rows ``pos[b] + t``, so the head-
+    major flash prefill follows without a qkv_split or an in-kernel cache copy.
+    Returns False (nothing launched) where it does not apply: fp8 weights or
+    cache, decode-sized M, or a shape off the 256^2 tile path."""
+    from .fp8 import Fp8Weight
+    if not (QKV_SCATTER and FOLD_NORM_PREFILL) or isinstance(f.w, Fp8Weight) or kc.dtype != torch.bfloat16:
+        return False
+    M, K = x.shape
+    N = f.w.shape[0]
+    if M != B * T or N != (H + 2 * Hkv) * hd or skinny_rows(M, N) or x.stride(1) != 1:
+        return False
+    if not (kc.is_contiguous() and vc.is_contiguous()) or q.numel() < M * H * hd or pos.dtype != torch.int32:
+        return False
+    from .transformer_ops import row_stats
+    st = std_buf.reshape(-1)[:4 * M].view(torch.float32).view(M, 2)
+    row_stats(x, st, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+    rc = lib().gemm_bf16_qkv_scatter(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(f.bias), ptr(st), ptr(f.colsum),
+                                     ptr(q), ptr(kc), ptr(vc), ptr(pos), B, T, H, Hkv, hd, kc.shape[2], K, stream_ptr())
+    if rc == -3:  # off the 256^2 path: the caller runs the qkv-row GEMM instead (st is recomputed there)
+        return False
+    check(rc, "gemm_bf16_qkv_scatter")
+    return True
+
+
 def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
     """Pre-shuffle a decode weight [N, K] (bf16, or e4m3 bytes) into the skinny
     GEMM's MFMA fragment order: for column tile t (16 rows) and 64-B chunk c,

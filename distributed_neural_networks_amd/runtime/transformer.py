@@ -35,7 +35,8 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import transformer_ops as T_
-from ..ops.gemm import ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up, skinny_rows
+from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up,
+                        qkv_scatter_norm, skinny_rows)
 from .stages import StageCompute, StageOutput
 
 
@@ -283,14 +284,21 @@ class TransformerStage(StageCompute):
         ws = self.ws[r0 * self.ws_per_seq:] if T == 1 else self.ws
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
-            if self.fuse_norm:
+            att = self.buf_att[r0:r1]
+            scattered = (T > 1 and self.cos is None and self.fuse_norm and
+                         qkv_scatter_norm(h_in, L.w_qkv, a, self.buf_q, kc, vc, pos, B, T, self.H, self.Hkv,
+                                          self.hd))
+            if scattered:
+                pass  # prefill (no RoPE): c_attn wrote q head-major and K / V straight into the caches
+            elif self.fuse_norm:
                 qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[r0:r1], std_buf=a, ones=self.ones, q8=q8,
                                   s8=s8)
             else:
                 T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
                 qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[r0:r1])
-            att = self.buf_att[r0:r1]
-            if T == 1:  # decode: split/RoPE/cache write fused into the attention launch
+            if scattered:
+                T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
+            elif T == 1:  # decode: split/RoPE/cache write fused into the attention launch
                 T_.attn_decode_qkv(qkv, kc, vc, att, B, self.H, self.Hkv, self.hd, pos, ws, self.splits,
                                    self.cos, self.sin)
             elif self.cos is None:  # no RoPE (GPT-2): attention reads the c_attn output directly

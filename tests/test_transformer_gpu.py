@@ -788,3 +788,39 @@ def test_linear_norm_prefill_fold_vs_normalised_copy(M, N, K, rms, act):
     torch.cuda.synchronize()
     assert _rel(outs[True], y) < 1.5e-2, _rel(outs[True], y)
     assert _rel(outs[False], y) < 1.5e-2
+
+
+@pytest.mark.parametrize("B,T,H,Hkv,hd,pos0,S", [(4, 256, 12, 12, 64, 0, 300), (2, 200, 8, 2, 64, 30, 240),
+                                                 (3, 100, 4, 4, 128, 7, 400), (2, 160, 12, 12, 64, 100, 200)])
+def test_qkv_scatter_prefill(B, T, H, Hkv, hd, pos0, S):
+    """Prefill c_attn with the QKV scatter epilogue (q head-major, K/V straight
+    into the caches at pos[b] + t, rows past S dropped) == the qkv-row GEMM +
+    qkv_split, bit for bit, with the folded LayerNorm."""
+    from distributed_neural_networks_amd.ops import gemm as G
+    from distributed_neural_networks_amd.ops import transformer_ops as T_
+    torch.manual_seed(12)
+    d = 256
+    N = (H + 2 * Hkv) * hd
+    x = (torch.randn(B * T, d, device=DEV) * 2 + 0.5).bfloat16()
+    w = torch.randn(N, d, device=DEV) * 0.05
+    f = G.fold_norm(w, 1.0 + 0.1 * torch.randn(d, device=DEV), 0.1 * torch.randn(d, device=DEV),
+                    torch.randn(N, device=DEV) * 0.02, False, 1e-5, DEV)
+    std = torch.empty(B * T, d, device=DEV, dtype=torch.bfloat16)
+    ones = torch.ones(d, device=DEV)
+    pos = torch.full((B,), pos0, device=DEV, dtype=torch.int32)
+    kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(B * H * T * hd, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q)
+    assert G.qkv_scatter_norm(x, f, std, q, kc, vc, pos, B, T, H, Hkv, hd)
+    G.set_gemm_tile(256)  # the scatter runs on the 256^2 kernel: same tile order -> same bits
+    try:
+        qkv = G.linear_norm(x, f, std_buf=std, ones=ones)
+    finally:
+        G.set_gemm_tile(0)
+    T_.qkv_split(qkv, q2, kc2, vc2, B, T, H, Hkv, hd, pos)
+    torch.cuda.synchronize()
+    keep = pos0 + torch.arange(T, device=DEV) < S  # qkv_split skips every head of a row past the cache
+    assert torch.equal(q.view(B, H, T, hd)[:, :, keep], q2.view(B, H, T, hd)[:, :, keep])
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
