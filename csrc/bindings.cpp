@@ -60,6 +60,11 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_bf16_qkv_scatter(CP(A), lda, CP(W), ldw, CFP(bias), CFP(rowstat), CFP(colsum), P(q), P(kc), P(vc),
                                      CIP(pos), B, T, H, Hkv, hd, S, K, ST(st));
   });
+  m.def("gemm_fp8_qkv_scatter", [](u64 A8, u64 sa, u64 W8, u64 sw, u64 bias, u64 q, u64 kc, u64 vc, u64 pos, int B,
+                                   int T, int H, int Hkv, int hd, int S, int Kb, u64 st) {
+    return dnn_gemm_fp8_qkv_scatter(CP(A8), CFP(sa), CP(W8), CFP(sw), CFP(bias), P(q), P(kc), P(vc), CIP(pos), B, T, H,
+                                    Hkv, hd, S, Kb, ST(st));
+  });
   m.def("gemm_set_res_prefetch", [](int on) { return dnn_gemm_set_res_prefetch(on); });
   m.def("gemm_set_skinny_max_m", [](int m) { return dnn_gemm_set_skinny_max_m(m); });
   m.def("gemm_fp8_set_tile", [](int tile) { return dnn_gemm_fp8_set_tile(tile); });

@@ -14,6 +14,9 @@ int dnn_gemm_set_tile(int tile);
 int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, int ldw, const float* bias, const float* rowstat,
                               const float* colsum, void* q, void* kc, void* vc, const int* pos, int B, int T, int H,
                               int Hkv, int hd, int S, int K, hipStream_t st);
+int dnn_gemm_fp8_qkv_scatter(const void* A8, const float* sa, const void* W8, const float* sw, const float* bias,
+                             void* q, void* kc, void* vc, const int* pos, int B, int T, int H, int Hkv, int hd, int S,
+                             int Kb, hipStream_t st);
 int dnn_gemm_set_res_prefetch(int on);
 int dnn_gemm_set_skinny_max_m(int m);
 int dnn_gemm_fp8_set_tile(int tile);

@@ -257,6 +257,25 @@ __device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c) 
   return (isk ? sc.k : sc.v) + (((size_t)b * sc.Hkv + cc / sc.hd) * sc.S + p) * sc.hd + cc % sc.hd;
 }
 
+// One widened 16-B store per lane (as epi_pair_bf16) of a whole 32-column pair
+// to its head-major / cache destination (bias added first, no activation).
+__device__ __forceinline__ void epi_pair_scatter(f32x4 a0, f32x4 a1, int m, int nb, int M,
+                                                 const float* __restrict__ bias, int lane, const QkvScatter& sc) {
+  const int q = lane >> 4;
+  if (bias != nullptr) {
+    a0 += *reinterpret_cast<const f32x4*>(bias + nb + q * 4);
+    a1 += *reinterpret_cast<const f32x4*>(bias + nb + 16 + q * 4);
+  }
+  const uint32_t x0 = pack2bf(a0[0], a0[1]), x1 = pack2bf(a0[2], a0[3]);
+  const uint32_t y0 = pack2bf(a1[0], a1[1]), y1 = pack2bf(a1[2], a1[3]);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+  if (m < M) {
+    bf16_t* d = qkv_dest(sc, m, nb + ((q & 1) << 4) + ((q >> 1) << 3));
+    if (d != nullptr) *reinterpret_cast<uint4*>(d) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  }
+}
+
 template <int ACT, bool OUT_F32, bool SCATTER = false>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
@@ -425,22 +444,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
         } else if (SCATTER) {
           // widened 16-B stores as in epi_pair_bf16, to the head-major / cache
           // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
-          // residual, N % 256 == 0, hd % 8 == 0 -> every pair is whole)
-          f32x4 a0 = acc[mq][nq][i][0], a1 = acc[mq][nq][i][1];
-          const int q = lane >> 4;
-          if (bias != nullptr) {
-            a0 += *reinterpret_cast<const f32x4*>(bias + nb + q * 4);
-            a1 += *reinterpret_cast<const f32x4*>(bias + nb + 16 + q * 4);
-          }
-          const uint32_t x0 = pack2bf(a0[0], a0[1]), x1 = pack2bf(a0[2], a0[3]);
-          const uint32_t y0 = pack2bf(a1[0], a1[1]), y1 = pack2bf(a1[2], a1[3]);
-          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-          if (m < M) {
-            const int c = nb + ((q & 1) << 4) + ((q >> 1) << 3);
-            bf16_t* d = qkv_dest(scat, m, c);
-            if (d != nullptr) *reinterpret_cast<uint4*>(d) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-          }
+          // residual, N % 32 == 0, hd % 8 == 0 -> a 32-column pair is whole or
+          // past N, wave-uniformly)
+          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, bias, lane, scat);
         } else if (!OUT_F32 && pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
                              bias, R, ldr, lane);
@@ -488,11 +494,11 @@ __device__ __forceinline__ void bg_mfma_f8(f32x4 (&acc)[MI][NJ], const bf16x8 (&
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int ACT>
+template <int ACT, bool SCATTER = false>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     const uint8_t* __restrict__ A8, const float* __restrict__ sa, const uint8_t* __restrict__ W8,
     const float* __restrict__ sw, bf16_t* __restrict__ C, int ldc, const float* __restrict__ bias,
-    const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb) {
+    const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb, QkvScatter scat = {}) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
@@ -610,7 +616,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
           }
           v[j] = acc[mq][nq][i][j] * (cs * rs);
         }
-        if (ACT == ACT_SILU_MUL) {
+        if (SCATTER) {
+          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb, M, bias, lane, scat);
+        } else if (ACT == ACT_SILU_MUL) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) epi_silu_t4<false>(v[j], m, (nb + j * 16) / 2, M, N / 2, C, ldc, vec, lane);
         } else if (rpre) {
@@ -754,12 +762,27 @@ extern "C" int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, 
                                          hipStream_t st) {
   const int M = B * T, N = (H + 2 * Hkv) * hd;
   if (K % 64 != 0 || M <= 0 || hd % 8 != 0 || (colsum != nullptr && rowstat == nullptr)) return -1;
-  if (N % 256 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
-  const int tiles = ((M + BG_M - 1) / BG_M) * (N / BG_N);
+  if (N % 32 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
+  const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
   QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, hd, S};
   hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(tiles), dim3(512), 0, st, (const bf16_t*)A,
                      lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, N, K, 0,
                      reinterpret_cast<const float2*>(rowstat), colsum, sc);
+  return (int)hipGetLastError();
+}
+
+// fp8 (W8A8) c_attn with the QKV scatter epilogue: A8 / sa the per-token
+// e4m3 activations (layernorm_q8), W8 / sw the e4m3 weight, Kb its row bytes.
+extern "C" int dnn_gemm_fp8_qkv_scatter(const void* A8, const float* sa, const void* W8, const float* sw,
+                                        const float* bias, void* q, void* kc, void* vc, const int* pos, int B, int T,
+                                        int H, int Hkv, int hd, int S, int Kb, hipStream_t st) {
+  const int M = B * T, N = (H + 2 * Hkv) * hd;
+  if (Kb % 128 != 0 || M <= 0 || hd % 8 != 0 || sa == nullptr || sw == nullptr) return -1;
+  if (N % 32 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
+  const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, hd, S};
+  hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A8, sa,
+                     (const uint8_t*)W8, sw, (bf16_t*)q, hd, bias, (const bf16_t*)nullptr, 0, M, N, Kb, sc);
   return (int)hipGetLastError();
 }
 

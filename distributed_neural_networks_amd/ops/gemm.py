@@ -205,22 +205,37 @@ QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)
 
 
 def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q: torch.Tensor, kc: torch.Tensor,
-                     vc: torch.Tensor, pos: torch.Tensor, B: int, T: int, H: int, Hkv: int, hd: int) -> bool:
+                     vc: torch.Tensor, pos: torch.Tensor, B: int, T: int, H: int, Hkv: int, hd: int,
+                     ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
+                     s8: Optional[torch.Tensor] = None) -> bool:
     """Prefill c_attn (folded pre-norm, no RoPE) with the QKV scatter epilogue
     (gemm_bf16.hip ``dnn_gemm_bf16_qkv_scatter``): q lands in ``q`` as (B, H, T,
     hd) and K / V straight in the bf16 caches at rows ``pos[b] + t``, so the head-
     major flash prefill follows without a qkv_split or an in-kernel cache copy.
-    Returns False (nothing launched) where it does not apply: fp8 weights or
+    fp8 weights (W8A8): the standardise + quantise pass (``ones`` / ``q8`` /
+    ``s8`` buffers, as ``linear_norm``) feeds the fp8 256^2 kernel's scatter
+    variant.  Returns False (nothing launched) where it does not apply: an fp8
     cache, decode-sized M, or a shape off the 256^2 tile path."""
     from .fp8 import Fp8Weight
-    if not (QKV_SCATTER and FOLD_NORM_PREFILL) or isinstance(f.w, Fp8Weight) or kc.dtype != torch.bfloat16:
+    w8 = isinstance(f.w, Fp8Weight)
+    if not (QKV_SCATTER and FOLD_NORM_PREFILL) or kc.dtype != torch.bfloat16:
         return False
     M, K = x.shape
     N = f.w.shape[0]
-    if M != B * T or N != (H + 2 * Hkv) * hd or skinny_rows(M, N) or x.stride(1) != 1:
+    if M != B * T or N != (H + 2 * Hkv) * hd or skinny_rows(M, N, w8) or x.stride(1) != 1:
         return False
     if not (kc.is_contiguous() and vc.is_contiguous()) or q.numel() < M * H * hd or pos.dtype != torch.int32:
         return False
+    if w8:
+        if ones is None or q8 is None or s8 is None or N % 32 or M < 256:
+            return False
+        from .transformer_ops import layernorm_q8
+        kp = f.w.q.shape[1]
+        layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+        check(lib().gemm_fp8_qkv_scatter(ptr(q8), ptr(s8), ptr(f.w.q), ptr(f.w.scale), ptr(f.bias), ptr(q), ptr(kc),
+                                         ptr(vc), ptr(pos), B, T, H, Hkv, hd, kc.shape[2], kp, stream_ptr()),
+              "gemm_fp8_qkv_scatter")
+        return True
     from .transformer_ops import row_stats
     st = std_buf.reshape(-1)[:4 * M].view(torch.float32).view(M, 2)
     row_stats(x, st, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))

@@ -287,7 +287,7 @@ class TransformerStage(StageCompute):
             att = self.buf_att[r0:r1]
             scattered = (T > 1 and self.cos is None and self.fuse_norm and
                          qkv_scatter_norm(h_in, L.w_qkv, a, self.buf_q, kc, vc, pos, B, T, self.H, self.Hkv,
-                                          self.hd))
+                                          self.hd, ones=self.ones, q8=q8, s8=s8))
             if scattered:
                 pass  # prefill (no RoPE): c_attn wrote q head-major and K / V straight into the caches
             elif self.fuse_norm:

@@ -791,11 +791,13 @@ def test_linear_norm_prefill_fold_vs_normalised_copy(M, N, K, rms, act):
 
 
 @pytest.mark.parametrize("B,T,H,Hkv,hd,pos0,S", [(4, 256, 12, 12, 64, 0, 300), (2, 200, 8, 2, 64, 30, 240),
-                                                 (3, 100, 4, 4, 128, 7, 400), (2, 160, 12, 12, 64, 100, 200)])
+                                                 (3, 100, 4, 4, 128, 7, 400), (2, 160, 12, 12, 64, 100, 200),
+                                                 (2, 192, 25, 25, 64, 0, 256)])
 def test_qkv_scatter_prefill(B, T, H, Hkv, hd, pos0, S):
     """Prefill c_attn with the QKV scatter epilogue (q head-major, K/V straight
     into the caches at pos[b] + t, rows past S dropped) == the qkv-row GEMM +
-    qkv_split, bit for bit, with the folded LayerNorm."""
+    qkv_split, bit for bit, with the folded LayerNorm; H = 25 (GPT-2 XL) has a
+    partial last column tile (N = 4800)."""
     from distributed_neural_networks_amd.ops import gemm as G
     from distributed_neural_networks_amd.ops import transformer_ops as T_
     torch.manual_seed(12)
@@ -823,4 +825,38 @@ def test_qkv_scatter_prefill(B, T, H, Hkv, hd, pos0, S):
     torch.cuda.synchronize()
     keep = pos0 + torch.arange(T, device=DEV) < S  # qkv_split skips every head of a row past the cache
     assert torch.equal(q.view(B, H, T, hd)[:, :, keep], q2.view(B, H, T, hd)[:, :, keep])
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
+def test_qkv_scatter_prefill_fp8():
+    """fp8 (W8A8) c_attn with the scatter epilogue == the fp8 qkv-row GEMM +
+    qkv_split, bit for bit (GPT-2 XL head layout, N = 4800)."""
+    from distributed_neural_networks_amd.ops import gemm as G
+    from distributed_neural_networks_amd.ops import transformer_ops as T_
+    from distributed_neural_networks_amd.ops.fp8 import kpad_of
+    torch.manual_seed(13)
+    B, T, H, hd, d, S = 2, 192, 25, 64, 256, 256
+    N = 3 * H * hd
+    x = (torch.randn(B * T, d, device=DEV) * 2 + 0.5).bfloat16()
+    f = G.fold_norm(torch.randn(N, d, device=DEV) * 0.05, 1.0 + 0.1 * torch.randn(d, device=DEV),
+                    0.1 * torch.randn(d, device=DEV), torch.randn(N, device=DEV) * 0.02, False, 1e-5, DEV, fp8=True)
+    std = torch.empty(B * T, d, device=DEV, dtype=torch.bfloat16)
+    ones = torch.ones(d, device=DEV)
+    q8 = torch.empty(B * T * kpad_of(d), device=DEV, dtype=torch.uint8)
+    s8 = torch.empty(B * T, device=DEV)
+    pos = torch.zeros(B, device=DEV, dtype=torch.int32)
+    kc, vc = torch.zeros(B, H, S, hd, device=DEV).bfloat16(), torch.zeros(B, H, S, hd, device=DEV).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(B * H * T * hd, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q)
+    assert G.qkv_scatter_norm(x, f, std, q, kc, vc, pos, B, T, H, H, hd, ones=ones, q8=q8, s8=s8)
+    from distributed_neural_networks_amd.ops.fp8 import set_fp8_tile
+    set_fp8_tile(256)
+    try:
+        qkv = G.linear_norm(x, f, std_buf=std, ones=ones, q8=q8, s8=s8)
+    finally:
+        set_fp8_tile(0)
+    T_.qkv_split(qkv, q2, kc2, vc2, B, T, H, H, hd, pos)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q2)
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
