@@ -242,19 +242,27 @@ struct QkvScatter {
   bf16_t* k;
   bf16_t* v;
   const int* pos;
-  int T, H, Hkv, hd, S;
+  int T, H, Hkv, hd_shift, S;  // head dim = 1 << hd_shift
+  float invT;                  // 1 / T (row -> sequence without an integer division)
 };
 
-// 8 consecutive output columns c..c+7 (one head) of row m -> destination.
+// 8 consecutive output columns c..c+7 (one head) of row m -> destination.  The
+// store count is 32 per lane and tile, so the index math avoids integer
+// division: b = m / T from the fp32 reciprocal with a one-step correction
+// (exact for m < 2^24), head / dim by shifts (hd a power of two).
 __device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c) {
-  const int b = m / sc.T, t = m - b * sc.T;
-  const int qw = sc.H * sc.hd, kw = sc.Hkv * sc.hd;
-  if (c < qw) return sc.q + (((size_t)b * sc.H + c / sc.hd) * sc.T + t) * sc.hd + c % sc.hd;
+  int b = (int)(((float)m + 0.5f) * sc.invT);
+  b -= b * sc.T > m ? 1 : 0;
+  b += (b + 1) * sc.T <= m ? 1 : 0;
+  const int t = m - b * sc.T;
+  const int hs = sc.hd_shift, hmask = (1 << hs) - 1;
+  const int qw = sc.H << hs, kw = sc.Hkv << hs;
+  if (c < qw) return sc.q + ((((size_t)b * sc.H + (c >> hs)) * sc.T + t) << hs) + (c & hmask);
   const int p = sc.pos[b] + t;
   if (p >= sc.S) return nullptr;  // past the cache capacity: dropped, as in qkv_split
   const bool isk = c < qw + kw;
   const int cc = isk ? c - qw : c - qw - kw;
-  return (isk ? sc.k : sc.v) + (((size_t)b * sc.Hkv + cc / sc.hd) * sc.S + p) * sc.hd + cc % sc.hd;
+  return (isk ? sc.k : sc.v) + ((((size_t)b * sc.Hkv + (cc >> hs)) * sc.S + p) << hs) + (cc & hmask);
 }
 
 // One widened 16-B store per lane (as epi_pair_bf16) of a whole 32-column pair
@@ -764,7 +772,8 @@ extern "C" int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, 
   if (K % 64 != 0 || M <= 0 || hd % 8 != 0 || (colsum != nullptr && rowstat == nullptr)) return -1;
   if (N % 32 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
   const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
-  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, hd, S};
+  if ((hd & (hd - 1)) != 0 || M >= (1 << 24)) return -3;
+  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, __builtin_ctz(hd), S, 1.0f / (float)T};
   hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(tiles), dim3(512), 0, st, (const bf16_t*)A,
                      lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, N, K, 0,
                      reinterpret_cast<const float2*>(rowstat), colsum, sc);
@@ -780,7 +789,8 @@ extern "C" int dnn_gemm_fp8_qkv_scatter(const void* A8, const float* sa, const v
   if (Kb % 128 != 0 || M <= 0 || hd % 8 != 0 || sa == nullptr || sw == nullptr) return -1;
   if (N % 32 != 0 || M < 256 || ((uintptr_t)bias & 15) != 0) return -3;
   const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
-  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, hd, S};
+  if ((hd & (hd - 1)) != 0 || M >= (1 << 24)) return -3;
+  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, __builtin_ctz(hd), S, 1.0f / (float)T};
   hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A8, sa,
                      (const uint8_t*)W8, sw, (bf16_t*)q, hd, bias, (const bf16_t*)nullptr, 0, M, N, Kb, sc);
   return (int)hipGetLastError();
