@@ -14,6 +14,7 @@
 #   prof_argmax      Llama-3 8B fp8 B=1 decode kernel gaps with the split argmax
 #   prof_llama_b32   Llama-3 8B bf16 B=32 decode kernel table + gaps, M=32 projection sweep
 #   scatter3         QKV scatter prefill: tests, in-process A/B, per-layer prefill sequence
+#   prof_kv8         GPT-2 B=64 decode with the e4m3 KV cache: kernel table + gaps
 #   tail_check       kernel + transformer + pipeline GPU tests, smoke, decode benches
 set -o pipefail
 export TMPDIR=/tmp
@@ -156,8 +157,17 @@ case_tail_check() {
   bash tools/gpu_decode_bench.sh
 }
 
+case_prof_kv8() {
+  # GPT-2 4-stage B=64 decode with the e4m3 KV cache: kernel table + gaps
+  G="bench/gpt_bench.py --steps 16 --warmup 2 --prefill_iters 1 --kv fp8"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kv8 -o run -- python3 $G > gpurun_out/prof_kv8.log 2>&1 &&
+  python3 tools/rocprof_summary.py gpurun_out/prof_kv8 > gpurun_out/kv8_kernels.md &&
+  python3 tools/rocprof_gaps.py gpurun_out/prof_kv8 > gpurun_out/kv8_gaps.md
+  rc=$?; rm -rf gpurun_out/prof_kv8; head -8 gpurun_out/kv8_gaps.md; return $rc
+}
+
 c=${1:-}
 if ! declare -F "case_$c" > /dev/null; then
-  echo "usage: $0 <case>; cases: argmax_ab decode_ab decode_check flash_check gemm_epi kv8 kv8_ab kv8g prof_argmax prof_llama_b32 scatter3 tail_check"; exit 2
+  echo "usage: $0 <case>; cases: argmax_ab decode_ab decode_check flash_check gemm_epi kv8 kv8_ab kv8g prof_argmax prof_llama_b32 scatter3 prof_kv8 tail_check"; exit 2
 fi
 "case_$c"
