@@ -672,7 +672,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   DEC_PROBE(10, 0);
   // first batch of value rows: requested now, in flight across the barrier and
-  // the softmax (they depend only on the key range)
+  // the softmax (they depend only on the key range).  Issuing it before the
+  // score loop instead measured slower on the e4m3 path (GPT-2 B=64 0.523 ->
+  // 0.531 ms, B=256 1.053 -> 1.108: 142 VGPRs, profiles/r2_kv8_v_early_ab.jsonl)
   bf16x8 vr0[DEC_U];
 #pragma unroll
   for (int u = 0; u < DEC_U; ++u) {
