@@ -807,6 +807,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   DEC_PROBE(7, 0);
 }
 
+// (Folding this pass into the attention kernel — the last-arriving split
+// combines, tickets behind an agent-scope release / acquire — measured 20 %
+// slower on Llama-3 8B B=32 decode, 4.49 -> 5.39 ms/step: every split pays the
+// release fence's L2 write-back.  profiles/r2_decode_fold_combine_ab.jsonl;
+// write-through sc1 stores + sc1 loads without the fences read stale partials.)
 __global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H, int Hkv,
                                       int HD, int NS) {
   const int bh = blockIdx.x;  // b*H + h
