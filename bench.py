@@ -4,26 +4,36 @@
 Metric/config from BASELINE.json (the reference's only measured headline:
 CIFAR-10 2-stage images/s; 3.40-4.15 k img/s on CPU over localhost gRPC,
 BASELINE.md).  Synthetic fp32 images, random-init weights of the reference
-architecture, computed at the reference's precision (fp32: every product as
-three bf16 MFMA terms, ops/cifar.py); ``--precision bf16`` is the reduced-
-precision variant and is reported as extra keys.  Every timed step runs the
-complete forward of both stages (conv stage + fc/softmax/argmax stage) on
-fresh launches; nothing is cached across steps.
+architecture.  Precision: the reference's fp32 contract, computed as **fp32
+(bf16x3 split emulation, ~2^-16 relative per product, fp32 accumulation)**:
+every product is three bf16 MFMA terms (ops/cifar.py); the line reports the
+measured max|dprob| against fp32 torch on 4096 images (outside the timed
+region).  ``--precision bf16`` is the reduced-precision variant (extra keys).
+Every timed step runs the complete forward of both stages (conv stage +
+fc/softmax/argmax stage) on fresh launches; nothing is cached across steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Placements:
+Placements (the stage cut is the reference's at every N: conv | fc1+fc2+softmax,
+``cifar_model_parts.py:29-58``, an fp32 16 KiB/img hop):
 * N = 1: both stages colocated on the GPU, one HIP graph per step; extra keys:
   the bf16 pipeline, the GPT-2 small 4-stage pipeline (decode / prefill
   tokens/s, p50 per-token latency; bench/gpt_bench.py) and BASELINE configs 4
   and 5 colocated (Llama-3 8B bf16 8-stage B=32, GPT-2 XL fp8 8-stage B=64).
-* N > 1 (one process per GPU, RCCL): ``linear`` (default) — the reference
-  topology, one stage per GPU, isend/irecv over the direct xGMI links; the
-  bottleneck stage is replicated (``parallel/partition.py::linear_plan``: n0
-  stage-0 GPUs feed n1 stage-1 GPUs, each sender on its own link), the K steps
-  stream as one fill/drain.  ``interleaved`` (opt-in) — every GPU hosts stage
-  0 of its pipeline and stage 1 of the others; the hop is an all-to-all.
+* N > 1 (one process per GPU, RCCL; ``--placement pp2``, the headline): one
+  pipeline stage per GPU — N/2 GPUs run stage 0, N/2 run stage 1.  The hop is
+  bipartite: each stage-0 GPU cuts every microbatch into N/2 row slices and
+  sends slice j to stage-1 GPU j, so a transfer uses N/2 direct xGMI links at
+  once (``parallel/links.py SplitLink``; at N = 2 it is the single pair).
+  The K steps stream as one fill/drain.  p50 latency = one image through stage
+  0 -> RCCL hop -> stage 1 -> prediction back to stage 0 over the back-edge
+  (the reference's request path, ``node.py:137-200``).  Extra keys: the
+  fc1-cut plan (``--placement fc1cut``: conv+fc1 | fc2, replicated stage 0,
+  receivers fill), and the GPT-2 4-stage, Llama-3 8B 8-stage and GPT-2 XL fp8
+  8-stage decode rings across min(N, stages) GPU groups with per-token p50.
+  ``--placement interleaved`` (opt-in): every GPU hosts stage 0 of its
+  pipeline and stage 1 of the others; the hop is an all-to-all.
 Scaling is weak: each stage-0 GPU sources ``--batch`` images per step.
 
 ``--model gpt2`` runs the GPT-2 4-stage token throughput bench instead
@@ -42,6 +52,7 @@ import torch
 
 BASELINE_IMG_S = 4150.0  # reference CIFAR-10 2-stage, best batch (255), CPU gRPC
 METRIC = "images/sec CIFAR-10 2-stage"
+DTYPE_LABEL = {"fp32": "fp32 (bf16x3 split emulation, ~2^-16 per product)", "bf16": "bf16"}
 
 
 def parse():
@@ -54,11 +65,11 @@ def parse():
                     help="linear N>1: stage-1 GPUs only serve received microbatches (no own images)")
     ap.add_argument("--fill_rows", type=int, default=-1, help="linear N>1: own images per round on a stage-1 GPU "
                                                                "(-1 = sized from timing, see receiver_fill_rows)")
-    ap.add_argument("--microbatches", type=int, default=2,
-                    help="microbatches per step on N>1 (2 x 32768 rows fill the fc1 GEMM's 256 tiles)")
-    ap.add_argument("--placement", default="linear", choices=["linear", "interleaved"],
-                    help="N>1: linear = the reference topology (one stage per GPU, RCCL send/recv); "
-                         "interleaved = opt-in all-to-all variant")
+    ap.add_argument("--microbatches", type=int, default=8,
+                    help="microbatches per step on N>1 (the hop of one overlaps the stage-0 compute of the next)")
+    ap.add_argument("--placement", default="pp2", choices=["pp2", "fc1cut", "interleaved"],
+                    help="N>1: pp2 = the reference topology and cut (one stage per GPU, RCCL send/recv, headline); "
+                         "fc1cut = conv+fc1 | fc2 with replicated stage 0; interleaved = all-to-all variant")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="compute precision of the headline (fp32 = the reference's)")
     ap.add_argument("--no_extra", action="store_true", help="skip the extra bf16 / GPT-2 keys")
@@ -71,7 +82,9 @@ def parse():
                     help="CUs left free of the persistent stage-0 kernel for the RCCL hop kernels to run "
                          "concurrently (-1 = auto: 0 on 1 GPU, 16 on N > 1)")
     ap.add_argument("--cut", default="auto", choices=["auto", "1", "2"],
-                    help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = cost model")
+                    help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = per placement")
+    ap.add_argument("--extra_budget_s", type=float, default=420.0,
+                    help="N>1: wall-clock budget of the extra keys (a hang only drops keys)")
     return ap.parse_args()
 
 
@@ -103,9 +116,10 @@ def pick_cut(args, info) -> int:
     from distributed_neural_networks_amd.parallel.partition import cifar_cut
     if args.cut != "auto":
         return int(args.cut)
-    if info.world == 1:
-        return 1  # colocated: no hop; keep the reference split
-    return cifar_cut(args.placement, info.world, precision=args.precision)
+    if info.world == 1 or args.placement == "pp2":
+        return 1  # the reference split (conv | fc)
+    return cifar_cut("linear" if args.placement == "fc1cut" else args.placement, info.world,
+                     precision=args.precision)
 
 
 def dsync(dev):
@@ -225,9 +239,91 @@ def bench_interleaved(args, info):
     return t1 - t0, mb * M, statistics.median(ts) * 1e3, f"pp2-interleaved-a2a-x{N}"
 
 
-def bench_linear(args, info):
-    """Linear 2-stage pipeline, one stage per GPU, RCCL isend/irecv over the
-    direct xGMI links (``parallel/partition.py::linear_plan``): n0 stage-0 GPUs
+def bench_pp2(args, info):
+    """BASELINE config 2 on N GPUs: the reference's 2-stage pipeline with its
+    cut (conv | fc1+fc2+softmax, ``cifar_model_parts.py:29-58``), one stage per
+    GPU.  Rank 2p runs stage 0 and rank 2p+1 stage 1 (pipeline p of N/2).
+    The fp32 boundary (16 KiB/img) crosses a bipartite hop: every stage-0 GPU
+    splits each microbatch into N/2 row slices, slice j to stage-1 GPU j,
+    each pair on its own direct xGMI link (``SplitLink``; N = 2: one pair).
+    No receiver fill: a stage-1 GPU runs only stage 1 on what it receives."""
+    from distributed_neural_networks_amd.parallel import comm
+    from distributed_neural_networks_amd.parallel.links import P2PLink, SplitLink
+    from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
+    dev, N, r = info.device, info.world, info.rank
+    if N % 2:
+        raise ValueError(f"the 2-stage pipeline needs an even GPU count, got {N}")
+    n = N // 2
+    stage = r % 2
+    s0, s1 = stages_for(dev, 1, args.precision)
+    M = max(1, args.microbatches)
+    mb = (args.batch // M) // n * n  # rows per microbatch, split evenly over the N/2 receivers
+    if mb < n:
+        raise ValueError(f"--batch {args.batch} / {M} microbatches is too small to split over {n} receivers")
+    g = torch.Generator(device=dev).manual_seed(1 + r)
+    back = comm.back_group()
+    if stage == 0:
+        xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
+        nxt = SplitLink([P2PLink(2 * j + 1, dev) for j in range(n)])
+
+        def stream(steps):
+            run_gpipe(s0, steps * M, mb, None, nxt, source=lambda i: xs[i % M], depth=2)
+    else:
+        prev = SplitLink([P2PLink(2 * a, dev) for a in range(n)])
+
+        def stream(steps):
+            run_gpipe(s1, steps * M, mb, prev, None, depth=2)
+
+    stream(args.warmup)
+    t0 = sync_time(info)
+    stream(args.steps)
+    t1 = sync_time(info)
+    p50 = pp2_latency(args, info, s0, s1, back)
+    return t1 - t0, n * mb * M / N, p50, f"pp2-rccl-{n}x{n}" + ("-bipartite" if n > 1 else "")
+
+
+def pp2_latency(args, info, s0, s1, back) -> float:
+    """p50 of one image through the pipeline as the reference serves a
+    request (``node.py:137-200``): rank 0 runs stage 0, the 16 KiB boundary
+    crosses to rank 1 over RCCL, rank 1 runs stage 1 and returns the
+    prediction to rank 0 (``return_to_node_id``) over the back-edge.  Timed
+    on rank 0 from the input on the device to the prediction back on it."""
+    from distributed_neural_networks_amd.parallel.links import P2PLink
+    dev, r = info.device, info.rank
+    iters = max(3, min(args.latency_iters, 200))
+    ts = []
+    sync_time(info)
+    if r == 0:
+        x = torch.randn((1, 3, 32, 32), device=dev)
+        y = torch.empty(s0.out_spec(1)[0], dtype=s0.out_spec(1)[1], device=dev)
+        pred = torch.empty((1,), dtype=torch.int32, device=dev)
+        fwd, ret = P2PLink(1, dev), P2PLink(1, dev, back)
+        for _ in range(iters):
+            dsync(dev)
+            a = time.perf_counter()
+            s0.forward(x, y)
+            w = fwd.isend(y)
+            ret.recv(pred)
+            w.wait()
+            dsync(dev)
+            ts.append(time.perf_counter() - a)
+    elif r == 1:
+        y = torch.empty(s1.in_spec(1)[0], dtype=s1.in_spec(1)[1], device=dev)
+        probs = torch.empty((1, 10), device=dev)
+        fwd, ret = P2PLink(0, dev), P2PLink(0, dev, back)
+        for _ in range(iters):
+            fwd.recv(y)
+            out = s1.forward(y, probs)
+            ret.send(out.pred)
+        dsync(dev)
+    sync_time(info)
+    return statistics.median(ts) * 1e3 if ts else float("nan")
+
+
+def bench_fc1cut(args, info):
+    """Extra key (not the headline): the 2-stage pipeline cut after fc1
+    (conv+fc1 | fc2+softmax, a 2 KiB/img hop), one stage per GPU, RCCL
+    isend/irecv over the direct xGMI links (``parallel/partition.py::linear_plan``): n0 stage-0 GPUs
     each source ``--batch`` images per step and stream them to one of n1
     stage-1 GPUs.  The K timed steps run as ONE stream of K x M microbatches
     (fill and drain once, not per step).  A stage-1 GPU spends ~2 % of a
@@ -240,12 +336,10 @@ def bench_linear(args, info):
     from distributed_neural_networks_amd.parallel.partition import linear_plan, linear_role
     from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     dev, N, r = info.device, info.world, info.rank
-    plan = linear_plan(N, args.precision)
-    if args.cut != "auto":
-        plan = dict(plan, cut=args._cut)
-    args._cut = plan["cut"]
+    plan = linear_plan(N, args.precision, cuts=(2,))
+    cut = plan["cut"]
     role = linear_role(r, plan)
-    s0, s1 = stages_for(dev, args._cut, args.precision)
+    s0, s1 = stages_for(dev, cut, args.precision)
     M = max(1, args.microbatches)
     mb = args.batch // M
     g = torch.Generator(device=dev).manual_seed(1 + r)
@@ -288,9 +382,8 @@ def bench_linear(args, info):
     import torch.distributed as dist
     dist.all_reduce(local)
     imgs_total_per_step = plan["n0"] * mb * M + float(local.item())
-    args._fill_rows = float(local.item())
-    par = f"pp2-linear-{plan['n0']}x{plan['n1']}" + ("+fill" if local.item() > 0 else "")
-    return t1 - t0, imgs_total_per_step / N, float("nan"), par
+    par = f"pp2-fc1cut-{plan['n0']}x{plan['n1']}" + ("+fill" if local.item() > 0 else "")
+    return t1 - t0, imgs_total_per_step / N, float(local.item()), par
 
 
 RECV_ITEM_OVERHEAD_S = 30e-6  # host wait + launch per received microbatch (assumed, not measured here)
@@ -401,6 +494,32 @@ def extra_keys(args, info):
     return out
 
 
+def precision_check(dev, precision: str, n_img: int = 4096) -> dict:
+    """max|dprob| and argmax agreement of the HIP pipeline (the benchmarked
+    stages and weights) against the fp32 torch model (TF32 off), on n_img
+    random images.  Outside every timed region."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    s0, s1 = stages_for(dev, 1, precision)
+    ref = NeuralNetwork().to(dev).eval()
+    ref.load_state_dict(ckpt.random_stage_state_dict("cifar10", 0, 3, True, True, 0))
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn((n_img, 3, 32, 32), device=dev, generator=g)
+    out = ColocatedPipeline([s0, s1], n_img)(x)
+    tf32 = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        with torch.no_grad():
+            p = ref(x)
+    finally:
+        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
+    dsync(dev)
+    return {"max_abs_dprob_vs_fp32_torch": float((out.probs - p).abs().max().item()),
+            "argmax_agreement_vs_fp32_torch": round(float((out.pred.long() == p.argmax(1)).float().mean().item()), 6),
+            "precision_check_images": n_img}
+
+
 def main():
     args = parse()
     if args.model != "cifar10":
@@ -409,21 +528,30 @@ def main():
         return gpt_bench.main(args)
     info = dist_setup(args.gpus, args.cpu)
     N = info.world
+    if N > 1:
+        from distributed_neural_networks_amd.parallel import comm
+        comm.back_group()  # collective: the back-edge communicator (latency path, decode rings)
     args._cut = pick_cut(args, info)
     spare = args.s0_spare_cus if args.s0_spare_cus >= 0 else (16 if N > 1 else 0)
+    if info.device.type != "cuda":
+        spare = 0
     if spare and info.device.type == "cuda":
         # the stage-0 kernel holds every VGPR of the CUs it runs on, so without
-        # spare CUs the all-to-all / isend kernels only start between stage-0
-        # launches and each hop is exposed; 16 of 256 CUs (2 per XCD) stay free
+        # spare CUs the RCCL send kernels only start between stage-0 launches
+        # and each hop is exposed; 16 of 256 CUs (2 per XCD) stay free
         from distributed_neural_networks_amd.ops import cifar as cops
         n_cu = torch.cuda.get_device_properties(info.device).multi_processor_count
         cops.set_stage0_grid(max(1, n_cu - spare))
+    fill = 0.0
     if N == 1:
         el, imgs_per_gpu, p50, par = bench_colocated(args, info)
     elif args.placement == "interleaved":
         el, imgs_per_gpu, p50, par = bench_interleaved(args, info)
+    elif args.placement == "fc1cut":
+        el, imgs_per_gpu, fill, par = bench_fc1cut(args, info)
+        p50 = float("nan")
     else:
-        el, imgs_per_gpu, p50, par = bench_linear(args, info)
+        el, imgs_per_gpu, p50, par = bench_pp2(args, info)
     el = max_over_ranks(info, el)
     total = imgs_per_gpu * N * args.steps
     value = total / el
@@ -431,29 +559,27 @@ def main():
     if N == 1 and not args.no_extra and info.device.type == "cuda":
         extra = extra_keys(args, info)
     hop_kib = 4 * (4 if args.precision == "fp32" else 2)
+    out = None
     if info.rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
-            "dtype": args.precision, "data": "synthetic (random fp32 images, random-init weights)",
+            "dtype": DTYPE_LABEL[args.precision], "data": "synthetic (random fp32 images, random-init weights)",
             "p50_latency_ms": None if p50 != p50 else round(p50, 4),
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
-                       "receiver_fill_images_per_step": getattr(args, "_fill_rows", 0),
+                       "receiver_fill_images_per_step": fill,
                        "stage0_spare_cus": spare,
                        "stage_cut": {1: f"conv|fc (reference split, {hop_kib} KiB/img hop)",
                                      2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},
         }
+        if info.device.type == "cuda" and args.precision == "fp32":
+            out.update(precision_check(info.device, args.precision))
         out.update(extra)
     if N > 1 and not args.no_extra:
-        # GPT-2 small 4-stage decode ring across the GPUs (BASELINE config 3 at
-        # N = 4: one stage per GPU, tokens back to stage 0 over RCCL).  Guarded:
-        # a failure or hang here only drops these keys, never the headline line.
-        g = guarded_multi_gpu_gpt(args, info, out if info.rank == 0 else None)
-        if info.rank == 0 and g:
-            out.update(g)
+        multi_gpu_extras(args, info, out)
     if info.rank == 0:
         print(json.dumps(out), flush=True)
     if N > 1:
@@ -462,46 +588,83 @@ def main():
     return 0
 
 
-def guarded_multi_gpu_gpt(args, info, line, limit_s: float = 150.0):
-    """Run bench/gpt_bench.py's decode ring on all ranks under a timer: on a
-    hang every rank exits 0 after ``limit_s`` (rank 0 first prints the CIFAR
-    line it already has), on an exception the keys are skipped."""
+# extra decode rings at N > 1: (key, GPU argv, schedule-test argv on gloo CPU, config label)
+RINGS = (
+    ("gpt2_4stage", ["--model", "gpt2", "--stages", "4", "--batch", "64", "--prompt", "512", "--dtype", "bf16",
+                     "--steps", "32", "--warmup", "4", "--prefill_iters", "3"],
+     ["--model", "gpt2-tiny", "--stages", "4"], "gpt2 (124M, random init), bf16"),
+    ("llama3_8b_8stage_b32", ["--model", "llama3-8b", "--stages", "8", "--batch", "32", "--prompt", "512",
+                              "--dtype", "bf16", "--steps", "16", "--warmup", "2", "--prefill_iters", "1"],
+     ["--model", "llama3-tiny", "--stages", "4"], "llama3-8b (random init), bf16"),
+    ("gpt2xl_fp8_8stage_b64", ["--model", "gpt2-xl", "--stages", "8", "--batch", "64", "--prompt", "512",
+                               "--dtype", "fp8", "--steps", "16", "--warmup", "2", "--prefill_iters", "1"],
+     ["--model", "gpt2-tiny", "--stages", "4", "--dtype", "fp8"],
+     "gpt2-xl (random init), fp8-e4m3 weights (W8A16 decode, W8A8 prefill), bf16 activations"),
+)
+
+
+def multi_gpu_extras(args, info, line):
+    """Extra keys at N > 1, on every rank, under one wall-clock budget: the
+    fc1-cut CIFAR plan, then the GPT-2 4-stage, Llama-3 8B 8-stage and GPT-2 XL
+    fp8 8-stage decode rings across min(N, stages) GPU groups (tokens back to
+    group 0 over RCCL) with per-token p50.  A failure drops that key; a hang
+    past the budget makes every rank exit 0 (rank 0 first prints the line it
+    has), so the headline is never lost."""
+    import copy
     import threading
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
     import gpt_bench
+    from distributed_neural_networks_amd.parallel import comm
+    current = ["fc1cut"]
 
     def bail():
         if line is not None:
-            line["gpt2_4stage_error"] = f"decode ring exceeded {limit_s:.0f} s; skipped"
+            line["extras_error"] = f"{current[0]} exceeded the {args.extra_budget_s:.0f} s extras budget; skipped"
             print(json.dumps(line), flush=True)
         os._exit(0)
-    timer = threading.Timer(limit_s, bail)
+    timer = threading.Timer(args.extra_budget_s, bail)
     timer.daemon = True
     timer.start()
+    cuda = info.device.type == "cuda"
     try:
-        if info.device.type == "cuda":
-            ga = gpt_bench.parse(["--gpus", str(info.world), "--steps", "32", "--warmup", "4", "--batch", "64",
-                                  "--prompt", "512", "--stages", "4", "--dtype", "bf16", "--prefill_iters", "3"])
-        else:  # schedule-test mode (gloo): the same ring on the tiny model
-            ga = gpt_bench.parse(["--gpus", str(info.world), "--cpu", "--model", "gpt2-tiny", "--steps", "3",
-                                  "--warmup", "1", "--batch", "2", "--prompt", "8", "--stages", "4",
-                                  "--prefill_iters", "1"])
-        g = gpt_bench.run(ga)
-    except Exception as e:  # noqa: BLE001
-        g = None
-        if line is not None:
-            line["gpt2_4stage_error"] = f"{type(e).__name__}: {e}"[:200]
+        try:
+            a = copy.copy(args)
+            a.latency_iters = 3
+            el, imgs, fill, par = bench_fc1cut(a, info)
+            el = max_over_ranks(info, el)
+            if line is not None:
+                line["fc1cut_images_per_s"] = round(imgs * info.world * args.steps / el, 1)
+                line["fc1cut_ms_per_step"] = round(el / args.steps * 1e3, 4)
+                line["fc1cut_config"] = {"parallelism": par, "receiver_fill_images_per_step": fill,
+                                         "stage_cut": "conv+fc1|fc2 (2 KiB/img fp32 hop)"}
+        except Exception as e:  # noqa: BLE001
+            if line is not None:
+                line["fc1cut_error"] = f"{type(e).__name__}: {e}"[:200]
+        for key, argv_gpu, argv_cpu, label in RINGS:
+            current[0] = key
+            if cuda:
+                torch.cuda.empty_cache()
+            comm.barrier(info)
+            argv = ["--gpus", str(info.world)] + (argv_gpu if cuda else
+                                                  ["--cpu", "--steps", "3", "--warmup", "1", "--batch", "2",
+                                                   "--prompt", "8", "--prefill_iters", "1"] + argv_cpu)
+            try:
+                g = gpt_bench.run(gpt_bench.parse(argv), shutdown=False)
+            except Exception as e:  # noqa: BLE001
+                if line is not None:
+                    line[key + "_error"] = f"{type(e).__name__}: {e}"[:200]
+                continue
+            if line is not None and g is not None:
+                c = g["config"]
+                line[key + "_decode_tok_s"] = g["value"]
+                line[key + "_decode_ms_per_step"] = g["ms_per_step"]
+                line[key + "_prefill_tok_s"] = g["prefill_tokens_per_s"]
+                line[key + "_p50_token_ms"] = g["decode_p50_token_latency_ms"]
+                line[key + "_config"] = dict(
+                    c, model=label if cuda else f"{c['model']} (gloo schedule test)",
+                    placement=f"{c['gpu_groups']} GPU groups x {c['replicas']} replicas, decode ring over RCCL")
     finally:
         timer.cancel()
-    if g is None:
-        return {}
-    return {"gpt2_4stage_decode_tok_s": g["value"], "gpt2_4stage_decode_ms_per_step": g["ms_per_step"],
-            "gpt2_4stage_prefill_tok_s": g["prefill_tokens_per_s"],
-            "gpt2_4stage_config": dict(g["config"], dtype="bf16" if info.device.type == "cuda" else "fp32",
-                                       model=("gpt2 (124M, random init)" if info.device.type == "cuda"
-                                              else "gpt2-tiny (schedule test)"),
-                                       placement=f"{g['config']['gpu_groups']} GPU groups x "
-                                                 f"{g['config']['replicas']} replicas, decode ring over RCCL")}
 
 
 if __name__ == "__main__":

@@ -28,6 +28,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+LAT_ROUNDS = 16
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -74,8 +77,10 @@ def main(args=None):
     return 0
 
 
-def run(args=None):
-    """Run the bench on every rank; rank 0 returns the JSON record (others None)."""
+def run(args=None, shutdown: bool = True):
+    """Run the bench on every rank; rank 0 returns the JSON record (others None).
+    ``shutdown=False`` keeps the process group for a caller that runs more
+    benches in the same processes (bench.py's multi-GPU extras)."""
     if args is None or not hasattr(args, "prompt"):
         base = args
         args = parse([])
@@ -111,7 +116,7 @@ def run(args=None):
     M = args.microbatches or groups
     B = args.batch
     T0 = args.prompt
-    total_steps = args.warmup + args.steps + 16 + 2  # + the 16 latency steps + graph-capture slack
+    total_steps = args.warmup + args.steps + LAT_ROUNDS + 2  # + the latency rounds + graph-capture slack
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
     kv = getattr(args, "kv", "bf16")
@@ -119,8 +124,9 @@ def run(args=None):
     base = rep * groups
     prev = P2PLink(base + grp - 1, dev) if grp > 0 else None
     nxt = P2PLink(base + grp + 1, dev) if 0 <= grp < groups - 1 else None
-    back_to0 = P2PLink(base + 0, dev) if (grp == groups - 1 and groups > 1) else None
-    back_from = P2PLink(base + groups - 1, dev) if (grp == 0 and groups > 1) else None
+    bg = comm.back_group() if N > 1 else None  # the token back-edge on its own communicator / stream
+    back_to0 = P2PLink(base + 0, dev, bg) if (grp == groups - 1 and groups > 1) else None
+    back_from = P2PLink(base + groups - 1, dev, bg) if (grp == 0 and groups > 1) else None
     d = model_info(model).cfg.n_embd
     V = model_info(model).cfg.vocab_size
 
@@ -171,13 +177,28 @@ def run(args=None):
     t1 = sync()
     decode_s = (t1 - t0) / args.steps
     dec_tok = B * M * replicas
-    # per-token latency of one synced decode round (single group only)
+    # per-token latency.  One group: a synced decode round.  Several groups:
+    # microbatch 0 circulates alone (ring.decode_round([0]) on every rank), so
+    # a round is one trip stage 0 -> ... -> last -> back-edge -> stage 0; the
+    # time between group 0's consecutive post-round syncs is one token.
     lat = []
     if groups == 1 and ring is not None:
-        for _ in range(16):
+        for _ in range(LAT_ROUNDS):
             ta = sync()
             ring.decode_round()
             lat.append(sync() - ta)
+    elif ring is not None:
+        comm.barrier(info)
+        stamps = []
+        for _ in range(LAT_ROUNDS):
+            ring.decode_round([0])
+            if grp == 0:
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                stamps.append(time.perf_counter())
+        ring.drain()
+        lat = [b - a for a, b in zip(stamps, stamps[1:])]
+    sync()
     graphs = ring is not None and bool(ring.graphs)
 
     def mx(v):
@@ -208,7 +229,7 @@ def run(args=None):
                        "decode_lanes": len(ring.lanes) if ring is not None and ring.lanes else 1,
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},
         }
-    if N > 1:
+    if N > 1 and shutdown:
         comm.shutdown()
     return out if r == 0 else None
 

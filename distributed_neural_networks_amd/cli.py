@@ -118,6 +118,30 @@ def stage_ranges(ctx: NodeContext) -> List[Tuple[int, int]]:
     return resolve_ranges(info.num_layers, pipe.num_parts, given)
 
 
+def rccl_device_index(ctx: NodeContext, n_dev: int) -> int:
+    """GPU of this rank on the rccl transport: the node's ``device`` (default
+    its ``part_index``) plus ``replica * num_parts``.  Every (node, replica)
+    of the config must map to its own visible GPU; RCCL would otherwise fail
+    late with a duplicate-GPU error, so overlaps are a ConfigError up front."""
+    pipe = ctx.pipeline
+
+    def idx(node, rep):
+        base = node.device if node.device is not None else node.part_index
+        return base + rep * ctx.num_parts
+    owner = {}
+    for rep in range(pipe.replicas):
+        for n in pipe.stages:
+            i = idx(n, rep)
+            if i >= n_dev:
+                raise ConfigError(f"ERROR: node '{n.id}' replica {rep} needs GPU {i}, "
+                                  f"but only {n_dev} are visible")
+            if i in owner:
+                raise ConfigError(f"ERROR: node '{n.id}' replica {rep} and node '{owner[i][0]}' replica "
+                                  f"{owner[i][1]} both map to GPU {i} (rccl needs one GPU per rank)")
+            owner[i] = (n.id, rep)
+    return idx(ctx.node, ctx.replica)
+
+
 def pick_device(ctx: NodeContext, override: Optional[str]) -> torch.device:
     if override:
         return torch.device(override)
@@ -125,8 +149,7 @@ def pick_device(ctx: NodeContext, override: Optional[str]) -> torch.device:
         idx = ctx.node.device if ctx.node.device is not None else 0
         if ctx.pipeline.transport == "rccl":
             # one GPU per rank; replica r of a stage pinned to device d runs on d + r * num_parts
-            base = ctx.node.device if ctx.node.device is not None else ctx.part_index
-            idx = (base + ctx.replica * ctx.num_parts) % torch.cuda.device_count()
+            idx = rccl_device_index(ctx, torch.cuda.device_count())
         return torch.device("cuda", idx)
     return torch.device("cpu")
 
@@ -369,13 +392,27 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     s0 = pipe.stage(0)
     info = comm.init(backend, rank=ctx.rank, world=ctx.world, master_addr=s0.host,
                      timeout_s=pipe.comm_timeout_s, master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
-    ranges = stage_ranges(ctx)
-    stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device, None, args)
+    comm.back_group()  # collective: the back-edge's own communicator
     fam = model_info(pipe.model).family
+    # the watchdog runs from here on, so a rank that fails while loading its
+    # weights takes the pipeline down within heartbeat_timeout_s instead of
+    # leaving its peers in the first barrier for comm_timeout_s
     wd = Watchdog(info.rank, info.world, peer_timeout_s=pipe.heartbeat_timeout_s,
                   stall_timeout_s=pipe.stall_timeout_s, tag=f"[{nid}]")
-    comm.barrier(info)
     wd.start()
+    try:
+        ranges = stage_ranges(ctx)
+        stage, _ = build_stage(ctx, ctx.part_index, ranges, info.device, None, args)
+    except FileNotFoundError:
+        log(f"[{nid}] ERROR: Weights file not found at '{ctx.model_weights}'")
+        wd.abort("weights file not found")
+        return 1
+    except Exception as e:  # noqa: BLE001
+        log(f"[{nid}] ERROR loading model/weights: {e}")
+        traceback.print_exc()
+        wd.abort(f"stage build failed: {type(e).__name__}: {e}")
+        return 1  # only reached when exit_fn does not exit (tests)
+    comm.barrier(info)
     rep = f", replica {ctx.replica}" if pipe.replicas > 1 else ""
     log(f"[{nid}] rank {info.rank}/{info.world} ready on {info.device} (backend {backend}{rep})")
     rc = 0
@@ -400,6 +437,7 @@ def run_dist(ctx: NodeContext, args, device) -> int:
 
 
 def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
+    from .parallel import comm
     from .parallel.links import P2PLink
     from .runtime.scheduler import ForwardLinks, ForwardPipeline
     nid, pipe, dev = ctx.node_id, ctx.pipeline, info.device
@@ -408,10 +446,11 @@ def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
     ret_part = ret.part_index if ret is not None else 0
     last = r == S - 1
     peer = ctx.peer  # ranks of this replica's stages
+    bg = comm.back_group()
     links = ForwardLinks(prev=P2PLink(peer(r - 1), dev) if r > 0 else None,
                          nxt=P2PLink(peer(r + 1), dev) if not last else None,
-                         ret_out=P2PLink(peer(ret_part), dev) if (last and ret_part != r) else None,
-                         ret_in=P2PLink(peer(S - 1), dev) if (r == ret_part and not last) else None)
+                         ret_out=P2PLink(peer(ret_part), dev, bg) if (last and ret_part != r) else None,
+                         ret_in=P2PLink(peer(S - 1), dev, bg) if (r == ret_part and not last) else None)
     rep = f" (replica {ctx.replica})" if pipe.replicas > 1 else ""
 
     def on_result(role, tag, preds):
@@ -472,10 +511,10 @@ def main(argv=None) -> int:
         ctx = load_node(args.config, nid, _replica_arg(args))
         log(f"Loaded configuration from {args.config}")
         check_config_capacity(ctx, args)
+        device = pick_device(ctx, args.device)
     except ConfigError as e:
         print(str(e), flush=True)
         return 1
-    device = pick_device(ctx, args.device)
     log(banner(ctx, str(device)))
     try:
         transport = ctx.pipeline.transport

@@ -78,6 +78,26 @@ def init(backend: Optional[str] = None, rank: Optional[int] = None, world: Optio
     return DistInfo(rank=rank, world=world, local_rank=local_rank, backend=backend, device=device)
 
 
+_BACK_GROUP = None
+
+
+def back_group():
+    """A second communicator over every rank, for the pipeline back-edge
+    (predictions / sampled tokens from the last stage to the return stage).
+
+    On RCCL all P2P between one rank pair shares one communicator and one
+    stream, so a return rank that posts its receives ahead of its forward
+    sends to the same peer (the 2-stage CIFAR stream, the 2-group decode ring)
+    would queue them in front of the data they wait for.  On its own
+    communicator the back-edge has its own stream and never orders against
+    forward traffic.  Collective: every rank calls it (once, right after
+    ``init``); later calls return the cached group.  None on one rank."""
+    global _BACK_GROUP
+    if _BACK_GROUP is None and dist.is_initialized() and dist.get_world_size() > 1:
+        _BACK_GROUP = dist.new_group(list(range(dist.get_world_size())))
+    return _BACK_GROUP
+
+
 def barrier(info: DistInfo) -> None:
     if info.world > 1 and dist.is_initialized():
         if info.backend == "nccl":
@@ -87,5 +107,7 @@ def barrier(info: DistInfo) -> None:
 
 
 def shutdown() -> None:
+    global _BACK_GROUP
+    _BACK_GROUP = None
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -11,8 +11,9 @@ CPU.  On RCCL:
   work already queued on the compute stream when the op is posted, and
   ``Work.wait()`` orders the compute stream after the transfer without
   blocking the host — so a stage never waits on the host for a hop;
-* ``exchange`` posts a middle stage's send-to-next and receive-from-prev as one
-  group (one ``ncclGroupStart/End``, one fused launch) instead of two.
+* ``exchange`` posts a middle stage's send-to-next and receive-from-prev
+  together; each peer pair keeps its own communicator and stream, so the two
+  transfers run concurrently (see ``exchange`` for why no op is batched).
 
 Every link counts messages and bytes (``stats``) for the METRICS line.
 Message framing for open-ended streams (the CLI): a 4 x int64 header
@@ -79,25 +80,23 @@ class P2PLink:
 
 
 def exchange(sends: Sequence[Tuple[P2PLink, torch.Tensor]], recvs: Sequence[Tuple[P2PLink, torch.Tensor]]):
-    """Post several sends and receives as one group; returns their works
-    (sends first).  RCCL fuses a group into one launch and never deadlocks on
-    the order of the ops inside it."""
-    ops = []
-    for link, t in sends:
-        link._count_send(t)
-        ops.append(dist.P2POp(dist.isend, t, link.peer, group=link.group))
-    for link, t in recvs:
-        link._count_recv(t)
-        ops.append(dist.P2POp(dist.irecv, t, link.peer, group=link.group))
-    if not ops:
-        return None
-    return GroupWork(dist.batch_isend_irecv(ops))
+    """Post several sends and receives together; returns one ``GroupWork``.
+
+    Each op is a plain ``isend``/``irecv``, deliberately not
+    ``batch_isend_irecv``: ProcessGroupNCCL runs a single P2P op on the
+    two-rank communicator of its peer pair, but a *batched* op on the
+    group-wide communicator, and a send posted on one is never matched by a
+    receive posted on the other.  Every link in this package therefore uses
+    single ops only, so every peer pair has one communicator and one stream
+    (different pairs — a middle stage's prev and next, a fan-out's receivers
+    — progress concurrently on their own streams)."""
+    works = [link.isend(t) for link, t in sends] + [link.irecv(t) for link, t in recvs]
+    return GroupWork(works) if works else None
 
 
 class GroupWork:
-    """The works of one ``exchange`` group (RCCL returns one coalesced work,
-    gloo one per op); ``wait`` is idempotent so every slot that depends on the
-    group can wait on it."""
+    """The works of one ``exchange`` group; ``wait`` is idempotent so every
+    slot that depends on the group can wait on it."""
 
     def __init__(self, works):
         self.works = list(works)
@@ -106,6 +105,48 @@ class GroupWork:
         while self.works:
             self.works.pop(0).wait()
         return True
+
+
+class SplitLink:
+    """One logical stage hop over several peers: a tensor sent through it is
+    cut into ``len(links)`` equal row slices, slice j going to ``links[j]``; a
+    receive assembles its rows from the same slices of every peer, slice a
+    from ``links[a]``.  Used for the bipartite hop of the multi-GPU CIFAR
+    pipeline (every stage-0 GPU feeds every stage-1 GPU, each pair over its
+    own xGMI link), so one microbatch's transfer is spread over all links
+    instead of queueing on one.  Same ``isend``/``irecv`` contract as
+    ``P2PLink``; rows must divide evenly."""
+
+    def __init__(self, links: Sequence[P2PLink]):
+        if not links:
+            raise ValueError("SplitLink needs at least one link")
+        self.links = list(links)
+        self.peer = self.links[0].peer if len(self.links) == 1 else tuple(l.peer for l in self.links)
+
+    def _slices(self, t: torch.Tensor):
+        n = len(self.links)
+        if t.shape[0] % n:
+            raise ValueError(f"SplitLink: {t.shape[0]} rows do not split into {n} equal slices")
+        if not t.is_contiguous():
+            raise ValueError("SplitLink needs a contiguous tensor")
+        sl = t.shape[0] // n
+        return [t[j * sl:(j + 1) * sl] for j in range(n)]
+
+    def isend(self, t: torch.Tensor):
+        return GroupWork([l.isend(p) for l, p in zip(self.links, self._slices(t))])
+
+    def irecv(self, out: torch.Tensor):
+        return GroupWork([l.irecv(p) for l, p in zip(self.links, self._slices(out))])
+
+    def send(self, t: torch.Tensor) -> None:
+        self.isend(t).wait()
+
+    def recv(self, out: torch.Tensor) -> torch.Tensor:
+        self.irecv(out).wait()
+        return out
+
+    def stats(self) -> dict:
+        return {"peers": [l.stats() for l in self.links]}
 
 
 def wait(work: Optional[object]) -> None:

@@ -194,55 +194,64 @@ class ForwardPipeline:
         self.depth = depth
         self.progress = progress or _noop
         self.on_result = on_result or (lambda role, tag, preds: None)
-        self._slots: Dict[int, List[torch.Tensor]] = {}
+        self._slots: Dict[tuple, List[torch.Tensor]] = {}
 
     def _send_header(self, kind, a=0, b=0, tag=0):
         if self.links.nxt is not None:
             self.links.nxt.send_header(kind, a, b, tag)
 
     def _stream(self, mbs: int, M: int, tag: int, source=None) -> Optional[torch.Tensor]:
-        """This rank's part of one request; returns the last stage's predictions."""
+        """This rank's part of one request; returns the last stage's predictions.
+
+        The last stage gives every microbatch its own back-edge slot and waits
+        on those sends only after the stream: a send that completes only once
+        the return rank has posted its receive (gloo) can never stall the
+        forward stream, whatever ``M`` is."""
         local: Dict[int, torch.Tensor] = {}
-        work: List[object] = [None, None]
+        work: List[object] = []
         sink = None
         if self.is_last:
-            slots = self._slots.get(mbs)
+            slots = self._slots.get((mbs, M))
             if slots is None:
-                slots = self._slots[mbs] = [torch.empty((mbs,), dtype=torch.int32, device=self.stage.device)
-                                            for _ in range(2)]
+                slots = self._slots[(mbs, M)] = [torch.empty((mbs,), dtype=torch.int32, device=self.stage.device)
+                                                 for _ in range(M)]
 
             def sink(i, y: StageOutput):
                 local[i] = y.pred.clone()
                 if self.links.ret_out is not None:
-                    k = i % 2
-                    if work[k] is not None:
-                        work[k].wait()
-                    slots[k].copy_(y.pred)
-                    work[k] = self.links.ret_out.isend(slots[k])
+                    slots[i].copy_(y.pred)
+                    work.append(self.links.ret_out.isend(slots[i]))
         run_gpipe(self.stage, M, mbs, self.links.prev, self.links.nxt, source=source, sink=sink,
                   depth=self.depth, progress=self.progress)
         for w in work:
-            if w is not None:
-                w.wait()
+            w.wait()
         if not self.is_last:
             return None
         preds = torch.cat([local[i] for i in range(M)]).cpu()
         self.on_result("last", tag, preds)
         return preds
 
-    def _collect(self, mbs: int, M: int) -> torch.Tensor:
+    def _post_collect(self, mbs: int, M: int):
+        """Return rank: post the receives of all M prediction slots before
+        streaming (the back-edge travels on its own communicator,
+        ``comm.back_group``, so these never queue ahead of forward traffic)."""
         dev = self.stage.device
         preds = [torch.empty((mbs,), dtype=torch.int32, device=dev) for _ in range(M)]
-        for p in preds:
-            self.links.ret_in.recv(p)
-            self.progress()
-        return torch.cat(preds).cpu()
+        return preds, [self.links.ret_in.irecv(p) for p in preds]
 
     def _request(self, mbs: int, M: int, tag: int, source=None) -> Optional[torch.Tensor]:
+        pending = self._post_collect(mbs, M) if (self.is_ret and self.links.ret_in is not None) else None
         own = self._stream(mbs, M, tag, source)
         if not self.is_ret:
             return None
-        preds = own if self.links.ret_in is None else self._collect(mbs, M)
+        if pending is None:
+            preds = own
+        else:
+            bufs, works = pending
+            for w in works:
+                w.wait()
+                self.progress()
+            preds = torch.cat(bufs).cpu()
         self.on_result("return", tag, preds)
         return preds
 
@@ -328,6 +337,8 @@ class DecodeRing:
         else:
             self.out = [torch.empty((B, self.d), dtype=out_dt, device=dev) for _ in range(M)]
         self.swork: List[object] = [None] * M
+        # group 0 (G > 1): a sampled token of microbatch m is on its way back
+        self.pending = [False] * M
         self.sorder = SlotOrder("ring_out", M)
         self.toks: List[List[torch.Tensor]] = [[] for _ in range(M)]
         self.use_graphs = use_graphs and dev.type == "cuda"
@@ -381,8 +392,11 @@ class DecodeRing:
     def _recv_token(self, m: int):
         """Group 0: the token sampled for microbatch m arrives over the back-edge."""
         if self.G > 1:
+            if not self.pending[m]:
+                return  # already received (drain) — the ring resumes from cur[m]
             with trace.span("token_recv", "p2p", mb=m):
                 self.links.back_in.recv(self.cur[m].view(self.B))
+            self.pending[m] = False
         if self.record:
             self.toks[m].append(self.cur[m].view(self.B).clone())
 
@@ -437,6 +451,8 @@ class DecodeRing:
         for w in pf_work:
             if w is not None:
                 w.wait()
+        if self.first and self.G > 1:
+            self.pending = [True] * self.M  # every prompt's first token comes back over the back-edge
         self.steps_done = 0
 
     # -- decode -------------------------------------------------------------------
@@ -455,12 +471,15 @@ class DecodeRing:
                 self.cur[m].copy_(cur)
         torch.cuda.synchronize(self.dev)
 
-    def decode_round(self) -> None:
-        """Every microbatch advances one token on this rank's stages."""
-        if self.lanes:
+    def decode_round(self, mbs: Optional[Sequence[int]] = None) -> None:
+        """Every microbatch (or those in ``mbs``; every rank must pass the same
+        list) advances one token on this rank's stages.  ``mbs=[0]`` after a
+        ``drain`` lets one microbatch circulate alone: a round is then exactly
+        one trip around the ring (per-token latency)."""
+        if self.lanes and mbs is None:
             return self._decode_round_lanes()
         G = self.G
-        for m in range(self.M):
+        for m in (range(self.M) if mbs is None else mbs):
             if self.first and G > 1:
                 self._recv_token(m)
             elif not self.first:
@@ -473,6 +492,8 @@ class DecodeRing:
                 else:
                     self._decode_body(m)
             self._send(m)
+            if self.first and G > 1:
+                self.pending[m] = True
             if self.first and G == 1 and self.record:
                 self.toks[m].append(self.cur[m].view(self.B).clone())
             self.progress()
@@ -505,7 +526,7 @@ class DecodeRing:
         rank waits for its outstanding sends."""
         if self.first and self.G > 1:
             for m in range(self.M):
-                self._recv_token(m)
+                self._recv_token(m)  # only the tokens still in flight
                 self.progress()
         for m in range(self.M):
             if self.swork[m] is not None:

@@ -91,6 +91,10 @@ class TransformerStage(StageCompute):
         self.rms = self.family == "llama3"
         self.max_batch, self.max_seq = max_batch, max_seq
         self.max_tokens = max_tokens or max_batch * max_seq
+        # activation rows: a prefill chunk uses rows [0, B*T), a decode step of
+        # microbatch m rows [m*B, (m+1)*B) (they follow the KV rows), so the
+        # buffers hold max(max_tokens, max_batch) rows
+        self.buf_rows = max(self.max_tokens, max_batch)
         self.ones = torch.ones((self.d,), dtype=torch.float32, device=dev)
         self.layers: List[LayerW] = [self._pack_layer(sd, j) for j in range(end - start + 1)]
         if first:
@@ -130,7 +134,7 @@ class TransformerStage(StageCompute):
         kvt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
         self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=kvt, device=dev)
         self.vc = torch.zeros_like(self.kc)
-        self._alloc(self.max_tokens)
+        self._alloc(self.buf_rows)
 
     # ------------------------------------------------------------------ weights
     def _attach_decode_copies(self):
@@ -268,6 +272,8 @@ class TransformerStage(StageCompute):
         # uses the rows from 0 and stays one-at-a-time
         r0 = b0 if T == 1 else 0
         r1 = r0 + ntok
+        if r1 > self.buf_h.shape[0]:
+            raise ValueError(f"stage buffers hold {self.buf_h.shape[0]} rows, step needs rows [{r0}, {r1})")
         if self.first:
             if x.dtype != torch.int32 or tuple(x.shape) != (B, T):
                 raise ValueError(f"first stage expects int32 ids (B,T)=({B},{T}), got {x.dtype} {tuple(x.shape)}")
@@ -279,7 +285,7 @@ class TransformerStage(StageCompute):
         a = self.buf_a[r0:r1]
         q8, s8 = self.q8, self.s8
         if self.fp8 and T == 1:
-            q8 = self.q8[r0 * (self.q8.numel() // self.max_tokens):]
+            q8 = self.q8[r0 * (self.q8.numel() // self.buf_rows):]
             s8 = self.s8[r0:]
         ws = self.ws[r0 * self.ws_per_seq:] if T == 1 else self.ws
         for li, L in enumerate(self.layers):

@@ -126,3 +126,26 @@ def test_kv_cache_dtype():
         resolve_node(c, "node1")
     c.update(model="llama3-8b", kv_cache_dtype="fp8")
     assert resolve_node(c, "node1").pipeline.kv_cache_dtype == "fp8"
+
+
+def test_rccl_device_mapping_validated(tmp_path):
+    """rccl: every (node, replica) needs its own visible GPU; overlaps and
+    out-of-range indices are config errors before any communicator exists."""
+    import json
+    from distributed_neural_networks_amd.cli import rccl_device_index
+    from distributed_neural_networks_amd.config import ConfigError, load_node
+
+    def cfg(nodes, **extra):
+        c = {"nodes": nodes, "model_weights": "x.pth", "num_parts": len(nodes), "transport": "rccl"}
+        c.update(extra)
+        p = tmp_path / "c.json"
+        p.write_text(json.dumps(c))
+        return str(p)
+    two = [{"id": "a", "address": "127.0.0.1:1", "part_index": 0},
+           {"id": "b", "address": "127.0.0.1:2", "part_index": 1}]
+    assert rccl_device_index(load_node(cfg(two, replicas=2), "b", replica=1), 4) == 3
+    with pytest.raises(ConfigError, match="only 2 are visible"):
+        rccl_device_index(load_node(cfg(two, replicas=2), "a"), 2)
+    pinned = [dict(two[0], device=1), dict(two[1], device=1)]
+    with pytest.raises(ConfigError, match="both map to GPU 1"):
+        rccl_device_index(load_node(cfg(pinned), "a"), 8)

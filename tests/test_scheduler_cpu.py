@@ -271,3 +271,55 @@ def test_cli_chunked_prefill_gloo(tmp_path):
     from distributed_neural_networks_amd.runtime.generate import make_prompts
     prompts = make_prompts(load_node(str(cfg), "node1").pipeline, None).tolist()
     assert toks == _golden_tokens("gpt2-tiny", 4, 8, prompts, 4)
+
+
+def _ring_resume_worker(rank, world, port, q):
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import default_ranges
+    from distributed_neural_networks_amd.parallel import comm
+    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.stages import TorchStage
+    torch.set_num_threads(1)
+    info = comm.init("gloo", rank=rank, world=world, master_addr="127.0.0.1", master_port=port)
+    bg = comm.back_group()
+    a, b = default_ranges("gpt2-tiny", world)[rank]
+    first, last = rank == 0, rank == world - 1
+    st = TorchStage("gpt2-tiny", ckpt.random_stage_state_dict("gpt2-tiny", a, b, first, last, 5), a, b, first, last)
+    links = RingLinks(prev=P2PLink(rank - 1, info.device) if rank > 0 else None,
+                      nxt=P2PLink(rank + 1, info.device) if not last else None,
+                      back_out=P2PLink(0, info.device, bg) if last else None,
+                      back_in=P2PLink(world - 1, info.device, bg) if first else None)
+    ring = DecodeRing([st], links, world, 2, 2)
+    g = torch.Generator().manual_seed(9)
+    prompts = [torch.randint(0, 512, (2, 5), generator=g) for _ in range(2)] if first else None
+    ring.prefill(prompts, 5)
+    for _ in range(2):
+        ring.decode_round()
+    ring.drain()
+    for _ in range(3):  # microbatch 0 alone (the per-token latency rounds of bench/gpt_bench.py)
+        ring.decode_round([0])
+    ring.drain()
+    if first:
+        q.put(([p.tolist() for p in prompts], [torch.stack(t, 1).tolist() for t in ring.toks]))
+    comm.barrier(info)
+    comm.shutdown()
+
+
+def test_decode_ring_single_microbatch_resume_gloo():
+    """After a drain, ``decode_round([0])`` lets microbatch 0 circulate alone
+    through 3 gloo ranks (tokens over the back-edge communicator); its tokens
+    continue the golden greedy sequence and microbatch 1 stays where it was."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_ring_resume_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    prompts, toks = q.get(timeout=180)
+    for p in ps:
+        p.join(60)
+    assert len(toks[0][0]) == 6 and len(toks[1][0]) == 3
+    assert toks[0] == _golden_tokens("gpt2-tiny", 4, 5, prompts[0], 6)
+    assert toks[1] == _golden_tokens("gpt2-tiny", 4, 5, prompts[1], 3)
