@@ -248,7 +248,7 @@ def bench_pp2(args, info):
     each pair on its own direct xGMI link (``SplitLink``; N = 2: one pair).
     No receiver fill: a stage-1 GPU runs only stage 1 on what it receives."""
     from distributed_neural_networks_amd.parallel import comm
-    from distributed_neural_networks_amd.parallel.links import P2PLink, SplitLink
+    from distributed_neural_networks_amd.parallel.links import SplitLink, make_link
     from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     dev, N, r = info.device, info.world, info.rank
     if N % 2:
@@ -264,12 +264,12 @@ def bench_pp2(args, info):
     back = comm.back_group()
     if stage == 0:
         xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
-        nxt = SplitLink([P2PLink(2 * j + 1, dev) for j in range(n)])
+        nxt = SplitLink([make_link(2 * j + 1, dev) for j in range(n)])
 
         def stream(steps):
             run_gpipe(s0, steps * M, mb, None, nxt, source=lambda i: xs[i % M], depth=2)
     else:
-        prev = SplitLink([P2PLink(2 * a, dev) for a in range(n)])
+        prev = SplitLink([make_link(2 * a, dev) for a in range(n)])
 
         def stream(steps):
             run_gpipe(s1, steps * M, mb, prev, None, depth=2)
@@ -288,7 +288,7 @@ def pp2_latency(args, info, s0, s1, back) -> float:
     crosses to rank 1 over RCCL, rank 1 runs stage 1 and returns the
     prediction to rank 0 (``return_to_node_id``) over the back-edge.  Timed
     on rank 0 from the input on the device to the prediction back on it."""
-    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.parallel.links import make_link
     dev, r = info.device, info.rank
     iters = max(3, min(args.latency_iters, 200))
     ts = []
@@ -297,7 +297,7 @@ def pp2_latency(args, info, s0, s1, back) -> float:
         x = torch.randn((1, 3, 32, 32), device=dev)
         y = torch.empty(s0.out_spec(1)[0], dtype=s0.out_spec(1)[1], device=dev)
         pred = torch.empty((1,), dtype=torch.int32, device=dev)
-        fwd, ret = P2PLink(1, dev), P2PLink(1, dev, back)
+        fwd, ret = make_link(1, dev), make_link(1, dev, back)
         for _ in range(iters):
             dsync(dev)
             a = time.perf_counter()
@@ -310,7 +310,7 @@ def pp2_latency(args, info, s0, s1, back) -> float:
     elif r == 1:
         y = torch.empty(s1.in_spec(1)[0], dtype=s1.in_spec(1)[1], device=dev)
         probs = torch.empty((1, 10), device=dev)
-        fwd, ret = P2PLink(0, dev), P2PLink(0, dev, back)
+        fwd, ret = make_link(0, dev), make_link(0, dev, back)
         for _ in range(iters):
             fwd.recv(y)
             out = s1.forward(y, probs)
@@ -332,7 +332,7 @@ def bench_fc1cut(args, info):
     microbatches: stage 0 1.245 ms, stage 1 0.023 ms -> 27648 / 24576 / 19456
     own rows per round at N = 2 / 4 / 8, i.e. 1.84 / 3.75 / 7.59 GPUs of work
     instead of 1 / 3 / 7)."""
-    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.parallel.links import make_link
     from distributed_neural_networks_amd.parallel.partition import linear_plan, linear_role
     from distributed_neural_networks_amd.runtime.scheduler import run_gpipe
     dev, N, r = info.device, info.world, info.rank
@@ -345,12 +345,12 @@ def bench_fc1cut(args, info):
     g = torch.Generator(device=dev).manual_seed(1 + r)
     if role["stage"] == 0:
         xs = [torch.randn((mb, 3, 32, 32), device=dev, generator=g) for _ in range(M)]
-        nxt = P2PLink(role["send_to"], dev)
+        nxt = make_link(role["send_to"], dev)
 
         def stream(steps):
             run_gpipe(s0, steps * M, mb, None, nxt, source=lambda i: xs[i % M], depth=2)
     else:
-        prevs = [P2PLink(p, dev) for p in role["recv_from"]]
+        prevs = [make_link(p, dev) for p in role["recv_from"]]
         # receiver fill: a stage-1 GPU is mostly idle (fc2 is ~1 % of the model),
         # so between rounds of received microbatches it runs its own images
         # through both stages, sized so a round still fits in a sender's period

@@ -45,13 +45,15 @@ def parse(argv=None):
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--prefill_iters", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
-    ap.add_argument("--kv", default="bf16", choices=["bf16", "fp8"], help="KV cache dtype (fp8: OCP e4m3, GPT-2 family)")
+    ap.add_argument("--kv", default="bf16", choices=["bf16", "fp8"], help="KV cache dtype (fp8: OCP e4m3)")
+    ap.add_argument("--kv_scale", default="calibrated", choices=["calibrated", "unit"],
+                    help="fp8 KV cache scale: per-layer, from the first prefill's amax, or unit")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     return ap.parse_args(argv)
 
 
-def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16"):
+def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16", kv_scale="calibrated"):
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import TorchStage
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
@@ -65,7 +67,7 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf1
             continue
         sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0, device=dev)
         out.append(TransformerStage(model, sd, a, b, s == 0, s == S - 1, dev, max_batch=max_batch,
-                                    max_seq=max_seq, fp8=fp8, kv_dtype=kv))
+                                    max_seq=max_seq, fp8=fp8, kv_dtype=kv, kv_scale=kv_scale))
         del sd
     return out
 
@@ -90,7 +92,7 @@ def run(args=None, shutdown: bool = True):
                     setattr(args, k, getattr(base, k))
     from distributed_neural_networks_amd.models import default_ranges, gpt2, model_info
     from distributed_neural_networks_amd.parallel import comm
-    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.parallel.links import make_link
 
     N = args.gpus
     if getattr(args, "cpu", False):
@@ -120,13 +122,14 @@ def run(args=None, shutdown: bool = True):
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
     kv = getattr(args, "kv", "bf16")
-    stages = _build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv) if stage_ids else []
+    stages = (_build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv, getattr(args, "kv_scale", "calibrated"))
+              if stage_ids else [])
     base = rep * groups
-    prev = P2PLink(base + grp - 1, dev) if grp > 0 else None
-    nxt = P2PLink(base + grp + 1, dev) if 0 <= grp < groups - 1 else None
+    prev = make_link(base + grp - 1, dev) if grp > 0 else None
+    nxt = make_link(base + grp + 1, dev) if 0 <= grp < groups - 1 else None
     bg = comm.back_group() if N > 1 else None  # the token back-edge on its own communicator / stream
-    back_to0 = P2PLink(base + 0, dev, bg) if (grp == groups - 1 and groups > 1) else None
-    back_from = P2PLink(base + groups - 1, dev, bg) if (grp == 0 and groups > 1) else None
+    back_to0 = make_link(base + 0, dev, bg) if (grp == groups - 1 and groups > 1) else None
+    back_from = make_link(base + groups - 1, dev, bg) if (grp == 0 and groups > 1) else None
     d = model_info(model).cfg.n_embd
     V = model_info(model).cfg.vocab_size
 

@@ -6,7 +6,7 @@ K/V stream, for both score paths (suffix ``m``: MFMA key tiles,
 the GQA default; none: DPP row reductions).  Shapes are the decode benches' (Llama-3 8B B=1 / B=32, GPT-2
 B=64 / B=256).
 
-    python bench/attn_decode_bench.py [--iters 50] [--splits 1,2,4,8,16]
+    python bench/probes/attn_decode_bench.py [--iters 50] [--splits 1,2,4,8,16]
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 SHAPES = {  # name: (B, H, Hkv, hd, S capacity, pos, rope)
     "llama_b1": (1, 32, 8, 128, 151, 140, True),

@@ -7,8 +7,8 @@ the s_memrealtime (100 MHz) deltas between the kernel's phase marks:
     0 entry  1 lens read  2 q (+RoPE) packed  3 scores in LDS  4 softmax
     5 P.V done  6 reduction scratch written  7 output written
 
-    python bench/attn_probe.py --build        # CPU host
-    python bench/attn_probe.py                # GPU box
+    python bench/probes/attn_probe.py --build        # CPU host
+    python bench/probes/attn_probe.py                # GPU box
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SO = os.path.join(ROOT, "bench", "_attn_probe.so")
 sys.path.insert(0, ROOT)
 

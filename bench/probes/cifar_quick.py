@@ -8,7 +8,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from distributed_neural_networks_amd.models.cifar import NeuralNetwork
 from distributed_neural_networks_amd.ops import cifar as cops

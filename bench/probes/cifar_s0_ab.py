@@ -2,7 +2,7 @@
 differences cancel): stage-0 time at B=65536 for each setting, plus the
 max |difference| of the two outputs (must be 0).  One JSON line.
 
-    python bench/cifar_s0_ab.py [--switch wide_store] [--batch 65536]
+    python bench/probes/cifar_s0_ab.py [--switch wide_store] [--batch 65536]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from distributed_neural_networks_amd.models.cifar import NeuralNetwork  # noqa: E402
 from distributed_neural_networks_amd.ops import _lib, cifar as cops  # noqa: E402

@@ -2,7 +2,7 @@
 differences cancel): bench/gpt_bench.py runs alternately with each variant's
 setting applied before the stages are built and captured.
 
-    python bench/decode_ab.py --switch skinny_max_m --values 32,64 [gpt_bench args...]
+    python bench/probes/decode_ab.py --switch skinny_max_m --values 32,64 [gpt_bench args...]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bench"))
 

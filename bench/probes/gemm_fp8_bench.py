@@ -3,7 +3,7 @@
 256^2 4-phase kernels, GEMM only (operands pre-quantised), vs torch bf16
 matmul on the same shape for scale.  One JSON line per shape.
 
-    python bench/gemm_fp8_bench.py [--shapes 32768x4800x1600,...] [--iters 30]
+    python bench/probes/gemm_fp8_bench.py [--shapes 32768x4800x1600,...] [--iters 30]
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 DEFAULT = "32768x4800x1600,32768x1600x1600,32768x6400x1600,32768x1600x6400,16384x6144x4096,16384x28672x4096,16384x4096x14336,8192x8192x8192"
 

@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 SHAPES = [(32768, 2304, 768, "norm"), (32768, 3072, 768, "gelu+norm"), (32768, 2304, 768, "none"),

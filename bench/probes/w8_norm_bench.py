@@ -4,7 +4,7 @@ plain, with the fused RMSNorm statistics (norm=1), and the SwiGLU gate|up
 (act=3), each with and without the fragment-order weight copy.  Device time
 per launch as HIP-graph replays, weight copies rotated past the 256 MB MALL.
 
-    python bench/w8_norm_bench.py [--iters 20] [--m 1]
+    python bench/probes/w8_norm_bench.py [--iters 20] [--m 1]
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 CASES = [  # name, N, K, act, norm
     ("qkv", 6144, 4096, 0, 1), ("qkv_nonorm", 6144, 4096, 0, 0), ("o", 4096, 4096, 0, 0),

@@ -18,6 +18,11 @@ Transports (config ``transport``):
   With config ``replicas`` = R the pipeline runs as R data-parallel copies
   (``--replica r``, rank = r * num_parts + part_index, one GPU each): copy r
   serves requests r, r+R, ... (CIFAR) or its own batch of sequences (GPT/Llama).
+* ``gloo_gpu``: the ``gloo`` schedules with the stages on the GPU (node
+  ``device``, default 0; several ranks may share one device, which RCCL
+  refuses) and every hop staged through pinned host memory with RCCL-like
+  stream ordering (``parallel/links.py HostStagedLink``): the multi-process
+  schedules run with device compute and HIP graphs on a 1-GPU box.
 """
 from __future__ import annotations
 
@@ -200,7 +205,7 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
             st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
                                     max_batch=n_seq, max_seq=n_pos, max_tokens=ntok,
                                     temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed,
-                                    kv_dtype=pipe.kv_cache_dtype)
+                                    kv_dtype=pipe.kv_cache_dtype, kv_scale=pipe.kv_cache_scale)
     else:
         st = TorchStage(pipe.model, sd, a, b, first, last, device,
                         sampling=(pipe.temperature, pipe.top_k, pipe.seed))
@@ -384,14 +389,23 @@ def run_dist(ctx: NodeContext, args, device) -> int:
     nid = ctx.node_id
     pipe = ctx.pipeline
     backend = "nccl" if pipe.transport == "rccl" else "gloo"
+    if pipe.transport == "gloo_gpu" and device.type != "cuda":
+        log(f"[{nid}] ERROR: transport 'gloo_gpu' needs a GPU")
+        return 1
     if backend == "nccl" and device.type != "cuda":
         log(f"[{nid}] ERROR: transport 'rccl' needs a GPU")
         return 1
-    if backend == "gloo":
+    if pipe.transport == "gloo":
         device = torch.device("cpu")
     s0 = pipe.stage(0)
     info = comm.init(backend, rank=ctx.rank, world=ctx.world, master_addr=s0.host,
                      timeout_s=pipe.comm_timeout_s, master_port=s0.port + comm.PORT_OFFSET, device_index=device.index)
+    if pipe.transport == "gloo_gpu":
+        # gloo process group, stages on the GPU: hops stage through pinned host
+        # memory (parallel/links.py HostStagedLink); ranks may share a device
+        import dataclasses
+        torch.cuda.set_device(device)
+        info = dataclasses.replace(info, device=device)
     comm.back_group()  # collective: the back-edge's own communicator
     fam = model_info(pipe.model).family
     # the watchdog runs from here on, so a rank that fails while loading its
@@ -438,7 +452,7 @@ def run_dist(ctx: NodeContext, args, device) -> int:
 
 def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
     from .parallel import comm
-    from .parallel.links import P2PLink
+    from .parallel.links import make_link
     from .runtime.scheduler import ForwardLinks, ForwardPipeline
     nid, pipe, dev = ctx.node_id, ctx.pipeline, info.device
     r, S = ctx.part_index, ctx.num_parts
@@ -447,10 +461,10 @@ def _cifar_stream(ctx: NodeContext, args, stage, info, wd) -> int:
     last = r == S - 1
     peer = ctx.peer  # ranks of this replica's stages
     bg = comm.back_group()
-    links = ForwardLinks(prev=P2PLink(peer(r - 1), dev) if r > 0 else None,
-                         nxt=P2PLink(peer(r + 1), dev) if not last else None,
-                         ret_out=P2PLink(peer(ret_part), dev, bg) if (last and ret_part != r) else None,
-                         ret_in=P2PLink(peer(S - 1), dev, bg) if (r == ret_part and not last) else None)
+    links = ForwardLinks(prev=make_link(peer(r - 1), dev) if r > 0 else None,
+                         nxt=make_link(peer(r + 1), dev) if not last else None,
+                         ret_out=make_link(peer(ret_part), dev, bg) if (last and ret_part != r) else None,
+                         ret_in=make_link(peer(S - 1), dev, bg) if (r == ret_part and not last) else None)
     rep = f" (replica {ctx.replica})" if pipe.replicas > 1 else ""
 
     def on_result(role, tag, preds):
@@ -520,7 +534,7 @@ def main(argv=None) -> int:
         transport = ctx.pipeline.transport
         if transport == "colocated":
             return run_colocated(ctx, args, device)
-        if transport in ("rccl", "gloo"):
+        if transport in ("rccl", "gloo", "gloo_gpu"):
             return run_dist(ctx, args, device)
         ranges = stage_ranges(ctx)
         stage, _ = build_stage(ctx, ctx.part_index, ranges, device, None, args)

@@ -12,7 +12,8 @@ Behavioural contract (reference ``node.py:222-290``, ``config.json:1-18``):
 * Additive optional fields (absent in the reference file, so it still loads):
   top level ``model``, ``dtype``, ``transport``, ``micro_batch_size``,
   ``num_microbatches``, ``seq_len``, ``decode_steps``, ``prompt_len``, ``temperature``, ``top_k``,
-  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``, ``replicas``; per node
+  ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``, ``replicas``,
+  ``kv_cache_dtype``, ``kv_cache_scale``; per node
   ``layers: [start, end]`` (inclusive, as in
   ``partitions/gpt_model_parts.py:12``) and ``device``.
 
@@ -24,7 +25,8 @@ import json
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 
-TRANSPORTS = ("grpc", "colocated", "rccl", "gloo")
+TRANSPORTS = ("grpc", "colocated", "rccl", "gloo", "gloo_gpu")
+DIST_TRANSPORTS = ("rccl", "gloo", "gloo_gpu")  # one rank per stage (and replica)
 MODELS = ("cifar10", "gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl", "gpt2-tiny",
           "llama3-8b", "llama3-tiny")
 
@@ -61,6 +63,7 @@ class PipelineConfig:
     model: str = "cifar10"
     dtype: Optional[str] = None
     kv_cache_dtype: str = "bf16"              # "fp8": OCP e4m3 KV cache (half the decode K/V bytes)
+    kv_cache_scale: str = "calibrated"        # fp8 cache: per-layer scale from the first prefill's amax, or "unit"
     transport: str = "grpc"
     micro_batch_size: int = 1
     num_microbatches: int = 1
@@ -193,23 +196,27 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     reps = cfg.get("replicas", 1)
     if not isinstance(reps, int) or isinstance(reps, bool) or reps < 1:
         raise ConfigError(f"ERROR: 'replicas' must be a positive integer, got {reps!r}")
-    if reps > 1 and transport not in ("rccl", "gloo"):
-        raise ConfigError(f"ERROR: 'replicas' > 1 needs transport 'rccl' or 'gloo' (one rank per stage and replica), "
+    if reps > 1 and transport not in DIST_TRANSPORTS:
+        raise ConfigError(f"ERROR: 'replicas' > 1 needs transport 'rccl', 'gloo' or 'gloo_gpu' (one rank per stage and replica), "
                           f"got '{transport}'")
     kvd = cfg.get("kv_cache_dtype", "bf16")
     if kvd not in ("bf16", "fp8"):
         raise ConfigError(f"ERROR: 'kv_cache_dtype' must be 'bf16' or 'fp8', got {kvd!r}")
+    kvs = cfg.get("kv_cache_scale", "calibrated")
+    if kvs not in ("calibrated", "unit"):
+        raise ConfigError(f"ERROR: 'kv_cache_scale' must be 'calibrated' or 'unit', got {kvs!r}")
     t = cfg.get("temperature", 0.0)
     if not isinstance(t, (int, float)) or t < 0:
         raise ConfigError(f"ERROR: 'temperature' must be >= 0, got {t!r}")
     ret = cfg.get("return_to_node_id")
-    if ret is not None and transport in ("rccl", "gloo"):
+    if ret is not None and transport in DIST_TRANSPORTS:
         rn = next((n for n in nodes if n.id == ret), None)
         if rn is None:
             raise ConfigError(f"ERROR: return_to_node_id '{ret}' is not a node of this config")
     return PipelineConfig(
         nodes=nodes, model_weights=str(weights), num_parts=num_parts,
         return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"), kv_cache_dtype=kvd,
+        kv_cache_scale=kvs,
         transport=transport, micro_batch_size=int(cfg.get("micro_batch_size", 1)),
         num_microbatches=int(cfg.get("num_microbatches", 1)), seq_len=int(cfg.get("seq_len", 64)),
         prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),

@@ -31,7 +31,7 @@ def skinny_rows(M: int, N: int, w8: bool = False) -> bool:
 
 def set_skinny_max_m(m: int = 64) -> None:
     """bf16 rows up to which every GEMM streams weights on the skinny kernels
-    (default 64, the maximum); lower values are A/B probes (bench/decode_ab.py)."""
+    (default 64, the maximum); lower values are A/B probes (bench/probes/decode_ab.py)."""
     global SKINNY_ALWAYS_M
     check(lib().gemm_set_skinny_max_m(int(m)), "gemm_set_skinny_max_m")
     SKINNY_ALWAYS_M = int(m)

@@ -209,7 +209,7 @@ def attn_decode_qkv(qkv: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: 
 
 
 ARGMAX_PART_PER_ROW = 64  # int2 partials per row of the row-split argmax workspace
-ARGMAX_SPLIT = True  # use the workspace when one is given (A/B switch, bench/decode_ab.py)
+ARGMAX_SPLIT = True  # use the workspace when one is given (A/B switch, bench/probes/decode_ab.py)
 
 
 def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None, also: Optional[torch.Tensor] = None,

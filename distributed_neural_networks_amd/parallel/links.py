@@ -107,6 +107,84 @@ class GroupWork:
         return True
 
 
+class HostStagedLink(P2PLink):
+    """A gloo link between ranks whose stages compute on a GPU (transport
+    ``gloo_gpu``: several ranks sharing one device — RCCL refuses two ranks on
+    one GPU — so the multi-process schedules run with device compute and HIP
+    graphs on a 1-GPU box).  Each hop goes device -> pinned host -> gloo ->
+    pinned host -> device, ordered with streams and events the way RCCL
+    orders its P2P:
+
+    * ``isend(t)`` reads ``t`` after the work queued on the current stream
+      when it is posted (a side stream waits on it, copies to pinned memory);
+    * ``irecv(out)`` records the current stream when posted; its ``wait()``
+      lands the bytes in ``out`` on the side stream *after that event only*
+      and makes the current stream wait for the copy — so, exactly as with
+      RCCL, the receive may overwrite ``out`` concurrently with compute
+      queued after the post, and a schedule that reuses a slot too early races
+      here too instead of passing by accident."""
+
+    def __init__(self, peer: int, device: torch.device, group=None):
+        super().__init__(peer, device, group)
+        self._side = torch.cuda.Stream(device)
+
+    @staticmethod
+    def _host_like(t: torch.Tensor) -> torch.Tensor:
+        return torch.empty(t.numel() * t.element_size(), dtype=torch.uint8, pin_memory=True)
+
+    def isend(self, t: torch.Tensor):
+        if not t.is_contiguous():
+            raise ValueError("HostStagedLink.isend needs a contiguous tensor")
+        self._count_send(t)
+        host = self._host_like(t)
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            host.view(t.dtype).view(t.shape).copy_(t, non_blocking=True)
+        self._side.synchronize()
+        return _HostWork(dist.isend(host, self.peer, group=self.group), host)
+
+    def irecv(self, out: torch.Tensor):
+        if not out.is_contiguous():
+            raise ValueError("HostStagedLink.irecv needs a contiguous tensor")
+        self._count_recv(out)
+        posted = torch.cuda.Event()
+        posted.record(torch.cuda.current_stream(self.device))
+        host = self._host_like(out)
+        return _HostWork(dist.irecv(host, self.peer, group=self.group), host, out, posted, self._side)
+
+
+class _HostWork:
+    """Work of a ``HostStagedLink`` op; ``wait`` is idempotent."""
+
+    def __init__(self, work, host, out=None, posted=None, side=None):
+        self.work, self.host, self.out, self.posted, self.side = work, host, out, posted, side
+        self.done = False
+
+    def wait(self):
+        if self.done:
+            return True
+        self.work.wait()
+        if self.out is not None:
+            dev = self.out.device
+            self.side.wait_event(self.posted)
+            with torch.cuda.stream(self.side):
+                self.out.copy_(self.host.view(self.out.dtype).view(self.out.shape), non_blocking=True)
+            landed = torch.cuda.Event()
+            landed.record(self.side)
+            torch.cuda.current_stream(dev).wait_event(landed)
+        self.done = True
+        return True
+
+
+def make_link(peer: int, device: torch.device, group=None) -> P2PLink:
+    """The link for this process's backend: RCCL / gloo-on-CPU move the tensor
+    itself (``P2PLink``); gloo with a GPU stage stages through pinned host
+    memory (``HostStagedLink``)."""
+    if device.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "gloo":
+        return HostStagedLink(peer, device, group)
+    return P2PLink(peer, device, group)
+
+
 class SplitLink:
     """One logical stage hop over several peers: a tensor sent through it is
     cut into ``len(links)`` equal row slices, slice j going to ``links[j]``; a

@@ -111,7 +111,7 @@ def run_generate_dist(ctx, args, stage, info, progress=None) -> int:
     """One rank per stage; tokens return to stage 0 over the back-edge.  The
     prompt shape travels down the chain in a header from stage 0."""
     from ..parallel import comm
-    from ..parallel.links import KIND_DATA, P2PLink
+    from ..parallel.links import KIND_DATA, make_link
     pipe = ctx.pipeline
     S, r, dev = pipe.num_parts, ctx.part_index, info.device
     peer = getattr(ctx, "peer", lambda p: p)  # ranks of this replica's stages
@@ -120,10 +120,10 @@ def run_generate_dist(ctx, args, stage, info, progress=None) -> int:
         log(f"[{ctx.node_id}] note: generated tokens feed the embedding, so they return to stage 0 "
             f"(return_to_node_id '{pipe.return_to_node_id}' is not stage 0)")
     bg = comm.back_group()  # the token back-edge on its own communicator / stream
-    links = RingLinks(prev=P2PLink(peer(r - 1), dev) if r > 0 else None,
-                      nxt=P2PLink(peer(r + 1), dev) if r < S - 1 else None,
-                      back_out=P2PLink(peer(0), dev, bg) if (r == S - 1 and S > 1) else None,
-                      back_in=P2PLink(peer(S - 1), dev, bg) if (r == 0 and S > 1) else None)
+    links = RingLinks(prev=make_link(peer(r - 1), dev) if r > 0 else None,
+                      nxt=make_link(peer(r + 1), dev) if r < S - 1 else None,
+                      back_out=make_link(peer(0), dev, bg) if (r == S - 1 and S > 1) else None,
+                      back_in=make_link(peer(S - 1), dev, bg) if (r == 0 and S > 1) else None)
     M, B = pipe.num_microbatches, pipe.micro_batch_size
     steps = max(1, pipe.decode_steps or 1)
     prompts = None

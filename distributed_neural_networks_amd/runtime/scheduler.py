@@ -406,7 +406,22 @@ class DecodeRing:
         ``prompts[m]`` (B, T) int; other groups pass None).  ``chunk`` > 0
         prefills in pieces of that many tokens (chunked prefill: activation
         buffers and stage hops stay bounded for long prompts; each piece
-        attends to the cache written by the previous ones)."""
+        attends to the cache written by the previous ones).
+
+        Stages with a calibrated fp8 KV cache that is not calibrated yet
+        (``needs_kv_calibration``: the same on every rank, it follows the
+        config) first run this prefill at unit scale, set their per-layer
+        scales from the cache's K / V amax and clear it; then the prefill runs
+        for real.  Once per stage lifetime."""
+        if any(getattr(s, "needs_kv_calibration", False) for s in self.stages):
+            self._prefill(prompts, T, chunk)
+            self.drain()
+            for s in self.stages:
+                if getattr(s, "needs_kv_calibration", False):
+                    s.calibrate_kv()
+        self._prefill(prompts, T, chunk)
+
+    def _prefill(self, prompts, T: int, chunk: int = 0) -> None:
         B, d = self.B, self.d
         C = T if chunk <= 0 else min(chunk, T)
         pieces = [(t0, min(C, T - t0)) for t0 in range(0, T, C)]

@@ -53,7 +53,7 @@ class CifarHipStage(StageCompute):
 
     Units 0-1 always run together (the fused conv1/pool/conv2/pool kernel), so
     the supported ranges are (0,1) = reference part 0, (2,3) = reference part 1,
-    (0,3) = whole model, and the fc1 cut (0,2) | (3,3) whose stage boundary is
+    (0,3) = whole model, (2,2) = fc1 alone (3-stage pipelines), and the fc1 cut (0,2) | (3,3) whose stage boundary is
     the 512-wide hidden (2 KiB/img in fp32 instead of 16 KiB: what the
     multi-GPU placement uses when the xGMI hop, not compute, would bound the
     pipeline, parallel/partition.py ``cifar_cut``).
@@ -61,7 +61,7 @@ class CifarHipStage(StageCompute):
     ``precision`` "fp32" (default, the reference's: fp32 in, fp32 boundary,
     3-term bf16 split products accumulated in fp32) or "bf16"."""
 
-    SUPPORTED = {(0, 1), (2, 3), (0, 3), (0, 2), (3, 3)}
+    SUPPORTED = {(0, 1), (2, 3), (0, 3), (0, 2), (2, 2), (3, 3)}
 
     def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device,
                  precision: str = "fp32"):

@@ -70,7 +70,7 @@ class TransformerStage(StageCompute):
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
                  device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
                  fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0,
-                 kv_dtype: str = "bf16"):
+                 kv_dtype: str = "bf16", kv_scale: str = "calibrated"):
         info = model_info(model)
         # sampling (last stage): temperature 0 = greedy argmax; otherwise
         # Gumbel-max over the top_k logits (0 = all), seeded per (row, position)
@@ -131,6 +131,14 @@ class TransformerStage(StageCompute):
         if kv_dtype == "fp8" and self.Hkv != self.H and (self.hd != 128 or self.H // self.Hkv not in (2, 4)):
             raise ValueError("fp8 KV cache: MHA, or GQA with head dim 128 and 2 or 4 query heads per kv head")
         self.kv_dtype = kv_dtype
+        # fp8 cache scale per layer (powers of two): "unit", or "calibrated" =
+        # set from the K / V amax of the first prefill (DecodeRing.prefill runs
+        # it, then calibrate_kv(), then the real prefill); see set_kv_scales
+        if kv_scale not in ("unit", "calibrated"):
+            raise ValueError(f"kv_scale {kv_scale!r}: unit or calibrated")
+        self.kv_scale_mode = kv_scale
+        self.kv_scales = [(1.0, 1.0)] * (end - start + 1)
+        self.kv_calibrated = False
         kvt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
         self.kc = torch.zeros((L, max_batch, self.Hkv, max_seq, self.hd), dtype=kvt, device=dev)
         self.vc = torch.zeros_like(self.kc)
@@ -152,6 +160,70 @@ class TransformerStage(StageCompute):
                     attach_shuffled(w)
         if self.last and not isinstance(self.w_head, torch.Tensor):
             attach_shuffled(self.w_head)
+
+    # ------------------------------------------------------------------ fp8 KV scale
+    @property
+    def needs_kv_calibration(self) -> bool:
+        return self.kv_dtype == "fp8" and self.kv_scale_mode == "calibrated" and not self.kv_calibrated
+
+    KV_TARGET = 224.0  # calibrated |K|, |V| max maps to <= 224 (half the e4m3 range: headroom for later tokens)
+
+    def calibrate_kv(self) -> List[tuple]:
+        """Per-tensor fp8 K / V scales from what the cache holds now (after a
+        unit-scale prefill): s = 2^ceil(log2(amax / KV_TARGET)) per layer, so
+        the values use the e4m3 normal range instead of its subnormals.  Then
+        clears the cache: the caller re-runs the prefill at the new scale."""
+        scales = []
+        for li in range(len(self.layers)):
+            sk0, sv0 = self.kv_scales[li]
+            ak = _e4m3_amax(self.kc[li]) * sk0
+            av = _e4m3_amax(self.vc[li]) * sv0
+            scales.append(tuple(2.0 ** math.ceil(math.log2(max(a, 1e-30) / self.KV_TARGET)) for a in (ak, av)))
+        self.set_kv_scales(scales)
+        self.kv_calibrated = True
+        self.reset()
+        return scales
+
+    def set_kv_scales(self, scales: List[tuple]) -> None:
+        """Store layer li's K as K / s_k and V as V / s_v in the fp8 cache, with
+        no kernel change: the scales fold into the weights.  The q rows of
+        the QKV projection are multiplied by s_k and the k rows divided by it
+        (q.k unchanged; RoPE is linear); the v rows are divided by s_v and the
+        output projection multiplied by s_v (P.V is linear).  Powers of two
+        keep every bf16 weight exact; e4m3 weights only change their channel
+        scales.  Relative to the scales already applied."""
+        from ..ops.fp8 import Fp8Weight
+        from ..ops.gemm import FoldedLinear, attach_shuffled
+        qn, kn = self.H * self.hd, self.Hkv * self.hd
+        for li, (L, (sk, sv)) in enumerate(zip(self.layers, scales)):
+            ok, ov = self.kv_scales[li]
+            rk, rv = sk / ok, sv / ov
+            if rk == 1.0 and rv == 1.0:
+                continue
+            r = torch.ones(qn + 2 * kn, dtype=torch.float32, device=self.device)
+            r[:qn], r[qn:qn + kn], r[qn + kn:] = rk, 1.0 / rk, 1.0 / rv
+            w = L.w_qkv
+            if isinstance(w, FoldedLinear):
+                if w.bias is not None:
+                    w.bias.mul_(r)
+                if w.colsum is not None:
+                    w.colsum.mul_(r)
+                w = w.w
+            elif L.b_qkv is not None:
+                L.b_qkv.mul_(r)
+            if isinstance(w, Fp8Weight):
+                w.scale.mul_(r)
+            else:
+                w.mul_(r.to(w.dtype)[:, None])
+                if isinstance(L.w_qkv, FoldedLinear) and L.w_qkv.ws is not None:
+                    attach_shuffled(L.w_qkv)
+            if isinstance(L.w_o, Fp8Weight):
+                L.w_o.scale.mul_(rv)
+            else:
+                L.w_o.mul_(rv)
+                if L.w_o_s is not None:
+                    L.w_o_s = attach_shuffled(L.w_o)
+            self.kv_scales[li] = (sk, sv)
 
     def _w(self, w):
         if self.fp8:
@@ -390,14 +462,22 @@ class TransformerStage(StageCompute):
         self.vc.zero_()
 
 
+def _e4m3_amax(t: torch.Tensor) -> float:
+    """max |x| of an e4m3fn tensor without widening it: with the sign bit
+    cleared the bytes order like the magnitudes (0x7f, NaN, never stored)."""
+    b = torch.bitwise_and(t.view(torch.uint8), 0x7F).amax()
+    return float(b.view(1).view(torch.float8_e4m3fn).float().item())
+
+
 def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
                        max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
-                       temperature: float = 0.0, top_k: int = 0, seed: int = 0, kv_dtype: str = "bf16"):
+                       temperature: float = 0.0, top_k: int = 0, seed: int = 0, kv_dtype: str = "bf16",
+                       kv_scale: str = "calibrated"):
     fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
     info = model_info(model)
     max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))
     return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8,
-                            temperature, top_k, seed, kv_dtype=kv_dtype)
+                            temperature, top_k, seed, kv_dtype=kv_dtype, kv_scale=kv_scale)
 
 
 # ---------------------------------------------------------------------- smoke / golden check

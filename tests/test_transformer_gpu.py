@@ -860,3 +860,155 @@ def test_qkv_scatter_prefill_fp8():
     torch.cuda.synchronize()
     assert torch.equal(q, q2)
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
+def test_decode_rows_past_max_tokens():
+    """A non-first stage whose activation buffers are sized for one prefill
+    chunk (max_tokens = micro_batch_size x prefill_chunk, as cli.build_stage
+    sizes them) still decodes microbatch m at scratch rows [m*B, (m+1)*B)
+    beyond max_tokens: the buffers hold max(max_tokens, max_batch) rows, and
+    the output equals a stage with ample buffers."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    sd = ckpt.random_stage_state_dict("gpt2-tiny", 2, 3, False, True, 3, nontrivial=True)
+    small = TransformerStage("gpt2-tiny", sd, 2, 3, False, True, DEV, max_batch=8, max_seq=16, max_tokens=4)
+    big = TransformerStage("gpt2-tiny", sd, 2, 3, False, True, DEV, max_batch=8, max_seq=16, max_tokens=128)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn((2, small.d), device=DEV, generator=g).to(torch.bfloat16)
+    pos = torch.zeros((2,), dtype=torch.int32, device=DEV)
+    a = small.step(x, pos, 2, 1, b0=6)
+    b = big.step(x, pos, 2, 1, b0=6)
+    torch.cuda.synchronize()
+    assert torch.equal(a.probs, b.probs) and torch.equal(a.pred, b.pred)
+    with pytest.raises(ValueError, match="batch slice exceeds"):
+        small.step(x, pos, 2, 1, b0=7)
+
+
+def _decode_vs_golden(st, golden_step, ids, steps, tol):
+    """Prefill ``ids`` then ``steps`` KV-cached decode steps on the device
+    stage; ``golden_step(x, p)`` returns the fp32 golden's last-position logits
+    for the new tokens ``x`` at position ``p`` (the device's own greedy tokens
+    are fed to both sides).  Every step's logits within ``tol`` relative."""
+    B, T = ids.shape
+    pos = torch.zeros(B, dtype=torch.int32, device=DEV)
+    x, Tn, p, worst = ids, T, 0, 0.0
+    for step in range(steps + 1):
+        out = st.step(x.to(DEV, torch.int32), pos, B, Tn)
+        pos.add_(Tn)
+        ref = golden_step(x.to(DEV), p)
+        rel = _rel(out.probs.float(), ref.float())
+        worst = max(worst, rel)
+        assert rel < tol, (step, rel)
+        x = out.pred.long().view(B, 1)
+        p += Tn
+        Tn = 1
+    return worst
+
+
+def test_llama3_8b_two_blocks_full_width_vs_golden():
+    """Llama-3 8B at real width — d 4096, 32 query / 8 kv heads (G = 4), head
+    dim 128, SwiGLU ffn 14336, RoPE theta 5e5, the 128256-wide head — as one
+    device stage of 2 blocks + embed + final norm + head, non-trivial norm
+    gains: an 80-row prefill (256^2 GEMMs, flash attention, qkv_split RoPE)
+    and 8 KV-cached decode steps (skinny GEMMs, MFMA GQA decode attention)
+    against the fp32 torch golden, logits within 2e-2 relative."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import build_golden_stage, model_info
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "llama3-8b"
+    cfg = model_info(model).cfg
+    B, T, steps = 2, 40, 8
+    S = T + steps + 1
+    sd = ckpt.random_stage_state_dict(model, 0, 1, True, True, 31, device=DEV, nontrivial=True)
+    st = TransformerStage(model, sd, 0, 1, True, True, DEV, max_batch=B, max_seq=S)
+    g = build_golden_stage(model, 0, 1, True, True)
+    g.load_state_dict(sd)
+    g = g.to(DEV).eval()
+    del sd
+    hd = cfg.n_embd // cfg.n_head
+    kv = [(torch.zeros(B, cfg.n_kv_head, S, hd, device=DEV), torch.zeros(B, cfg.n_kv_head, S, hd, device=DEV))
+          for _ in range(2)]
+
+    @torch.no_grad()
+    def golden(x, p):
+        return g(x, kv, p, last_only=True)[:, -1]
+    ids = torch.randint(0, cfg.vocab_size, (B, T), generator=torch.Generator().manual_seed(4))
+    worst = _decode_vs_golden(st, golden, ids, steps, 2e-2)
+    print(f"llama3-8b 2 blocks: worst logits rel err {worst:.3e}")
+
+
+def _gpt2_fp8_golden(st, sd):
+    """fp32 reference of a GPT-2 fp8 stage (first + last, all its blocks) on
+    the stage's own dequantised e4m3 weights: the folded pre-norm projections
+    use W' = dequant(e4m3(W diag(gamma))) and bias' = W beta + b on the
+    standardised input; c_proj / mlp.c_proj dequant(e4m3(W)).  Returns
+    step(x, p, quant_act) with a KV cache; with ``quant_act`` each block
+    projection's input is quantised per row to e4m3 (scale = row amax / 448)
+    as the W8A8 prefill kernels do (the last-position head stays W8A16)."""
+    c = st.cfg
+    H, hd, eps = c.n_head, c.n_embd // c.n_head, st.eps
+
+    def dq(w):
+        return w.q[:, :w.k].float() * w.scale[:, None]
+
+    quant = [False]
+
+    def qa(x):
+        if not quant[0]:
+            return x
+        s = x.abs().amax(dim=-1, keepdim=True).clamp_min(1e-12) / 448.0
+        return (x / s).to(torch.float8_e4m3fn).float() * s
+
+    def std(x):
+        return F.layer_norm(x, (x.shape[-1],), eps=eps)
+    layers = [(dq(L.w_qkv.w), L.w_qkv.bias, dq(L.w_o), L.b_o, dq(L.w_up.w), L.w_up.bias, dq(L.w_down), L.b_down)
+              for L in st.layers]
+    head_w, head_b = dq(st.w_head.w), st.w_head.bias
+    wte, wpe = sd["wte.weight"].float().to(DEV), sd["wpe.weight"].float().to(DEV)
+    cache = {}
+
+    @torch.no_grad()
+    def step(x, p, quant_act=False):
+        quant[0] = quant_act
+        B, Tn = x.shape
+        h = wte[x] + wpe[p:p + Tn][None]
+        for j, (wq, bq, wo, bo, wu, bu, wd, bd) in enumerate(layers):
+            qkv = qa(std(h)) @ wq.T + bq
+            q, k, v = qkv.split(c.n_embd, dim=-1)
+            q, k, v = (t.view(B, Tn, H, hd).transpose(1, 2) for t in (q, k, v))
+            if j in cache:
+                k, v = torch.cat([cache[j][0], k], 2), torch.cat([cache[j][1], v], 2)
+            cache[j] = (k, v)
+            att = F.scaled_dot_product_attention(q, k, v, is_causal=Tn > 1)
+            att = att.transpose(1, 2).reshape(B, Tn, c.n_embd)
+            h = h + qa(att) @ wo.T + bo
+            f = F.gelu(qa(std(h)) @ wu.T + bu)
+            h = h + qa(f) @ wd.T + bd
+        return std(h[:, -1]) @ head_w.T + (head_b if head_b is not None else 0)
+    return step
+
+
+@pytest.mark.parametrize("T,quant_act", [(24, False), (64, True)])
+def test_gpt2_xl_fp8_two_blocks_full_width_vs_golden(T, quant_act):
+    """GPT-2 XL at real width with fp8 weights — d 1600, 25 heads (hd 64),
+    c_attn N = 4800 (partial 256-column tiles), the 50257-wide head — as one
+    device stage of 2 blocks + embed + ln_f + head with non-trivial gains and
+    biases, against the fp32 golden on the dequantised e4m3 weights: 2 x 24
+    prompt rows run weight-only W8A16 (fused pre-norm skinny GEMMs), 2 x 64
+    the standardise + quantise + W8A8 fp8-MFMA prefill (golden with the same
+    per-row e4m3 activation quantisation); then 8 W8A16 decode steps.  Logits
+    within 2e-2 relative."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "gpt2-xl"
+    B, steps = 2, 8
+    sd = ckpt.random_stage_state_dict(model, 0, 1, True, True, 17, device=DEV, nontrivial=True)
+    st = TransformerStage(model, sd, 0, 1, True, True, DEV, max_batch=B, max_seq=T + steps + 1, fp8=True)
+    gold = _gpt2_fp8_golden(st, sd)
+    del sd
+    ids = torch.randint(0, 50257, (B, T), generator=torch.Generator().manual_seed(6))
+
+    def golden(x, p):  # only the prefill's block projections are W8A8 (> 64 rows)
+        return gold(x, p, quant_act and p == 0)
+    worst = _decode_vs_golden(st, golden, ids, steps, 2e-2)
+    print(f"gpt2-xl fp8 2 blocks T={T} quant_act={quant_act}: worst logits rel err {worst:.3e}")

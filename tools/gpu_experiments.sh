@@ -27,7 +27,7 @@ case_argmax_ab() {
     --timeout-method thread > gpurun_out/argmax_tests.log 2>&1
   rc=$?; tail -3 gpurun_out/argmax_tests.log; [ $rc -eq 0 ] || return $rc
   out=gpurun_out/argmax_ab.jsonl; : > $out
-  ab() { timeout -k 10 300 python -u bench/decode_ab.py --switch argmax_split --values 0,1 "$@" >> $out 2> gpurun_out/argmax_ab.err; }
+  ab() { timeout -k 10 300 python -u bench/probes/decode_ab.py --switch argmax_split --values 0,1 "$@" >> $out 2> gpurun_out/argmax_ab.err; }
   ab --steps 32 --warmup 4 --prefill_iters 1 &&
   ab --model llama3-8b --stages 8 --batch 1 --prompt 128 --dtype fp8 --steps 32 --warmup 4 --prefill_iters 1 &&
   ab --model gpt2-xl --stages 8 --batch 64 --prompt 512 --dtype fp8 --steps 16 --warmup 2 --prefill_iters 1
@@ -38,8 +38,8 @@ case_decode_ab() {
   # in-process A/B: bf16 skinny row limit 32 (tile path for wide-N heads at M 33-64) vs 64
   out=gpurun_out/decode_ab.jsonl
   : > $out
-  timeout -k 10 300 python bench/decode_ab.py --switch skinny_max_m --values 32,64 --steps 32 --warmup 4 --prefill_iters 1 >> $out 2>gpurun_out/dab.err &&
-  timeout -k 10 400 python bench/decode_ab.py --switch skinny_max_m --values 32,64 --model gpt2-xl --stages 8 --batch 64 --prompt 512 --steps 16 --warmup 2 --prefill_iters 1 >> $out 2>>gpurun_out/dab.err
+  timeout -k 10 300 python bench/probes/decode_ab.py --switch skinny_max_m --values 32,64 --steps 32 --warmup 4 --prefill_iters 1 >> $out 2>gpurun_out/dab.err &&
+  timeout -k 10 400 python bench/probes/decode_ab.py --switch skinny_max_m --values 32,64 --model gpt2-xl --stages 8 --batch 64 --prompt 512 --steps 16 --warmup 2 --prefill_iters 1 >> $out 2>>gpurun_out/dab.err
   rc=$?; cat $out; return $rc
 }
 
@@ -53,7 +53,7 @@ case_flash_check() {
   # flash / decode attention tests, flash-vs-SDPA bench, GPT-2 prefill
   timeout -k 10 300 python -u -m pytest tests/test_transformer_gpu.py -x -q --timeout 120 --timeout-method thread -k "flash or attn or stage or gpt2_small or forward" > gpurun_out/fl_tests.log 2>&1
   rc=$?; tail -2 gpurun_out/fl_tests.log; [ $rc -eq 0 ] || return $rc
-  timeout -k 10 200 python bench/flash_bench.py > gpurun_out/flash.jsonl 2>&1; rc=$?; grep '^{' gpurun_out/flash.jsonl | cut -c1-200; [ $rc -eq 0 ] || return $rc
+  timeout -k 10 200 python bench/probes/flash_bench.py > gpurun_out/flash.jsonl 2>&1; rc=$?; grep '^{' gpurun_out/flash.jsonl | cut -c1-200; [ $rc -eq 0 ] || return $rc
   timeout -k 10 200 python bench/gpt_bench.py --steps 8 --warmup 2 --prefill_iters 5 > gpurun_out/gb.log 2>&1 && tail -1 gpurun_out/gb.log | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('prefill', d['prefill_tokens_per_s'], 'decode ms', d['ms_per_step'])"
 }
 
@@ -94,7 +94,7 @@ case_kv8_ab() {
     > gpurun_out/kv8u_tests.log 2>&1
   rc=$?; tail -2 gpurun_out/kv8u_tests.log; [ $rc -eq 0 ] || return $rc
   out=gpurun_out/kv8u_ab.jsonl; : > $out
-  ab() { timeout -k 10 300 python -u bench/decode_ab.py --switch kv8_u --values 8,10 "$@" >> $out 2> gpurun_out/kv8u_ab.err; }
+  ab() { timeout -k 10 300 python -u bench/probes/decode_ab.py --switch kv8_u --values 8,10 "$@" >> $out 2> gpurun_out/kv8u_ab.err; }
   ab --steps 32 --warmup 4 --prefill_iters 1 --kv fp8 &&
   ab --batch 256 --steps 32 --warmup 4 --prefill_iters 1 --kv fp8 &&
   ab --model gpt2-xl --stages 8 --batch 64 --prompt 512 --dtype fp8 --kv fp8 --steps 16 --warmup 2 --prefill_iters 1
@@ -143,7 +143,7 @@ case_scatter3() {
   timeout -k 10 300 python -u -m pytest tests/test_transformer_gpu.py -m gpu -x -q -k "scatter or gpt2 or golden" \
     --timeout 120 --timeout-method thread > gpurun_out/scatter3_tests.log 2>&1
   rc=$?; tail -2 gpurun_out/scatter3_tests.log; [ $rc -eq 0 ] || return $rc
-  timeout -k 10 400 python -u bench/decode_ab.py --switch qkv_scatter --values 0,1 --rounds 3 --steps 4 --warmup 1 --prefill_iters 5 \
+  timeout -k 10 400 python -u bench/probes/decode_ab.py --switch qkv_scatter --values 0,1 --rounds 3 --steps 4 --warmup 1 --prefill_iters 5 \
     > gpurun_out/scatter3_ab.jsonl 2> gpurun_out/scatter3_ab.err && cat gpurun_out/scatter3_ab.jsonl &&
   bash tools/gpu_prof_prefill.sh && head -8 gpurun_out/prefill_seq.md
 }
