@@ -22,7 +22,7 @@ def main():
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
     dev = torch.device("cuda")
     sd = ckpt.random_stage_state_dict("gpt2-xl", 0, 1, True, True, 17, device=dev, nontrivial=True)
-    for Tn in (24, 64, 128):
+    for Tn in (24, 192, 320):
         st = TransformerStage("gpt2-xl", sd, 0, 1, True, True, dev, max_batch=2, max_seq=Tn + 2, fp8=True)
         ids = torch.randint(0, 50257, (2, Tn), generator=torch.Generator().manual_seed(6))
         pos = torch.zeros(2, dtype=torch.int32, device=dev)

@@ -25,31 +25,37 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("gemm_bf16", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N,
-                        int K, int act, int out_f32, u64 st, u64 wsh, u64 rowstat, u64 colsum) {
+                        int K, int act, int out_f32, u64 st, u64 wsh, u64 rowstat, u64 colsum, u64 ws,
+                        long long ws_bytes) {
     return dnn_gemm_bf16(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, out_f32, ST(st),
-                         CP(wsh), CFP(rowstat), CFP(colsum));
+                         CP(wsh), CFP(rowstat), CFP(colsum), P(ws), ws_bytes);
   }, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
      py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"), py::arg("out_f32"),
-     py::arg("st"), py::arg("wsh") = 0, py::arg("rowstat") = 0, py::arg("colsum") = 0);
+     py::arg("st"), py::arg("wsh") = 0, py::arg("rowstat") = 0, py::arg("colsum") = 0, py::arg("ws") = 0,
+     py::arg("ws_bytes") = 0);
   m.def("gemm_skinny", [](u64 A, int lda, u64 sa, u64 W, int ldw, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr,
                           int M, int N, int K, int act, int out_f32, int fp8, u64 st) {
     return dnn_gemm_skinny(CP(A), lda, CFP(sa), CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act,
                            out_f32, fp8, ST(st));
   });
   m.def("gemm_skinny_norm", [](u64 A, int lda, u64 W, int ldw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M,
-                               int N, int K, int act, int norm, u64 colsum, float eps, u64 st, u64 wsh) {
+                               int N, int K, int act, int norm, u64 colsum, float eps, u64 st, u64 wsh, u64 ws,
+                               long long ws_bytes) {
     return dnn_gemm_skinny_norm(CP(A), lda, CP(W), ldw, P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, norm,
-                                CFP(colsum), eps, ST(st), CP(wsh));
+                                CFP(colsum), eps, ST(st), CP(wsh), P(ws), ws_bytes);
   }, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
      py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"), py::arg("norm"),
-     py::arg("colsum"), py::arg("eps"), py::arg("st"), py::arg("wsh") = 0);
+     py::arg("colsum"), py::arg("eps"), py::arg("st"), py::arg("wsh") = 0, py::arg("ws") = 0, py::arg("ws_bytes") = 0);
   m.def("gemm_skinny_w8", [](u64 A, int lda, u64 W, int ldw, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M,
-                             int N, int K, int act, int norm, u64 colsum, float eps, u64 st, u64 wsh) {
+                             int N, int K, int act, int norm, u64 colsum, float eps, u64 st, u64 wsh, u64 ws,
+                             long long ws_bytes) {
     return dnn_gemm_skinny_w8(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, norm,
-                              CFP(colsum), eps, ST(st), CP(wsh));
+                              CFP(colsum), eps, ST(st), CP(wsh), P(ws), ws_bytes);
   }, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("sw"), py::arg("C"), py::arg("ldc"),
      py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"),
-     py::arg("norm"), py::arg("colsum"), py::arg("eps"), py::arg("st"), py::arg("wsh") = 0);
+     py::arg("norm"), py::arg("colsum"), py::arg("eps"), py::arg("st"), py::arg("wsh") = 0, py::arg("ws") = 0,
+     py::arg("ws_bytes") = 0);
+  m.def("gemm_set_stream", [](int on, long long min_bytes) { return dnn_gemm_set_stream(on, min_bytes); });
   m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 sw, u64 C, int ldc, int M, int N, int K, int nt,
                                 int u, int ks, int pipe, int w8, u64 st) {
     return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, M, N, K, nt, u, ks, pipe, w8, ST(st));

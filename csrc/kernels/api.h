@@ -1,14 +1,17 @@
 // C ABI of the kernel library (every function enqueues on `st` and returns the
 // hipError_t of the launch; 0 = success, negative = rejected shape).
 // GEMM entry points take an optional `Wsh`: the decode (M <= 64) weight in the
-// skinny kernel's fragment order (ops/gemm.py shuffle_weight); nullptr = use W.
+// skinny kernel's fragment order (ops/gemm.py shuffle_weight); nullptr = use W;
+// and an optional workspace `ws` of `ws_bytes` for the decode stream kernel's
+// split-K partials (nullptr: no K split).
 #pragma once
 #include <hip/hip_runtime.h>
 
 extern "C" {
 int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias, const void* R,
                   int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st, const void* Wsh = nullptr,
-                  const float* rowstat = nullptr, const float* colsum = nullptr);
+                  const float* rowstat = nullptr, const float* colsum = nullptr, void* ws = nullptr,
+                  long long ws_bytes = 0);
 int dnn_row_stats(const void* x, int ldx, float* stats, int M, int N, float eps, int rms, hipStream_t st);
 int dnn_gemm_set_tile(int tile);
 int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, int ldw, const float* bias, const float* rowstat,
@@ -26,13 +29,16 @@ int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int ldw, const 
                           int N, int K, int nt, int u, int ks, int pipe, int w8, hipStream_t st);
 int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                          const void* R, int ldr, int M, int N, int K, int act, int norm, const float* colsum, float eps,
-                         hipStream_t st, const void* Wsh = nullptr);
+                         hipStream_t st, const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0);
 int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                        const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
-                       const float* colsum, float eps, hipStream_t st, const void* Wsh = nullptr);
+                       const float* colsum, float eps, hipStream_t st, const void* Wsh = nullptr, void* ws = nullptr,
+                       long long ws_bytes = 0);
 int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw, void* C, int ldc,
                     const float* bias, const void* R, int ldr, int M, int N, int K, int act, int out_f32, int fp8,
-                    hipStream_t st, const void* Wsh = nullptr);
+                    hipStream_t st, const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0);
+// decode stream GEMM (gemm_stream.h) switch: on/off, and the weight-byte threshold (<= 0 keeps it)
+int dnn_gemm_set_stream(int on, long long min_bytes);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);

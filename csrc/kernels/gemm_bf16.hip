@@ -695,7 +695,7 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 template <int ACT, bool F32>
 static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                         const void* R, int ldr, int M, int N, int K, hipStream_t st, const void* Wsh,
-                        const float2* rowstat, const float* colsum) {
+                        const float2* rowstat, const float* colsum, void* ws, long long ws_bytes) {
   // decode-sized: the weight-streaming skinny kernels (gemm_skinny.hip); medium
   // M (<= 256) too while the 128^2 tiles would not fill 3/4 of the CUs (same
   // rule as ops/gemm.py skinny_rows)
@@ -703,7 +703,8 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   // path folds its norm itself, dnn_gemm_skinny_norm)
   if (rowstat == nullptr &&
       (M <= g_skinny_max_m || (M <= 256 && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 192))) {
-    dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh);
+    dnn_gemm_skinny(A, lda, nullptr, W, ldw, nullptr, C, ldc, bias, R, ldr, M, N, K, ACT, F32 ? 1 : 0, 0, st, Wsh, ws,
+                    ws_bytes);
     return;
   }
   // Auto choice by wave quantisation: the 256^2 kernel runs 1 block/CU (256
@@ -734,14 +735,15 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
 // residual (ops/gemm.py linear_norm at prefill sizes); nullptr = plain GEMM.
 extern "C" int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                              const void* R, int ldr, int M, int N, int K, int act, int out_f32, hipStream_t st,
-                             const void* Wsh, const float* rowstat, const float* colsum) {
+                             const void* Wsh, const float* rowstat, const float* colsum, void* ws,
+                             long long ws_bytes) {
   if (K % 64 != 0 || M <= 0 || N <= 0) return -1;
   if (colsum != nullptr && rowstat == nullptr) return -1;
   const float2* rs = reinterpret_cast<const float2*>(rowstat);
 #define DISPATCH(a)                                                                                  \
   if (act == a) {                                                                                    \
-    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum); \
-    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum);        \
+    if (out_f32) launch_gemm<a, true>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum, ws, ws_bytes); \
+    else launch_gemm<a, false>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, st, Wsh, rs, colsum, ws, ws_bytes);        \
     return (int)hipGetLastError();                                                                   \
   }
   DISPATCH(ACT_NONE)

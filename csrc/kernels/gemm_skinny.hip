@@ -29,6 +29,7 @@
 // and so the step time halve.  KS is chosen on the host so that N/16 x KS waves
 // cover the CUs.
 #include "gemm_epilogue.h"
+#include "gemm_stream.h"
 
 namespace dnn {
 
@@ -361,6 +362,74 @@ using namespace dnn;
 
 constexpr int SKINNY_MAX_M = 256;  // M > 64 only through the M split (medium-batch decode)
 
+// ---- stream kernel dispatch (gemm_stream.h): 17..64 rows, fragment-order
+// weights of >= g_stream_min_bytes; narrow N splits K across workgroups into
+// the caller's workspace (no workspace: one slice).
+static int g_stream_on = 1;  // 0 off, 1 where it measured faster, 2 forced (tests)
+static long long g_stream_min_bytes = 8ll << 20;
+
+// K-split plan: ntiles x splitk workgroups, cps chunks per slice.  Returns
+// false where the stream kernel measured slower than gemm_skinny (few K-steps
+// per workgroup: the prologue latency and, when split, the extra reduce
+// launch are not amortised — profiles/r3_stream_ab_*.jsonl): every workgroup
+// must stream >= 6 K-steps.
+static constexpr int STREAM_NT = 2, STREAM_MIN_STEPS = 6;
+
+template <bool W8>
+static bool stream_plan(int MP, int N, int kbytes, bool have_ws, long long ws_bytes, int& splitk, int& cps) {
+  constexpr int BN = 64 * STREAM_NT, CS = StrCfg<W8>::CS;
+  const int ntiles = (N + BN - 1) / BN, nch = kbytes / 64, steps = (nch + CS - 1) / CS;
+  splitk = 1;
+  if (ntiles < 160 && have_ws) {
+    splitk = min((256 + ntiles - 1) / ntiles, max(1, steps / STREAM_MIN_STEPS));
+    auto need = [&](int sk) { return (long long)sk * MP * ntiles * BN * 4 + (long long)sk * MP * 2 * 4; };
+    while (splitk > 1 && need(splitk) > ws_bytes) --splitk;
+  }
+  cps = (steps + splitk - 1) / splitk * CS;
+  splitk = (nch + cps - 1) / cps;
+  if (g_stream_on == 2) return true;  // forced (tests): every eligible shape, however small
+  if (splitk == 1 && ntiles < 128) return false;  // too few workgroups to stream at chip rate
+  return cps / CS >= STREAM_MIN_STEPS;
+}
+
+template <int ACT, int NORM, bool W8, int MT>
+static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
+                            const float* bias, const void* R, int ldr, int M, int N, int kbytes,
+                            const float* colsum, float eps, hipStream_t st, void* ws, int splitk, int cps) {
+  constexpr int NT = STREAM_NT, BN = 64 * NT, MP = MT * 16;
+  const int ntiles = (N + BN - 1) / BN, nch = kbytes / 64;
+  const int kelems = W8 ? kbytes : kbytes / 2;
+  const dim3 grid(ntiles * splitk), block(256);
+  if (splitk == 1) {
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, W8, NORM, ACT, false>), grid, block, 0, st, (const uint8_t*)A,
+                       lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch, cps, colsum,
+                       eps, kelems, (float*)nullptr);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, W8, NORM, ACT, true>), grid, block, 0, st, (const uint8_t*)A, lda_b,
+                     (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch, cps, colsum, eps, kelems,
+                     (float*)ws);
+  const int NO = ACT == ACT_SILU_MUL ? N / 2 : N;
+  const long long threads = (long long)M * ((NO + 3) / 4);
+  hipLaunchKernelGGL((gemm_stream_reduce<ACT, NORM, W8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                     (const float*)ws, splitk, MP, ntiles * BN, (const uint8_t*)A, lda_b, sw, colsum, eps, kelems, C,
+                     ldc, bias, (const bf16_t*)R, ldr, M, N);
+  return (int)hipGetLastError();
+}
+
+template <int ACT, int NORM, bool W8>
+static bool stream_eligible(const void* A, int lda_b, const void* Wsh, int M, int N, int kbytes) {
+  if (!g_stream_on || Wsh == nullptr || M < 17 || M > 64 || kbytes % 64 != 0) return false;
+  if (((uintptr_t)A & 15) != 0 || (lda_b & 15) != 0) return false;
+  return (long long)((N + 15) / 16 * 16) * kbytes >= g_stream_min_bytes;
+}
+
+extern "C" int dnn_gemm_set_stream(int on, long long min_bytes) {
+  g_stream_on = on;
+  if (min_bytes > 0) g_stream_min_bytes = min_bytes;
+  return 0;
+}
+
 // Per chunk a wave issues NT weight loads and MT activation loads (L2) for
 // NT x MT MFMAs.  The configuration table below is fitted to
 // bench/skinny_sweep.py on MI355X (profiles/r1_skinny_sweep.jsonl, weights
@@ -391,7 +460,18 @@ template <int ACT, bool F32, bool FP8, int NORM = NORM_NONE, bool W8 = false>
 static int launch_skinny(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st, const float* colsum = nullptr, float eps = 0.f,
-                         const void* Wsh = nullptr) {
+                         const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0) {
+  if constexpr (!F32 && !FP8 && ACT != ACT_RELU) {
+    int splitk = 1, cps = 0;
+    if (stream_eligible<ACT, NORM, W8>(A, lda_b, Wsh, M, N, kbytes) &&
+        stream_plan<W8>(M <= 32 ? 32 : 64, N, kbytes, ws != nullptr, ws_bytes, splitk, cps)) {
+      if (M <= 32)
+        return launch_stream_mt<ACT, NORM, W8, 2>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps,
+                                                  st, ws, splitk, cps);
+      return launch_stream_mt<ACT, NORM, W8, 4>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps,
+                                                st, ws, splitk, cps);
+    }
+  }
   const bool wide = N >= 16384;
 #define CFG(MTV, NTV, UV, PV, KSV)                                                                                   \
   return launch_skinny_cfg<ACT, F32, FP8, MTV, NTV, UV, PV, NORM, W8>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, R,   \
@@ -470,7 +550,8 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
 // bf16: K % 32 == 0 (64-B chunks), M <= SKINNY_MAX_M (M > 64: M split).  fp8: K (bytes) % 64 == 0, M <= 64.
 extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw,
                                void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int K,
-                               int act, int out_f32, int fp8, hipStream_t st, const void* Wsh) {
+                               int act, int out_f32, int fp8, hipStream_t st, const void* Wsh, void* ws,
+                               long long ws_bytes) {
   const int eb = fp8 ? 1 : 2;
   const int kbytes = K * eb;
   if (M <= 0 || M > (fp8 ? 64 : SKINNY_MAX_M) || N <= 0 || kbytes % 64 != 0) return -1;
@@ -488,7 +569,7 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
     return out_f32 ? launch_skinny<a, true, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st,   \
                                                    nullptr, 0.f, Wsh)                                         \
                    : launch_skinny<a, false, false>(A, la, sa, W, lw, sw, C, ldc, bias, R, ldr, M, N, kbytes, st,  \
-                                                    nullptr, 0.f, Wsh);                                       \
+                                                    nullptr, 0.f, Wsh, ws, ws_bytes);                         \
   }
   SKD(ACT_NONE)
   SKD(ACT_RELU)
@@ -503,7 +584,8 @@ extern "C" int dnn_gemm_skinny(const void* A, int lda, const float* sa, const vo
 // ops/gemm.py fold_norm.  act: NONE / GELU / SILU_MUL.
 extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, const float* bias,
                                     const void* R, int ldr, int M, int N, int K, int act, int norm,
-                                    const float* colsum, float eps, hipStream_t st, const void* Wsh) {
+                                    const float* colsum, float eps, hipStream_t st, const void* Wsh, void* ws,
+                                    long long ws_bytes) {
   const int kbytes = K * 2;
   if (M <= 0 || M > SKINNY_MAX_M || N <= 0 || kbytes % 64 != 0) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
@@ -512,7 +594,7 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
 #define SKN(a, nm)                                                                                                   \
   if (act == a && norm == nm)                                                                                        \
     return launch_skinny<a, false, false, nm>(A, la, nullptr, W, lw, nullptr, C, ldc, bias, R, ldr, M, N, kbytes, st, \
-                                              colsum, eps, Wsh);
+                                              colsum, eps, Wsh, ws, ws_bytes);
   SKN(ACT_NONE, NORM_RMS)
   SKN(ACT_SILU_MUL, NORM_RMS)
   SKN(ACT_NONE, NORM_LN)
@@ -527,7 +609,8 @@ extern "C" int dnn_gemm_skinny_norm(const void* A, int lda, const void* W, int l
 // (norm 0 = none).  K % 64 == 0 (logical K; the weight rows may be padded).
 extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const float* sw, void* C, int ldc,
                                   const float* bias, const void* R, int ldr, int M, int N, int K, int act, int norm,
-                                  const float* colsum, float eps, hipStream_t st, const void* Wsh) {
+                                  const float* colsum, float eps, hipStream_t st, const void* Wsh, void* ws,
+                                  long long ws_bytes) {
   if (M <= 0 || M > SKINNY_MAX_M || N <= 0 || K % 64 != 0 || ldw < K || sw == nullptr) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
   if (norm == NORM_LN && colsum == nullptr) return -1;
@@ -535,7 +618,7 @@ extern "C" int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw
 #define SKW(a, nm)                                                                                                    \
   if (act == a && norm == nm)                                                                                         \
     return launch_skinny<a, false, false, nm, true>(A, la, nullptr, W, ldw, sw, C, ldc, bias, R, ldr, M, N, K, st,     \
-                                                    colsum, eps, Wsh);
+                                                    colsum, eps, Wsh, ws, ws_bytes);
   SKW(ACT_NONE, NORM_NONE)
   SKW(ACT_NONE, NORM_RMS)
   SKW(ACT_SILU_MUL, NORM_RMS)

@@ -101,9 +101,11 @@ def set_fp8_tile(tile: int = 0) -> None:
 
 def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, norm: int = 0,
-              colsum: Optional[torch.Tensor] = None, eps: float = 0.0) -> torch.Tensor:
+              colsum: Optional[torch.Tensor] = None, eps: float = 0.0,
+              ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight-only fp8 GEMM for decode-sized M (<= 256): bf16 x (M, K) times e4m3 w, bf16 out.
-    ``norm`` (1 RMS / 2 LN, with ``colsum`` for LN) fuses a folded pre-norm."""
+    ``norm`` (1 RMS / 2 LN, with ``colsum`` for LN) fuses a folded pre-norm.
+    ``ws``: ``gemm.decode_workspace`` (split-K partials of the decode stream GEMM)."""
     M, K = x.shape
     N, kp = w.q.shape
     if M > 256 or (w.k and w.k != K) or kp < K or K % 64:
@@ -117,7 +119,8 @@ def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None
         raise ValueError("linear_w8: bad output buffer")
     if w.shuf is not None and w.shuf.numel() != -(-N // 16) * 16 * K:
         raise ValueError("linear_w8: shuf is not shuffle_weight(w.q[:, :K])")
+    wsp, wsb = (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
     check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0), ptr(bias),
                                ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, act, norm,
-                               ptr(colsum), eps, stream_ptr(), ptr(w.shuf)), "gemm_skinny_w8")
+                               ptr(colsum), eps, stream_ptr(), ptr(w.shuf), wsp, wsb), "gemm_skinny_w8")
     return out

@@ -37,12 +37,41 @@ def set_skinny_max_m(m: int = 64) -> None:
     SKINNY_ALWAYS_M = int(m)
 _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "silu_mul": ACT_SILU_MUL}
 
+DECODE_WS_BYTES = 16 << 20
+_decode_ws = {}
+
+
+def decode_workspace(device, slot: int = 0) -> torch.Tensor:
+    """Split-K workspace of the decode stream GEMM (``csrc/kernels/gemm_stream.h``):
+    fp32 partial slabs of one projection at a time.  One per (device, slot):
+    GEMMs on one stream reuse it in stream order; concurrent microbatches
+    (``DecodeRing`` lanes) pass their own slot.  Allocated on first use (a
+    graph's warm-up run, never inside a capture)."""
+    key = (str(device), slot)
+    t = _decode_ws.get(key)
+    if t is None:
+        t = _decode_ws[key] = torch.empty(DECODE_WS_BYTES, dtype=torch.uint8, device=device)
+    return t
+
+
+def set_stream_gemm(on: int = 1, min_bytes: int = 0) -> None:
+    """Decode stream GEMM: 0 off, 1 on where it measured faster (default), 2
+    forced on every eligible shape (tests); ``min_bytes`` = weight-byte
+    threshold (0 keeps it)."""
+    check(lib().gemm_set_stream(int(on), int(min_bytes)), "gemm_set_stream")
+
+
+def _ws_args(ws: Optional[torch.Tensor]):
+    return (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
+
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None,
-           rowstat: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+           rowstat: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
+           ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` on the skinny path (``skinny_rows``).
+    ``ws``: ``decode_workspace`` for the decode stream GEMM's split-K partials.
     ``rowstat`` ((M, 2) fp32 from ``transformer_ops.row_stats``) / ``colsum``: a
     folded pre-norm applied in the epilogue, ``rstd (x W^T) - mean rstd colsum``
     (MFMA tile kernels only)."""
@@ -74,10 +103,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         raise ValueError("linear: rowstat must be contiguous fp32 (M, 2)")
     if colsum is not None and (rowstat is None or colsum.dtype != torch.float32 or colsum.numel() < N):
         raise ValueError("linear: colsum needs rowstat and N fp32 entries")
+    wsp, wsb = _ws_args(ws)
     check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
                           ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
                           1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf), ptr(rowstat),
-                          ptr(colsum)), "gemm_bf16")
+                          ptr(colsum), wsp, wsb), "gemm_bf16")
     return out
 
 
@@ -147,7 +177,7 @@ def fold_norm(w: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor]
 def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, std_buf: Optional[torch.Tensor] = None,
                 ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
-                s8: Optional[torch.Tensor] = None) -> torch.Tensor:
+                s8: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  Decode-sized M (<= 64):
     one skinny-GEMM launch that accumulates the row statistics from the A
     fragments it streams (bf16 weights, or e4m3 weights converted in registers).
@@ -184,7 +214,7 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
         return linear(xs[:M], f.w, f.bias, a, residual, out)
     if w8:
-        return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps)
+        return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps, ws=ws)
     if K % 32:
         raise ValueError(f"linear_norm: K={K} must be a multiple of 32")
     Nout = N // 2 if a == ACT_SILU_MUL else N
@@ -196,9 +226,10 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         raise ValueError("linear_norm: bad residual")
     if f.ws is not None and f.ws.numel() != -(-N // 16) * 16 * K * 2:
         raise ValueError("linear_norm: ws is not shuffle_weight(w)")
+    wsp, wsb = _ws_args(ws)
     check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0), ptr(f.bias),
                                  ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, a, f.norm,
-                                 ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws)), "gemm_skinny_norm")
+                                 ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws), wsp, wsb), "gemm_skinny_norm")
     return out
 
 QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)

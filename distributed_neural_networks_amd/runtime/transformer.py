@@ -35,8 +35,8 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import transformer_ops as T_
-from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, fold_norm, linear, linear_norm, pack_gate_up,
-                        qkv_scatter_norm, skinny_rows)
+from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, decode_workspace, fold_norm, linear, linear_norm,
+                        pack_gate_up, qkv_scatter_norm, skinny_rows)
 from .stages import StageCompute, StageOutput
 
 
@@ -294,13 +294,13 @@ class TransformerStage(StageCompute):
             self.logits = torch.empty((ntok, self.Vpad), dtype=bf, device=dev)
             self.next_ids = torch.empty((ntok,), dtype=torch.int32, device=dev)
 
-    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None):
+    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None, ws=None):
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
             if skinny_rows(x.shape[0], w.q.shape[0], w8=True):  # decode: weight-only fp8 (bf16 activations)
-                return linear_w8(x, w, b, act, residual, out)
+                return linear_w8(x, w, b, act, residual, out, ws=ws)
             return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
-        return linear(x, w, b, act, residual, out, w_shuf=w_shuf)
+        return linear(x, w, b, act, residual, out, w_shuf=w_shuf, ws=ws)
 
     # ------------------------------------------------------------------ specs
     act_dtype = torch.bfloat16  # stage-boundary hidden states
@@ -360,6 +360,8 @@ class TransformerStage(StageCompute):
             q8 = self.q8[r0 * (self.q8.numel() // self.buf_rows):]
             s8 = self.s8[r0:]
         ws = self.ws[r0 * self.ws_per_seq:] if T == 1 else self.ws
+        # decode stream-GEMM split-K workspace: one per concurrent microbatch slot
+        gws = decode_workspace(self.device, b0 // B) if T == 1 else None
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
             att = self.buf_att[r0:r1]
@@ -370,7 +372,7 @@ class TransformerStage(StageCompute):
                 pass  # prefill (no RoPE): c_attn wrote q head-major and K / V straight into the caches
             elif self.fuse_norm:
                 qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[r0:r1], std_buf=a, ones=self.ones, q8=q8,
-                                  s8=s8)
+                                  s8=s8, ws=gws)
             else:
                 T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
                 qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[r0:r1])
@@ -384,15 +386,15 @@ class TransformerStage(StageCompute):
             else:
                 T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
-            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s)
+            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s, ws=gws)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
             if self.fuse_norm:
                 f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[r0:r1], std_buf=a, ones=self.ones, q8=q8,
-                                s8=s8)
+                                s8=s8, ws=gws)
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
                 f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[r0:r1])
-            self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s)
+            self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s, ws=gws)
             h_in = h
         if not self.last:
             if out is not None:
@@ -407,7 +409,7 @@ class TransformerStage(StageCompute):
         if self.fuse_norm:
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
             linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf[r0:], ones=self.ones,
-                        q8=q8, s8=s8)
+                        q8=q8, s8=s8, ws=gws)
         else:
             lnf = self.buf_lnf[r0:r0 + rows]
             T_.layernorm(src, self.lnf_w, self.lnf_b, lnf, self.eps, self.rms, rows=rows, ldx=ldx)

@@ -1,0 +1,142 @@
+"""Decode stream GEMM (csrc/kernels/gemm_stream.h): 17..64 rows, fragment-order
+weights, A shared through LDS, K split across workgroups into a workspace.
+Every variant (bf16 / W8A16 weights, no norm / RMS / LN folded pre-norm,
+none / GELU / SwiGLU epilogues, residual, one slice / split-K) against the
+fp32 torch reference of the same op, and bit-compared with itself across
+workspace sizes where the slicing cannot change the sums' grouping."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.fixture
+def force_stream():
+    from distributed_neural_networks_amd.ops.gemm import set_stream_gemm
+    set_stream_gemm(2, 1)  # forced: every eligible shape, however small, split or not
+    yield
+    set_stream_gemm(1, 8 << 20)
+
+
+@pytest.mark.parametrize("M", [17, 32, 48, 64])
+@pytest.mark.parametrize("N,K", [(640, 1024), (3072, 4096), (4096, 1536)])
+@pytest.mark.parametrize("split", [False, True])
+def test_stream_plain_bias_residual(force_stream, M, N, K, split):
+    from distributed_neural_networks_amd.ops.gemm import decode_workspace, linear, shuffle_weight
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=DEV) * 0.1
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ W.float().t() + b + R.float()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ws = decode_workspace(DEV, 7) if split else None
+    linear(x, W, b, residual=R, out=out, w_shuf=shuffle_weight(W), ws=ws)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+@pytest.mark.parametrize("M", [24, 64])
+@pytest.mark.parametrize("rms,act", [(True, "none"), (True, "silu_mul"), (False, "none"), (False, "gelu")])
+@pytest.mark.parametrize("split", [False, True])
+def test_stream_folded_norm(force_stream, M, rms, act, split):
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear_norm,
+                                                          pack_gate_up)
+    torch.manual_seed(9)
+    K, N = 2048, 2048
+    x = (torch.randn(M, K, device=DEV) * 2 + 3.0).bfloat16()  # |mean| >> 0: the LN shift matters
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = None if rms else torch.randn(K, device=DEV) * 0.1
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = None if rms else torch.randn(N, device=DEV) * 0.1
+    R = torch.randn(M, N, device=DEV).bfloat16() if act == "none" else None
+    xf = x.float()
+    xn = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma if rms
+          else F.layer_norm(xf, (K,), gamma, beta, 1e-5))
+    if act == "silu_mul":
+        g, u = W[: N // 2], W[N // 2:]
+        Wk = pack_gate_up(g, u)
+        ref = F.silu(xn @ g.t()) * (xn @ u.t())
+    else:
+        Wk = W
+        ref = xn @ W.t() + (bias if bias is not None else 0)
+        if act == "gelu":
+            ref = F.gelu(ref)
+    if R is not None:
+        ref = ref + R.float()
+    f = attach_shuffled(fold_norm(Wk, gamma, beta, bias, rms, 1e-5, DEV))
+    out = torch.empty(ref.shape, device=DEV, dtype=torch.bfloat16)
+    linear_norm(x, f, act=act, residual=R, out=out, ws=decode_workspace(DEV, 7) if split else None)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1.5e-2, _rel(out, ref)
+
+
+@pytest.mark.parametrize("M", [20, 64])
+@pytest.mark.parametrize("norm,act", [(0, 0), (2, 2), (1, 3)])
+@pytest.mark.parametrize("split", [False, True])
+def test_stream_w8(force_stream, M, norm, act, split):
+    """Weight-only fp8 (e4m3 weights widened in registers): vs the same algebra
+    in fp32 on the dequantised weights."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import attach_shuffled, decode_workspace, pack_gate_up
+    torch.manual_seed(3)
+    K, N = 1600, 6400
+    x = (torch.randn(M, K, device=DEV) + (1.0 if norm == 2 else 0.0)).bfloat16()
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    if act == 3:
+        W = pack_gate_up(W[: N // 2], W[N // 2:])
+    w8 = attach_shuffled(quantize_weight(W, DEV))
+    wd = w8.q[:, :K].float() * w8.scale[:, None]
+    xf = x.float()
+    colsum = None
+    if norm == 2:
+        xs = F.layer_norm(xf, (K,), eps=1e-5)
+        colsum = wd.sum(1).contiguous()
+    elif norm == 1:
+        xs = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    else:
+        xs = xf
+    y = xs @ wd.t()
+    bias = torch.randn(N, device=DEV) * 0.1 if act == 2 else None
+    if act == 2:
+        ref = F.gelu(y + bias)
+    elif act == 3:
+        y = y.view(M, N // 16, 2, 8)
+        ref = (F.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, N // 2)
+    else:
+        ref = y
+    out = torch.empty(ref.shape, device=DEV, dtype=torch.bfloat16)
+    linear_w8(x, w8, bias, act, None, out, norm, colsum, 1e-5, ws=decode_workspace(DEV, 7) if split else None)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+def test_stream_matches_skinny_kernel_decode_shapes():
+    """Llama-3 8B decode projections (M = 32) on the stream kernel equal the
+    skinny kernel's output within bf16 rounding of the differently ordered
+    sums, and the fp32 reference."""
+    from distributed_neural_networks_amd.ops.gemm import decode_workspace, linear, set_stream_gemm, shuffle_weight
+    torch.manual_seed(1)
+    M = 32
+    for N, K in ((6144, 4096), (4096, 14336)):
+        x = torch.randn(M, K, device=DEV).bfloat16()
+        W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+        ws_ = shuffle_weight(W)
+        outs = []
+        for on in (2, 0):
+            set_stream_gemm(on, 8 << 20)
+            o = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            linear(x, W, out=o, w_shuf=ws_, ws=decode_workspace(DEV, 7))
+            outs.append(o)
+        set_stream_gemm(1, 8 << 20)
+        torch.cuda.synchronize()
+        ref = x.float() @ W.float().t()
+        assert _rel(outs[0], ref) < 1e-2 and _rel(outs[0], outs[1]) < 1e-2
