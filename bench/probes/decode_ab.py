@@ -29,6 +29,8 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_KV8_U"] = str(v)
     elif switch == "qkv_scatter":  # prefill c_attn straight into q / the KV caches (ops/gemm.py QKV_SCATTER)
         gemm.QKV_SCATTER = bool(v)
+    elif switch == "stream":  # decode stream GEMM: 0 off, 1 where it measured faster, 2 forced (gemm_stream.h)
+        gemm.set_stream_gemm(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

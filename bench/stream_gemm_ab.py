@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the decode stream GEMM (csrc/kernels/gemm_stream.h) against the
-skinny kernel it replaces, on the decode projection shapes (Llama-3 8B at
+skinny kernel it replaces (the production plan: shapes the plan rejects
+fall back to the skinny kernel in both arms), on the decode projection shapes (Llama-3 8B at
 M = 32, GPT-2 XL W8 at M = 64, ...): device time per launch from HIP-graph
 replays of rotating weight copies (>= 1 GiB between reuses, so no MALL
 hits), the two kernels interleaved in one process.
@@ -86,7 +87,7 @@ def main():
             res = {"shape": name, "M": M, "N": N, "K": K, "w8": args.w8, "norm": norm, "MB": round(wbytes / 1e6, 1)}
             ts = {"stream": [], "skinny": []}
             for _ in range(args.rounds):
-                for k, on in (("stream", 2), ("skinny", 0)):
+                for k, on in (("stream", 1), ("skinny", 0)):
                     set_stream_gemm(on, 8 << 20)
                     ts[k].append(timed())
             set_stream_gemm(1, 8 << 20)

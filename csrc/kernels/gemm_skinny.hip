@@ -369,27 +369,31 @@ static int g_stream_on = 1;  // 0 off, 1 where it measured faster, 2 forced (tes
 static long long g_stream_min_bytes = 8ll << 20;
 
 // K-split plan: ntiles x splitk workgroups, cps chunks per slice.  Returns
-// false where the stream kernel measured slower than gemm_skinny (few K-steps
-// per workgroup: the prologue latency and, when split, the extra reduce
-// launch are not amortised — profiles/r3_stream_ab_*.jsonl): every workgroup
-// must stream >= 6 K-steps.
-static constexpr int STREAM_NT = 2, STREAM_MIN_STEPS = 6;
+// false where the stream kernel measured slower than gemm_skinny
+// (profiles/r3_stream_ab_*.jsonl, in-pipeline profiles/r3_llama8b_b32_decode_*):
+// fewer than 192 workgroups (most CUs idle), fewer than 6 K-steps per slice
+// (the prologue latency and the split's reduce launch not amortised), or an
+// unsplit K of fewer than 12 steps (small-K wide-N heads: the skinny kernel's
+// K-split waves ramp faster).  Measured wins: Llama-3 8B gate|up (no split,
+// 224 workgroups x 16 steps) and down (8 slices x 7 steps).
+static constexpr int STREAM_NT = 2, STREAM_MIN_STEPS = 6, STREAM_MIN_WGS = 192, STREAM_MAX_SPLIT = 16;
 
 template <bool W8>
 static bool stream_plan(int MP, int N, int kbytes, bool have_ws, long long ws_bytes, int& splitk, int& cps) {
   constexpr int BN = 64 * STREAM_NT, CS = StrCfg<W8>::CS;
   const int ntiles = (N + BN - 1) / BN, nch = kbytes / 64, steps = (nch + CS - 1) / CS;
   splitk = 1;
-  if (ntiles < 160 && have_ws) {
-    splitk = min((256 + ntiles - 1) / ntiles, max(1, steps / STREAM_MIN_STEPS));
+  if (ntiles < STREAM_MIN_WGS && have_ws) {
+    const int by_steps = g_stream_on == 2 ? steps : max(1, steps / STREAM_MIN_STEPS);  // forced: split anything
+    splitk = min(min((256 + ntiles - 1) / ntiles, STREAM_MAX_SPLIT), by_steps);
     auto need = [&](int sk) { return (long long)sk * MP * ntiles * BN * 4 + (long long)sk * MP * 2 * 4; };
     while (splitk > 1 && need(splitk) > ws_bytes) --splitk;
   }
   cps = (steps + splitk - 1) / splitk * CS;
   splitk = (nch + cps - 1) / cps;
-  if (g_stream_on == 2) return true;  // forced (tests): every eligible shape, however small
-  if (splitk == 1 && ntiles < 128) return false;  // too few workgroups to stream at chip rate
-  return cps / CS >= STREAM_MIN_STEPS;
+  if (g_stream_on == 2) return splitk <= STREAM_MAX_SPLIT;  // forced (tests): every eligible shape
+  if (ntiles * splitk < STREAM_MIN_WGS || cps / CS < STREAM_MIN_STEPS) return false;
+  return splitk > 1 || steps >= 2 * STREAM_MIN_STEPS;
 }
 
 template <int ACT, int NORM, bool W8, int MT>

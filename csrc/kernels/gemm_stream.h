@@ -328,7 +328,12 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __re
   }
 }
 
-// Split-K combine + epilogue: one thread per (row, 4 output columns).
+// Split-K combine + epilogue: one thread per (row, 4 output columns).  Every
+// slice's partial is loaded before the first add (splitk <= STR_MAX_SPLIT,
+// surplus loads clamped to the last slice and weighted 0): one memory round
+// trip, not splitk dependent ones.
+constexpr int STR_MAX_SPLIT = 16;
+
 template <int ACT, int NORM, bool W8>
 __global__ __launch_bounds__(256) void gemm_stream_reduce(const float* __restrict__ slab, int splitk, int MP, int Ns,
                                                           const uint8_t* __restrict__ A, int lda_b,
@@ -357,8 +362,13 @@ __global__ __launch_bounds__(256) void gemm_stream_reduce(const float* __restric
     rstd = rsqrtf(var + eps);
   }
   auto col = [&](int n) {  // combined, scaled, normalised accumulator of 4 columns n..n+3
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < splitk; ++s) v += *reinterpret_cast<const f32x4*>(slab + ((size_t)s * MP + m) * Ns + n);
+    f32x4 part[STR_MAX_SPLIT];
+#pragma unroll
+    for (int s = 0; s < STR_MAX_SPLIT; ++s)
+      part[s] = *reinterpret_cast<const f32x4*>(slab + ((size_t)min(s, splitk - 1) * MP + m) * Ns + n);
+    f32x4 v = part[0];
+#pragma unroll
+    for (int s = 1; s < STR_MAX_SPLIT; ++s) v += part[s] * (s < splitk ? 1.f : 0.f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool ok = n + r < N;
