@@ -29,6 +29,13 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_KV8_U"] = str(v)
     elif switch == "qkv_scatter":  # prefill c_attn straight into q / the KV caches (ops/gemm.py QKV_SCATTER)
         gemm.QKV_SCATTER = bool(v)
+    elif switch == "decode_splits":  # decode-attention split count (0 = the heuristic), read at stage build
+        if v:
+            os.environ["DNN_DECODE_SPLITS"] = str(v)
+        else:
+            os.environ.pop("DNN_DECODE_SPLITS", None)
+    elif switch == "stream_fold":  # stream GEMM split-K combine: 1 in the launch, 0 separate reduce launch
+        gemm.set_stream_gemm(1, 0, v)
     elif switch == "stream":  # decode stream GEMM: 0 off, 1 where it measured faster, 2 forced (gemm_stream.h)
         gemm.set_stream_gemm(v)
     elif switch == "argmax_split":

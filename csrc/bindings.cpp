@@ -55,7 +55,8 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"),
      py::arg("norm"), py::arg("colsum"), py::arg("eps"), py::arg("st"), py::arg("wsh") = 0, py::arg("ws") = 0,
      py::arg("ws_bytes") = 0);
-  m.def("gemm_set_stream", [](int on, long long min_bytes) { return dnn_gemm_set_stream(on, min_bytes); });
+  m.def("gemm_set_stream", [](int on, long long min_bytes, int fold) { return dnn_gemm_set_stream(on, min_bytes, fold); },
+        py::arg("on"), py::arg("min_bytes"), py::arg("fold") = -1);
   m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 sw, u64 C, int ldc, int M, int N, int K, int nt,
                                 int u, int ks, int pipe, int w8, u64 st) {
     return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, M, N, K, nt, u, ks, pipe, w8, ST(st));

@@ -37,8 +37,9 @@ int dnn_gemm_skinny_w8(const void* A, int lda, const void* W, int ldw, const flo
 int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int ldw, const float* sw, void* C, int ldc,
                     const float* bias, const void* R, int ldr, int M, int N, int K, int act, int out_f32, int fp8,
                     hipStream_t st, const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0);
-// decode stream GEMM (gemm_stream.h) switch: on/off, and the weight-byte threshold (<= 0 keeps it)
-int dnn_gemm_set_stream(int on, long long min_bytes);
+// decode stream GEMM (gemm_stream.h) switch: 0 off / 1 auto / 2 forced, the weight-byte threshold (<= 0
+// keeps it), and the in-launch split-K combine (fold: 1 on, 0 reduce launch, -1 keep)
+int dnn_gemm_set_stream(int on, long long min_bytes, int fold = -1);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);

@@ -366,6 +366,8 @@ constexpr int SKINNY_MAX_M = 256;  // M > 64 only through the M split (medium-ba
 // weights of >= g_stream_min_bytes; narrow N splits K across workgroups into
 // the caller's workspace (no workspace: one slice).
 static int g_stream_on = 1;  // 0 off, 1 where it measured faster, 2 forced (tests)
+static int g_stream_fold = 0;  // 1: split-K combine inside the launch (last arriver); measured 4.08 -> 4.20 ms (profiles/r3_fold_decode_ab.jsonl)
+static constexpr long long STREAM_CNT_BYTES = 4096;  // tile tickets at the end of the workspace (zeroed once)
 static long long g_stream_min_bytes = 8ll << 20;
 
 // K-split plan: ntiles x splitk workgroups, cps chunks per slice.  Returns
@@ -386,7 +388,9 @@ static bool stream_plan(int MP, int N, int kbytes, bool have_ws, long long ws_by
   if (ntiles < STREAM_MIN_WGS && have_ws) {
     const int by_steps = g_stream_on == 2 ? steps : max(1, steps / STREAM_MIN_STEPS);  // forced: split anything
     splitk = min(min((256 + ntiles - 1) / ntiles, STREAM_MAX_SPLIT), by_steps);
-    auto need = [&](int sk) { return (long long)sk * MP * ntiles * BN * 4 + (long long)sk * MP * 2 * 4; };
+    auto need = [&](int sk) {
+      return (long long)sk * MP * ntiles * BN * 4 + (long long)ntiles * sk * MP * 2 * 4 + STREAM_CNT_BYTES;
+    };
     while (splitk > 1 && need(splitk) > ws_bytes) --splitk;
   }
   cps = (steps + splitk - 1) / splitk * CS;
@@ -399,7 +403,8 @@ static bool stream_plan(int MP, int N, int kbytes, bool have_ws, long long ws_by
 template <int ACT, int NORM, bool W8, int MT>
 static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
                             const float* bias, const void* R, int ldr, int M, int N, int kbytes,
-                            const float* colsum, float eps, hipStream_t st, void* ws, int splitk, int cps) {
+                            const float* colsum, float eps, hipStream_t st, void* ws, long long ws_bytes, int splitk,
+                            int cps) {
   constexpr int NT = STREAM_NT, BN = 64 * NT, MP = MT * 16;
   const int ntiles = (N + BN - 1) / BN, nch = kbytes / 64;
   const int kelems = W8 ? kbytes : kbytes / 2;
@@ -407,12 +412,19 @@ static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const flo
   if (splitk == 1) {
     hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, W8, NORM, ACT, false>), grid, block, 0, st, (const uint8_t*)A,
                        lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch, cps, colsum,
-                       eps, kelems, (float*)nullptr);
+                       eps, kelems, (float*)nullptr, (unsigned*)nullptr);
+    return (int)hipGetLastError();
+  }
+  if (g_stream_fold) {
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + ws_bytes - STREAM_CNT_BYTES);
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, W8, NORM, ACT, true, true>), grid, block, 0, st, (const uint8_t*)A,
+                       lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch, cps, colsum,
+                       eps, kelems, (float*)ws, cnt);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, W8, NORM, ACT, true>), grid, block, 0, st, (const uint8_t*)A, lda_b,
                      (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch, cps, colsum, eps, kelems,
-                     (float*)ws);
+                     (float*)ws, (unsigned*)nullptr);
   const int NO = ACT == ACT_SILU_MUL ? N / 2 : N;
   const long long threads = (long long)M * ((NO + 3) / 4);
   hipLaunchKernelGGL((gemm_stream_reduce<ACT, NORM, W8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
@@ -428,8 +440,9 @@ static bool stream_eligible(const void* A, int lda_b, const void* Wsh, int M, in
   return (long long)((N + 15) / 16 * 16) * kbytes >= g_stream_min_bytes;
 }
 
-extern "C" int dnn_gemm_set_stream(int on, long long min_bytes) {
+extern "C" int dnn_gemm_set_stream(int on, long long min_bytes, int fold) {
   g_stream_on = on;
+  if (fold >= 0) g_stream_fold = fold;
   if (min_bytes > 0) g_stream_min_bytes = min_bytes;
   return 0;
 }
@@ -471,9 +484,9 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
         stream_plan<W8>(M <= 32 ? 32 : 64, N, kbytes, ws != nullptr, ws_bytes, splitk, cps)) {
       if (M <= 32)
         return launch_stream_mt<ACT, NORM, W8, 2>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps,
-                                                  st, ws, splitk, cps);
+                                                  st, ws, ws_bytes, splitk, cps);
       return launch_stream_mt<ACT, NORM, W8, 4>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps,
-                                                st, ws, splitk, cps);
+                                                st, ws, ws_bytes, splitk, cps);
     }
   }
   const bool wide = N >= 16384;

@@ -55,14 +55,141 @@ __device__ __forceinline__ void str_stats(const bf16x8& a, float c, float& s1, f
   }
 }
 
-template <int MT, int NT, bool W8, int NORM, int ACT, bool SPLIT>
+// Write-through (sc1) stores and L1-bypassing (sc1) loads of split-K partials:
+// relaxed agent-scope 8-byte atomics on global (addrspace 1) pointers lower to
+// global_store_dwordx2 sc1 / global_load_dwordx2 sc1 (MI355X_MICROARCH.md,
+// visibility: the forms that need no release / acquire fence).
+typedef GLB_AS unsigned long long gu64_t;
+__device__ __forceinline__ void str_store_sc1(float* p, const f32x4& v) {
+  gu64_t* q = (gu64_t*)(p);  // C-style: an address-space cast (flat -> global)
+  __hip_atomic_store(q, __builtin_bit_cast(unsigned long long, f32x2{v[0], v[1]}), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, __builtin_bit_cast(unsigned long long, f32x2{v[2], v[3]}), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void str_store_sc1_2(float* p, float a, float b) {
+  __hip_atomic_store((gu64_t*)(p),
+                     __builtin_bit_cast(unsigned long long, f32x2{a, b}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC1>
+__device__ __forceinline__ f32x2 str_load2(const float* p) {
+  if constexpr (SC1) {
+    const unsigned long long x = __hip_atomic_load((gu64_t*)(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_bit_cast(f32x2, x);
+  } else {
+    return *reinterpret_cast<const f32x2*>(p);
+  }
+}
+
+constexpr int STR_MAX_SPLIT = 16;
+
+// Row statistics (mean, rstd) of row m from the per-slice partial sums of
+// (tile `tile`'s copy in) the statistics region.
+template <int NORM, bool SC1>
+__device__ __forceinline__ void str_row_norm(const float* st, int splitk, int MP, int tile, int m,
+                                             const uint8_t* __restrict__ A, int lda_b, int kelems, float eps,
+                                             float& mean, float& rstd) {
+  float a = 0.f, q = 0.f;
+  for (int s = 0; s < splitk; ++s) {
+    const f32x2 v = str_load2<SC1>(st + (((size_t)tile * splitk + s) * MP + m) * 2);
+    a += v[0];
+    q += v[1];
+  }
+  const float invk = 1.f / (float)kelems, d = a * invk;
+  const float sh = NORM == 2 ? bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)m * lda_b)) : 0.f;
+  mean = NORM == 2 ? sh + d : 0.f;
+  const float var = NORM == 2 ? fmaxf(q * invk - d * d, 0.f) : q * invk;
+  rstd = rsqrtf(var + eps);
+}
+
+// Sum of the splitk partials of outputs (m, n..n+3): every slice's partial is
+// loaded before the first add (surplus loads clamped to the last slice and
+// weighted 0): one memory round trip, not splitk dependent ones.  Then the fp8
+// channel scale and the folded norm.
+template <int NORM, bool W8, bool SC1>
+__device__ __forceinline__ f32x4 str_combine4(const float* slab, int splitk, int MP, int Ns, int m, int n, int N,
+                                              const float* __restrict__ sw, const float* __restrict__ colsum,
+                                              float mean, float rstd) {
+  f32x2 part[STR_MAX_SPLIT][2];
+#pragma unroll
+  for (int s = 0; s < STR_MAX_SPLIT; ++s) {
+    const float* p = slab + ((size_t)min(s, splitk - 1) * MP + m) * Ns + n;
+    part[s][0] = str_load2<SC1>(p);
+    part[s][1] = str_load2<SC1>(p + 2);
+  }
+  f32x4 v = f32x4{part[0][0][0], part[0][0][1], part[0][1][0], part[0][1][1]};
+#pragma unroll
+  for (int s = 1; s < STR_MAX_SPLIT; ++s) {
+    const float w = s < splitk ? 1.f : 0.f;
+    v += f32x4{part[s][0][0], part[s][0][1], part[s][1][0], part[s][1][1]} * w;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool ok = n + r < N;
+    if constexpr (W8) v[r] *= ok ? sw[n + r] : 0.f;
+    if constexpr (NORM == 2) v[r] = rstd * (v[r] - mean * (ok ? colsum[n + r] : 0.f));
+    if constexpr (NORM == 1) v[r] *= rstd;
+  }
+  return v;
+}
+
+// Combine + epilogue of output items (row m, 4 output columns o): packed
+// gate|up (SiLU-mul) pairs gate columns 16g+w.. with up columns 16g+8+w.
+template <int ACT, int NORM, bool W8, bool SC1>
+__device__ __forceinline__ void str_combine_item(const float* slab, int splitk, int MP, int Ns, int tile, int m, int o,
+                                                 const uint8_t* __restrict__ A, int lda_b,
+                                                 const float* __restrict__ sw, const float* __restrict__ colsum,
+                                                 float eps, int kelems, void* __restrict__ Cv, int ldc,
+                                                 const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
+                                                 int M, int N) {
+  float mean = 0.f, rstd = 1.f;
+  if constexpr (NORM != 0)
+    str_row_norm<NORM, SC1>(slab + (size_t)splitk * MP * Ns, splitk, MP, tile, m, A, lda_b, kelems, eps, mean, rstd);
+  if constexpr (ACT == ACT_SILU_MUL) {
+    const int NO = N / 2;
+    if (o >= NO) return;
+    const int g = o >> 3, w = o & 7;
+    const f32x4 gt = str_combine4<NORM, W8, SC1>(slab, splitk, MP, Ns, m, g * 16 + w, N, sw, colsum, mean, rstd);
+    const f32x4 up = str_combine4<NORM, W8, SC1>(slab, splitk, MP, Ns, m, g * 16 + 8 + w, N, sw, colsum, mean, rstd);
+    bf16_t* C = reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (o + r < NO) C[r] = f2bf(silu(gt[r]) * up[r]);
+  } else {
+    if (o >= N) return;
+    epi_t4<ACT, false>(str_combine4<NORM, W8, SC1>(slab, splitk, MP, Ns, m, o, N, sw, colsum, mean, rstd), m, o, M,
+                       N, Cv, ldc, bias, R, ldr, epi_vec_ok(Cv, ldc, bias, R, ldr));
+  }
+}
+
+// The last-arriving workgroup of tile `tile` combines its MP x BN outputs.
+template <int ACT, int NORM, bool W8, bool SC1>
+__device__ __forceinline__ void str_combine_tile(const float* slab, int splitk, int MP, int Ns, int tile, int BN,
+                                                 const uint8_t* __restrict__ A, int lda_b,
+                                                 const float* __restrict__ sw, const float* __restrict__ colsum,
+                                                 float eps, int kelems, void* __restrict__ Cv, int ldc,
+                                                 const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
+                                                 int M, int N, int tid) {
+  const int per_row = (ACT == ACT_SILU_MUL ? BN / 2 : BN) / 4;
+  const int o0 = (ACT == ACT_SILU_MUL ? tile * BN / 2 : tile * BN);
+  for (int i = tid; i < MP * per_row; i += 256) {
+    const int m = i / per_row, o = o0 + (i - m * per_row) * 4;
+    if (m < M)
+      str_combine_item<ACT, NORM, W8, SC1>(slab, splitk, MP, Ns, tile, m, o, A, lda_b, sw, colsum, eps, kelems, Cv, ldc,
+                                           bias, R, ldr, M, N);
+  }
+}
+
+template <int MT, int NT, bool W8, int NORM, int ACT, bool SPLIT, bool FOLD = false>
 __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                              const uint8_t* __restrict__ Wsh,
                                                              const float* __restrict__ sw, void* __restrict__ Cv,
                                                              int ldc, const float* __restrict__ bias,
                                                              const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                              int nch, int cps, const float* __restrict__ colsum,
-                                                             float eps, int kelems, float* __restrict__ slab) {
+                                                             float eps, int kelems, float* __restrict__ slab,
+                                                             unsigned* __restrict__ cnt = nullptr) {
   using Cfg = StrCfg<W8>;
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
@@ -259,7 +386,7 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __re
 
   if constexpr (SPLIT) {
     // fp32 partials of this K slice: slab[slice][m][n] (Ns = ntiles * BN
-    // columns), statistics after the slabs: [splitk][MP][2]
+    // columns), then the row statistics per (tile, slice): [ntiles][splitk][MP][2]
     const int Ns = ntiles * BN;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -267,15 +394,46 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __re
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const int m = 16 * t + fr;
-        *reinterpret_cast<f32x4*>(slab + ((size_t)slice * MP + m) * Ns + n) = acc[j][t];
+        float* dst = slab + ((size_t)slice * MP + m) * Ns + n;
+        if constexpr (FOLD) {
+          str_store_sc1(dst, acc[j][t]);
+        } else {
+          *reinterpret_cast<f32x4*>(dst) = acc[j][t];
+        }
       }
     }
     if constexpr (NORM != 0) {
-      if (tile == 0 && wave < MT && lane < 16) {
-        float* st = slab + (size_t)splitk * MP * Ns;
-        st[((size_t)slice * MP + 16 * wave + lane) * 2 + 0] = s1;
-        st[((size_t)slice * MP + 16 * wave + lane) * 2 + 1] = s2;
+      if (wave < MT && lane < 16) {
+        float* st = slab + (size_t)splitk * MP * Ns + (((size_t)tile * splitk + slice) * MP + 16 * wave + lane) * 2;
+        if constexpr (FOLD) {
+          str_store_sc1_2(st, s1, s2);
+        } else {
+          st[0] = s1;
+          st[1] = s2;
+        }
       }
+    }
+    if constexpr (FOLD) {
+      // In-launch split-K combine (guide §5 'Projection GEMM at M = 256' item
+      // 2, write-through form; MI355X_MICROARCH.md visibility table row 1):
+      // partials stored sc1 and drained by every storing wave, a workgroup
+      // barrier, ONE lane's relaxed agent-scope ticket add; the workgroup that
+      // draws splitk - 1 combines the tile, reading every partial with sc1
+      // loads only (no acquire fence), and re-arms the ticket for the next call
+      // (the counters start zeroed: ops/gemm.py decode_workspace).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      unsigned* last_flag = reinterpret_cast<unsigned*>(st_lds);
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = old == (unsigned)splitk - 1;
+        if (last) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag[0] = last ? 1u : 0u;
+      }
+      __syncthreads();
+      if (last_flag[0] == 0) return;
+      str_combine_tile<ACT, NORM, W8, true>(slab, splitk, MP, Ns, tile, BN, A, lda_b, sw, colsum, eps, kelems, Cv, ldc,
+                                            bias, R, ldr, M, N, tid);
     }
     return;
   } else {
@@ -328,12 +486,8 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __re
   }
 }
 
-// Split-K combine + epilogue: one thread per (row, 4 output columns).  Every
-// slice's partial is loaded before the first add (splitk <= STR_MAX_SPLIT,
-// surplus loads clamped to the last slice and weighted 0): one memory round
-// trip, not splitk dependent ones.
-constexpr int STR_MAX_SPLIT = 16;
-
+// Split-K combine + epilogue as its own launch (no workspace counters, or the
+// fold switched off): one thread per (row, 4 output columns).
 template <int ACT, int NORM, bool W8>
 __global__ __launch_bounds__(256) void gemm_stream_reduce(const float* __restrict__ slab, int splitk, int MP, int Ns,
                                                           const uint8_t* __restrict__ A, int lda_b,
@@ -347,50 +501,8 @@ __global__ __launch_bounds__(256) void gemm_stream_reduce(const float* __restric
   const int idx = blockIdx.x * 256 + threadIdx.x;
   const int m = idx / per_row, o = (idx - m * per_row) * 4;
   if (m >= M) return;
-  float rstd = 1.f, mean = 0.f;
-  if constexpr (NORM != 0) {
-    const float* st = slab + (size_t)splitk * MP * Ns;
-    float a = 0.f, q = 0.f;
-    for (int s = 0; s < splitk; ++s) {
-      a += st[((size_t)s * MP + m) * 2 + 0];
-      q += st[((size_t)s * MP + m) * 2 + 1];
-    }
-    const float invk = 1.f / (float)kelems, d = a * invk;
-    const float sh = NORM == 2 ? bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)m * lda_b)) : 0.f;
-    mean = NORM == 2 ? sh + d : 0.f;
-    const float var = NORM == 2 ? fmaxf(q * invk - d * d, 0.f) : q * invk;
-    rstd = rsqrtf(var + eps);
-  }
-  auto col = [&](int n) {  // combined, scaled, normalised accumulator of 4 columns n..n+3
-    f32x4 part[STR_MAX_SPLIT];
-#pragma unroll
-    for (int s = 0; s < STR_MAX_SPLIT; ++s)
-      part[s] = *reinterpret_cast<const f32x4*>(slab + ((size_t)min(s, splitk - 1) * MP + m) * Ns + n);
-    f32x4 v = part[0];
-#pragma unroll
-    for (int s = 1; s < STR_MAX_SPLIT; ++s) v += part[s] * (s < splitk ? 1.f : 0.f);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = n + r < N;
-      if constexpr (W8) v[r] *= ok ? sw[n + r] : 0.f;
-      if constexpr (NORM == 2) v[r] = rstd * (v[r] - mean * (ok ? colsum[n + r] : 0.f));
-      if constexpr (NORM == 1) v[r] *= rstd;
-    }
-    return v;
-  };
-  if constexpr (ACT == ACT_SILU_MUL) {
-    // packed gate|up: 16-column groups of 8 gate then the 8 matching up columns
-    if (o >= NO) return;
-    const int g = o >> 3, w = o & 7;
-    const f32x4 gt = col(g * 16 + w), up = col(g * 16 + 8 + w);
-    bf16_t* C = reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (o + r < NO) C[r] = f2bf(silu(gt[r]) * up[r]);
-  } else {
-    if (o >= N) return;
-    epi_t4<ACT, false>(col(o), m, o, M, N, Cv, ldc, bias, R, ldr, epi_vec_ok(Cv, ldc, bias, R, ldr));
-  }
+  str_combine_item<ACT, NORM, W8, false>(slab, splitk, MP, Ns, 0, m, o, A, lda_b, sw, colsum, eps, kelems, Cv, ldc,
+                                         bias, R, ldr, M, N);
 }
 
 }  // namespace dnn

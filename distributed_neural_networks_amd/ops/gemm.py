@@ -50,15 +50,21 @@ def decode_workspace(device, slot: int = 0) -> torch.Tensor:
     key = (str(device), slot)
     t = _decode_ws.get(key)
     if t is None:
-        t = _decode_ws[key] = torch.empty(DECODE_WS_BYTES, dtype=torch.uint8, device=device)
+        # zeroed: its last 4 KiB are the stream kernel's split-K tickets, which
+        # every launch leaves at zero again (gemm_stream.h, in-launch combine)
+        t = _decode_ws[key] = torch.zeros(DECODE_WS_BYTES, dtype=torch.uint8, device=device)
     return t
 
 
-def set_stream_gemm(on: int = 1, min_bytes: int = 0) -> None:
+def set_stream_gemm(on: int = 1, min_bytes: int = 0, fold: int = -1) -> None:
     """Decode stream GEMM: 0 off, 1 on where it measured faster (default), 2
     forced on every eligible shape (tests); ``min_bytes`` = weight-byte
-    threshold (0 keeps it)."""
-    check(lib().gemm_set_stream(int(on), int(min_bytes)), "gemm_set_stream")
+    threshold (0 keeps it); ``fold`` = split-K combine inside the launch by
+    the last-arriving workgroup of a tile (1) or as a separate reduce launch
+    (0, default: the fold measured 4.08 -> 4.20 ms/step on Llama-3 8B B=32,
+    profiles/r3_fold_decode_ab.jsonl — one workgroup per tile serialises the
+    combine that the reduce launch spreads over the chip), -1 keeps it."""
+    check(lib().gemm_set_stream(int(on), int(min_bytes), int(fold)), "gemm_set_stream")
 
 
 def _ws_args(ws: Optional[torch.Tensor]):

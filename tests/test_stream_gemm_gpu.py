@@ -18,12 +18,14 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.fixture
-def force_stream():
+@pytest.fixture(params=[1, 0], ids=["fold", "reduce"])
+def force_stream(request):
+    """Forced stream kernel on every eligible shape, however small, split or
+    not; split-K combined in the launch (fold) or by the reduce launch."""
     from distributed_neural_networks_amd.ops.gemm import set_stream_gemm
-    set_stream_gemm(2, 1)  # forced: every eligible shape, however small, split or not
+    set_stream_gemm(2, 1, request.param)
     yield
-    set_stream_gemm(1, 8 << 20)
+    set_stream_gemm(1, 8 << 20, 0)
 
 
 @pytest.mark.parametrize("M", [17, 32, 48, 64])
@@ -140,3 +142,42 @@ def test_stream_matches_skinny_kernel_decode_shapes():
         torch.cuda.synchronize()
         ref = x.float() @ W.float().t()
         assert _rel(outs[0], ref) < 1e-2 and _rel(outs[0], outs[1]) < 1e-2
+
+
+@pytest.mark.parametrize("norm", [0, 1, 2])
+def test_stream_fold_matches_reduce_launch(norm):
+    """The in-launch split-K combine (last-arriving workgroup per tile, sc1
+    hand-off, self-re-arming tickets) gives bit-identical outputs to the
+    separate reduce launch, call after call (the tickets must return to zero
+    every launch, including when calls alternate between the two forms and
+    between shapes with different slice counts)."""
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
+                                                          linear_norm, set_stream_gemm, shuffle_weight)
+    torch.manual_seed(norm)
+    ws = decode_workspace(DEV, 5)
+    outs = {0: [], 1: []}
+    try:
+        for it in range(3):
+            for fold in (1, 0):
+                set_stream_gemm(2, 1, fold)
+                for (M, N, K) in ((32, 4096, 4096), (64, 1536, 2048)):
+                    g = torch.Generator(device=DEV).manual_seed(N + it)
+                    x = (torch.randn(M, K, device=DEV, generator=g) + 1).bfloat16()
+                    W = torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)
+                    o = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+                    if norm:
+                        gamma = torch.rand(K, device=DEV, generator=g) + 0.5
+                        f = attach_shuffled(fold_norm(W, gamma, None, None, norm == 1, 1e-5, DEV))
+                        linear_norm(x, f, out=o, ws=ws)
+                    else:
+                        Wb = W.bfloat16()
+                        R = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+                        linear(x, Wb, residual=R, out=o, w_shuf=shuffle_weight(Wb), ws=ws)
+                    outs[fold].append(o)
+        torch.cuda.synchronize()
+    finally:
+        set_stream_gemm(1, 8 << 20, 0)
+    for a, b in zip(outs[1], outs[0]):
+        assert torch.equal(a, b)
+    tickets = ws[-4096:].view(torch.int32)
+    assert int(tickets.abs().sum()) == 0  # every ticket re-armed
