@@ -5,10 +5,15 @@
 // `import torch`), never against torch's C++ ABI. Every entry returns the HIP
 // error code of the launch; the Python wrappers raise on non-zero.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 #include "kernels/api.h"
+#include "comm/p2p.h"
+
+#include <string>
+#include <vector>
 
 namespace py = pybind11;
 #define P(x) reinterpret_cast<void*>(static_cast<uintptr_t>(x))
@@ -164,4 +169,49 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_fp8(CP(A), CFP(sa), CP(W), CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, ST(st));
   });
 #endif
+
+  // ---- native RCCL data plane (csrc/comm/p2p.cpp) ----
+  m.def("comm_available", []() { return dnn_comm_available(); });
+  m.def("comm_last_error", []() { return std::string(dnn_comm_last_error()); });
+  m.def("comm_unique_id", []() {
+    char id[128];
+    if (dnn_comm_unique_id(id) != 0) throw std::runtime_error(dnn_comm_last_error());
+    return py::bytes(id, 128);
+  });
+  m.def("comm_create", [](py::bytes id, int nranks, int rank, int device, int async) {
+    std::string s = id;
+    if (s.size() != 128) throw std::runtime_error("comm_create: the unique id must be 128 bytes");
+    long long h;
+    {
+      py::gil_scoped_release nogil;
+      h = dnn_comm_create(s.data(), nranks, rank, device, async);
+    }
+    if (h == 0) throw std::runtime_error(dnn_comm_last_error());
+    return h;
+  });
+  m.def("comm_wait_ready", [](long long h, int timeout_ms) { return dnn_comm_wait_ready(h, timeout_ms); },
+        py::call_guard<py::gil_scoped_release>());
+  m.def("comm_post", [](long long h, int kind, u64 ptr, long long bytes, int peer, u64 st, int on_stream) {
+    return dnn_comm_post(h, kind, P(ptr), bytes, peer, ST(st), on_stream);
+  });
+  m.def("comm_group", [](long long h, std::vector<int> kinds, std::vector<u64> ptrs, std::vector<long long> bytes,
+                         std::vector<int> peers, u64 st, int on_stream) {
+    const size_t n = kinds.size();
+    if (ptrs.size() != n || bytes.size() != n || peers.size() != n) throw std::runtime_error("comm_group: ragged op lists");
+    std::vector<void*> p(n);
+    for (size_t i = 0; i < n; ++i) p[i] = P(ptrs[i]);
+    return dnn_comm_group(h, (int)n, kinds.data(), p.data(), bytes.data(), peers.data(), ST(st), on_stream);
+  });
+  m.def("comm_wait", [](long long h, long long tok, u64 st) { return dnn_comm_wait(h, tok, ST(st)); });
+  m.def("comm_query", [](long long h, long long tok) { return dnn_comm_query(h, tok); });
+  m.def("comm_sync", [](long long h, long long tok, int timeout_ms) { return dnn_comm_sync(h, tok, timeout_ms); },
+        py::call_guard<py::gil_scoped_release>());
+  m.def("comm_async_error", [](long long h) { return dnn_comm_async_error(h); });
+  m.def("comm_abort", [](long long h) { return dnn_comm_abort(h); }, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_destroy", [](long long h) { return dnn_comm_destroy(h); }, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_stats", [](long long h) {
+    long long o[4] = {0, 0, 0, 0};
+    dnn_comm_stats(h, o);
+    return py::make_tuple(o[0], o[1], o[2], o[3]);
+  });
 }

@@ -39,7 +39,8 @@ def _hipcc() -> str:
 
 
 def sources() -> List[str]:
-    return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]
+    return (sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+            + [os.path.join(CSRC, "bindings.cpp")])
 
 
 def _flags(src: str) -> List[str]:

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 from dataclasses import dataclass
 from typing import Optional
 
@@ -109,5 +110,8 @@ def barrier(info: DistInfo) -> None:
 def shutdown() -> None:
     global _BACK_GROUP
     _BACK_GROUP = None
+    rccl = sys.modules.get(__package__ + ".rccl")
+    if rccl is not None:  # native RCCL channels (parallel/rccl.py) go before the store they were bootstrapped from
+        rccl.destroy_all()
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -23,6 +23,7 @@ move payloads without headers.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -176,12 +177,66 @@ class _HostWork:
         return True
 
 
+class RcclLink(P2PLink):
+    """A hop over this package's own RCCL channel (``parallel/rccl.py``,
+    ``csrc/comm/p2p.cpp``): the default link between GPU stages.  Same
+    contract as ``P2PLink`` — ``isend``/``irecv`` are ordered after the work
+    queued on the current stream when posted, their ``wait()`` orders the
+    current stream after the transfer without blocking the host — plus
+    ``send_on_stream``/``recv_on_stream``, which enqueue the hop on the
+    current stream itself (a HIP graph can capture it with the stage's
+    kernels).  The pair's channel is opened (init started) at construction."""
+
+    def __init__(self, peer: int, device: torch.device, group=None):
+        super().__init__(peer, device, group)
+        from . import rccl
+        me = dist.get_rank()
+        self.ch = rccl.pair_channel(me, self.peer, device, rccl.group_tag(group))
+        self.pi = 1 if self.peer > me else 0  # the peer's rank inside the pair channel
+
+    def isend(self, t: torch.Tensor):
+        from .rccl import SEND, Work
+        if not t.is_contiguous():
+            raise ValueError("RcclLink.isend needs a contiguous tensor")
+        self._count_send(t)
+        return Work(self.ch, self.ch.post(SEND, t, self.pi))
+
+    def irecv(self, out: torch.Tensor):
+        from .rccl import RECV, Work
+        self._count_recv(out)
+        return Work(self.ch, self.ch.post(RECV, out, self.pi))
+
+    def send_on_stream(self, t: torch.Tensor) -> None:
+        from .rccl import SEND
+        self._count_send(t)
+        self.ch.post(SEND, t, self.pi, on_stream=True)
+
+    def recv_on_stream(self, out: torch.Tensor) -> None:
+        from .rccl import RECV
+        self._count_recv(out)
+        self.ch.post(RECV, out, self.pi, on_stream=True)
+
+
+def p2p_mode() -> str:
+    """``DNN_P2P``: ``native`` (default: ``RcclLink``) or ``torch``
+    (ProcessGroupNCCL isend/irecv) for RCCL stage hops."""
+    mode = os.environ.get("DNN_P2P", "native")
+    if mode not in ("native", "torch"):
+        raise ValueError(f"DNN_P2P must be native or torch, got {mode!r}")
+    return mode
+
+
 def make_link(peer: int, device: torch.device, group=None) -> P2PLink:
-    """The link for this process's backend: RCCL / gloo-on-CPU move the tensor
-    itself (``P2PLink``); gloo with a GPU stage stages through pinned host
-    memory (``HostStagedLink``)."""
-    if device.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "gloo":
-        return HostStagedLink(peer, device, group)
+    """The link for this process's backend: GPU stages on RCCL use the native
+    channel (``RcclLink``; ``DNN_P2P=torch``: ProcessGroupNCCL's P2P), gloo on
+    CPU moves the tensor itself (``P2PLink``), gloo with a GPU stage stages
+    through pinned host memory (``HostStagedLink``)."""
+    if device.type == "cuda" and dist.is_initialized():
+        backend = dist.get_backend(group)
+        if backend == "gloo":
+            return HostStagedLink(peer, device, group)
+        if backend == "nccl" and p2p_mode() == "native":
+            return RcclLink(peer, device, group)
     return P2PLink(peer, device, group)
 
 

@@ -67,6 +67,9 @@ class Watchdog:
         # abort() from the schedule and the thread's own poll can both fire
         if self._exited.acquire(blocking=False):
             self._stop.set()
+            rccl = sys.modules.get(__package__ + ".rccl")
+            if rccl is not None:  # native channels: in-flight P2P kernels return before the process goes
+                rccl.abort_all()
             self.exit_fn(EXIT_ABORT)
 
     # -- called from the schedule (cheap) -----------------------------------
