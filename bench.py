@@ -109,6 +109,9 @@ def stages_for(device, cut: int = 1, precision: str = "fp32"):
     if device.type == "cpu":  # schedule-test mode only (never used for a reported number)
         return (TorchStage("cifar10", sd0, 0, cut, True, False, device),
                 TorchStage("cifar10", sd1, cut + 1, 3, False, True, device))
+    # plain fp32 boundary: the blocked hi/lo encoding (ops/cifar.py) measured
+    # neutral end to end (profiles/r3_boundary_ab.jsonl: fc1 -0.08 ms, the
+    # stage-0 epilogue +0.09 ms)
     return CifarHipStage(sd0, 0, cut, device, precision), CifarHipStage(sd1, cut + 1, 3, device, precision)
 
 
@@ -576,7 +579,7 @@ def main():
                                      2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},
         }
         if info.device.type == "cuda" and args.precision == "fp32":
-            out.update(precision_check(info.device, args.precision))
+            out.update(precision_check(info.device, args.precision, 16384))
         out.update(extra)
     if N > 1 and not args.no_extra:
         multi_gpu_extras(args, info, out)

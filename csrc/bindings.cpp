@@ -88,17 +88,23 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("cifar_set_v4_pt", [](int pt) { return dnn_cifar_set_v4_pt(pt); });
   m.def("cifar_stage0_x3", [](u64 x, u64 out, u64 w1h, u64 w1l, u64 b1, u64 w2h, u64 w2l, u64 b2, int B, int grid,
-                              u64 st) {
+                              u64 st, int split_out) {
     return dnn_cifar_stage0_x3(CFP(x), FP(out), CP(w1h), CP(w1l), CFP(b1), CP(w2h), CP(w2l), CFP(b2), B, grid,
-                               ST(st));
-  });
+                               ST(st), split_out);
+  }, py::arg("x"), py::arg("out"), py::arg("w1h"), py::arg("w1l"), py::arg("b1"), py::arg("w2h"), py::arg("w2l"),
+        py::arg("b2"), py::arg("B"), py::arg("grid"), py::arg("st"), py::arg("split_out") = 0);
   m.def("cifar_s0_set_wide_store", [](int on) { return dnn_cifar_s0_set_wide_store(on); });
-  m.def("cifar_split3", [](u64 a, int lda, u64 o, int ldo, int M, int K, u64 st) {
-    return dnn_cifar_split3(CFP(a), lda, P(o), ldo, M, K, ST(st));
-  });
+  m.def("cifar_split3", [](u64 a, int lda, u64 o, int ldo, int M, int K, u64 st, int blocked) {
+    return dnn_cifar_split3(CFP(a), lda, P(o), ldo, M, K, ST(st), blocked);
+  }, py::arg("a"), py::arg("lda"), py::arg("o"), py::arg("ldo"), py::arg("M"), py::arg("K"), py::arg("st"),
+        py::arg("blocked") = 0);
   m.def("cifar_fc1_x3", [](u64 a, int lda, u64 wh, u64 wl, int ldw, u64 bias, u64 c, int ldc, int M, int N, int K,
-                           u64 st) {
-    return dnn_cifar_fc1_x3(CFP(a), lda, CP(wh), CP(wl), ldw, CFP(bias), FP(c), ldc, M, N, K, ST(st));
+                           u64 st, int a_split) {
+    return dnn_cifar_fc1_x3(CFP(a), lda, CP(wh), CP(wl), ldw, CFP(bias), FP(c), ldc, M, N, K, ST(st), a_split);
+  }, py::arg("a"), py::arg("lda"), py::arg("wh"), py::arg("wl"), py::arg("ldw"), py::arg("bias"), py::arg("c"),
+        py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("st"), py::arg("a_split") = 0);
+  m.def("cifar_split_blocked", [](u64 a, u64 o, int M, int K, int dir, u64 st) {
+    return dnn_cifar_split_blocked(CFP(a), FP(o), M, K, dir, ST(st));
   });
   m.def("cifar_head_tail_x3", [](u64 hid, u64 w2h, u64 w2l, u64 b2, u64 probs, u64 pred, int B, u64 st) {
     return dnn_cifar_head_tail_x3(CFP(hid), CP(w2h), CP(w2l), CFP(b2), FP(probs), IP(pred), B, ST(st));

@@ -45,11 +45,12 @@ int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float*
                         int B, int grid, hipStream_t st);
 int dnn_cifar_set_v4_pt(int pt);
 int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, const void* w1l, const float* b1, const void* w2h,
-                        const void* w2l, const float* b2, int B, int grid, hipStream_t st);
+                        const void* w2l, const float* b2, int B, int grid, hipStream_t st, int split_out = 0);
 int dnn_cifar_s0_set_wide_store(int on);
-int dnn_cifar_split3(const float* a, int lda, void* o, int ldo, int M, int K, hipStream_t st);
+int dnn_cifar_split3(const float* a, int lda, void* o, int ldo, int M, int K, hipStream_t st, int blocked = 0);
 int dnn_cifar_fc1_x3(const float* A, int lda, const void* Wh, const void* Wl, int ldw, const float* bias, float* C,
-                     int ldc, int M, int N, int K, hipStream_t st);
+                     int ldc, int M, int N, int K, hipStream_t st, int a_split = 0);
+int dnn_cifar_split_blocked(const float* a, float* o, int M, int K, int dir, hipStream_t st);
 int dnn_cifar_head_tail_x3(const float* hid, const void* w2h, const void* w2l, const float* b2, float* probs, int* pred,
                            int B, hipStream_t st);
 int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,

@@ -109,7 +109,9 @@ __device__ __forceinline__ void resident_fence(const bf16x8 (&w)[N]) {
 
 using namespace x3;
 
-template <bool WIDE>
+// SPLIT_OUT: the boundary leaves in the blocked hi/lo encoding
+// (cifar_split_blocked_kernel) that cifar_fc1_x3_kernel<true> stages by DMA.
+template <bool WIDE, bool SPLIT_OUT>
 __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
     const float* __restrict__ x, float* __restrict__ out, const bf16_t* __restrict__ w1h,
     const bf16_t* __restrict__ w1l, const float* __restrict__ b1, const bf16_t* __restrict__ w2h,
@@ -315,7 +317,16 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
             const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][1]), __float_as_uint(v[1][1]), false,
                                                              false);
             const int PY = 2 * ty2 + qy;
-            *reinterpret_cast<uint4*>(ob + PY * 8 + 4 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+            if constexpr (SPLIT_OUT) {  // k = oc2*64 + PY*8 + 4h + 0..3: one 8-B hi and one 8-B lo store
+              uint2 hi, lo;
+              split2(__uint_as_float(sx[0]), __uint_as_float(sy[0]), hi.x, lo.x);
+              split2(__uint_as_float(sx[1]), __uint_as_float(sy[1]), hi.y, lo.y);
+              char* bp = reinterpret_cast<char*>(ob - oc2 * 64) + (oc2 * 2 + (PY >> 2)) * 128 + ((PY & 3) * 8 + 4 * h) * 2;
+              *reinterpret_cast<uint2*>(bp) = hi;
+              *reinterpret_cast<uint2*>(bp + 64) = lo;
+            } else {
+              *reinterpret_cast<uint4*>(ob + PY * 8 + 4 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+            }
           }
         } else {
 #pragma unroll
@@ -328,7 +339,15 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
             pv.y = fmaxf(fmaxf(fmaxf(acc[i][g0 + 2], acc[i][g0 + 3]), fmaxf(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
                          0.f);
             const int PY = 2 * ty2 + qy, PX = 4 * i + 2 * h;
-            *reinterpret_cast<float2*>(ob + PY * 8 + PX) = pv;
+            if constexpr (SPLIT_OUT) {
+              uint32_t hi, lo;
+              split2(pv.x, pv.y, hi, lo);
+              char* bp = reinterpret_cast<char*>(ob - oc2 * 64) + (oc2 * 2 + (PY >> 2)) * 128 + ((PY & 3) * 8 + PX) * 2;
+              *reinterpret_cast<uint32_t*>(bp) = hi;
+              *reinterpret_cast<uint32_t*>(bp + 64) = lo;
+            } else {
+              *reinterpret_cast<float2*>(ob + PY * 8 + PX) = pv;
+            }
           }
         }
         }
@@ -380,6 +399,13 @@ __device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, in
 // two k-steps ahead once the loads were coalesced (flat, 6 spilled VGPRs).  Probes
 // (profiles/r2_cifar_fc1_probes.jsonl): without the A stream the kernel runs
 // 0.51 ms, without any load 0.45 ms (1.8 PF/s), with both 0.80 ms.
+//
+// SPLIT_IN: A arrives pre-split in the blocked boundary encoding (see
+// cifar_split_blocked_kernel: per row and 32-k block, 32 bf16 hi then 32 bf16
+// lo — the same 4 bytes per element as fp32, the same hi/lo this kernel would
+// form in registers), so A is staged by DMA exactly like W: no VGPR round
+// trip, no split ALU, no vmcnt stall on A inside the k loop.
+template <bool SPLIT_IN>
 __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __restrict__ A, int lda,
                                                               const bf16_t* __restrict__ Wh,
                                                               const bf16_t* __restrict__ Wl, int ldw,
@@ -422,6 +448,20 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
     }
   };
   // W: per plane 16 pieces of 16 rows (1 KiB per wave instruction), 2 per wave
+  // SPLIT_IN: A hi / lo planes by DMA, 2 pieces of 16 rows per wave and plane (as W)
+  auto stage_a = [&](int u, int t) {
+    const char* Ab = reinterpret_cast<const char*>(A);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int piece = wave * 2 + j, rl = piece * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ f1_swz(rl);
+        const int row = min(m0 + rl, M - 1);
+        glds16(Ab + (size_t)row * lda * 4 + t * 128 + p * 64 + c * 16, plane(u, p) + piece * 1024);
+      }
+    }
+  };
   auto stage_w = [&](int u, int t) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -442,10 +482,16 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   using I0 = std::integral_constant<int, 0>;
-  load_a(0, I0{});
-  stage_w(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  store_a(0, I0{});
+  if constexpr (SPLIT_IN) {
+    stage_a(0, 0);
+    stage_w(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    load_a(0, I0{});
+    stage_w(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_a(0, I0{});
+  }
   __syncthreads();
 
   const int fr = lane & 15, fc = lane >> 4;
@@ -490,13 +536,16 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
   for (int t = 0; t < nk; ++t) {
     const int u = t & 1;
     if (t + 1 < nk) {
-      load_a(t + 1, I0{});
+      if constexpr (SPLIT_IN)
+        stage_a(u ^ 1, t + 1);
+      else
+        load_a(t + 1, I0{});
       stage_w(u ^ 1, t + 1);
     }
     compute(u);
     if (t + 1 < nk) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store_a(u ^ 1, I0{});
+      if constexpr (!SPLIT_IN) store_a(u ^ 1, I0{});
     }
     barrier();
   }
@@ -512,20 +561,67 @@ __global__ __launch_bounds__(512, 1) void cifar_fc1_x3_kernel(const float* __res
   }
 }
 
+// Blocked boundary encoding of an fp32 (M,K) tensor, in place of the same
+// 4 bytes per element: row r, 32-k block b holds 32 bf16 hi then 32 bf16 lo
+// (hi + lo == x to ~2^-17 relative, the exact operand split of the x3 MFMAs).
+// dir 0: fp32 -> blocked, dir 1: blocked -> fp32 (hi + lo).  K % 32 == 0.
+__global__ __launch_bounds__(256) void cifar_split_blocked_kernel(const float* __restrict__ a, float* __restrict__ o,
+                                                                  int M, int K, int dir) {
+  const int per_row = K / 8;  // 8-element pieces
+  const long total = (long)M * per_row;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int m = (int)(e / per_row), k = (int)(e % per_row) * 8;
+    char* rowp = reinterpret_cast<char*>(o + (size_t)m * K);
+    const char* rowa = reinterpret_cast<const char*>(a + (size_t)m * K);
+    const int hoff = (k >> 5) * 128 + (k & 31) * 2;
+    if (dir == 0) {
+      const float4 u = *reinterpret_cast<const float4*>(rowa + k * 4);
+      const float4 v = *reinterpret_cast<const float4*>(rowa + k * 4 + 16);
+      uint4 hi, lo;
+      split2(u.x, u.y, hi.x, lo.x);
+      split2(u.z, u.w, hi.y, lo.y);
+      split2(v.x, v.y, hi.z, lo.z);
+      split2(v.z, v.w, hi.w, lo.w);
+      *reinterpret_cast<uint4*>(rowp + hoff) = hi;
+      *reinterpret_cast<uint4*>(rowp + hoff + 64) = lo;
+    } else {
+      const uint4 hi = *reinterpret_cast<const uint4*>(rowa + hoff);
+      const uint4 lo = *reinterpret_cast<const uint4*>(rowa + hoff + 64);
+      const uint32_t h[4] = {hi.x, hi.y, hi.z, hi.w}, l[4] = {lo.x, lo.y, lo.z, lo.w};
+      float r[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[2 * i] = __uint_as_float(h[i] << 16) + __uint_as_float(l[i] << 16);
+        r[2 * i + 1] = __uint_as_float(h[i] & 0xffff0000u) + __uint_as_float(l[i] & 0xffff0000u);
+      }
+      *reinterpret_cast<float4*>(rowp + k * 4) = float4{r[0], r[1], r[2], r[3]};
+      *reinterpret_cast<float4*>(rowp + k * 4 + 16) = float4{r[4], r[5], r[6], r[7]};
+    }
+  }
+}
+
 // fp32 (M,K) -> bf16 (M,3K) rows [hi | hi | lo]; K % 8 == 0, 16-B aligned rows.
+// blocked = 1: a is in the blocked hi/lo encoding (the split is already done).
 __global__ __launch_bounds__(256) void cifar_split3_kernel(const float* __restrict__ a, int lda,
-                                                           bf16_t* __restrict__ o, int ldo, int M, int K) {
+                                                           bf16_t* __restrict__ o, int ldo, int M, int K,
+                                                           int blocked) {
   const int per_row = K / 8;
   const long total = (long)M * per_row;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const int m = (int)(e / per_row), c = (int)(e % per_row) * 8;
-    const float4 u = *reinterpret_cast<const float4*>(a + (size_t)m * lda + c);
-    const float4 v = *reinterpret_cast<const float4*>(a + (size_t)m * lda + c + 4);
     uint4 hi, lo;
-    split2(u.x, u.y, hi.x, lo.x);
-    split2(u.z, u.w, hi.y, lo.y);
-    split2(v.x, v.y, hi.z, lo.z);
-    split2(v.z, v.w, hi.w, lo.w);
+    if (blocked) {
+      const char* rowa = reinterpret_cast<const char*>(a + (size_t)m * lda) + (c >> 5) * 128 + (c & 31) * 2;
+      hi = *reinterpret_cast<const uint4*>(rowa);
+      lo = *reinterpret_cast<const uint4*>(rowa + 64);
+    } else {
+      const float4 u = *reinterpret_cast<const float4*>(a + (size_t)m * lda + c);
+      const float4 v = *reinterpret_cast<const float4*>(a + (size_t)m * lda + c + 4);
+      split2(u.x, u.y, hi.x, lo.x);
+      split2(u.z, u.w, hi.y, lo.y);
+      split2(v.x, v.y, hi.z, lo.z);
+      split2(v.z, v.w, hi.w, lo.w);
+    }
     bf16_t* r = o + (size_t)m * ldo + c;
     *reinterpret_cast<uint4*>(r) = hi;
     *reinterpret_cast<uint4*>(r + K) = hi;
@@ -607,39 +703,60 @@ extern "C" int dnn_cifar_s0_set_wide_store(int on) {
   return 0;
 }
 
+template <bool SPLIT_OUT>
+static int launch_stage0_x3(const float* x, float* out, const void* w1h, const void* w1l, const float* b1,
+                            const void* w2h, const void* w2l, const float* b2, int B, int grid, hipStream_t st) {
+  if (g_s0_wide_store)
+    hipLaunchKernelGGL((cifar_stage0_x3_kernel<true, SPLIT_OUT>), dim3(grid), dim3(512), 0, st, x, out,
+                       (const bf16_t*)w1h, (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
+  else
+    hipLaunchKernelGGL((cifar_stage0_x3_kernel<false, SPLIT_OUT>), dim3(grid), dim3(512), 0, st, x, out,
+                       (const bf16_t*)w1h, (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
+  return (int)hipGetLastError();
+}
+
+// split_out = 1: the (B,4096) boundary in the blocked hi/lo encoding, else fp32.
 extern "C" int dnn_cifar_stage0_x3(const float* x, float* out, const void* w1h, const void* w1l, const float* b1,
                                    const void* w2h, const void* w2l, const float* b2, int B, int grid,
-                                   hipStream_t st) {
+                                   hipStream_t st, int split_out) {
   if (B <= 0) return 0;
   if (grid <= 0) grid = 256;
   if (grid > B) grid = B;
-  if (g_s0_wide_store) {
-    hipLaunchKernelGGL(cifar_stage0_x3_kernel<true>, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
-                       (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(cifar_stage0_x3_kernel<false>, dim3(grid), dim3(512), 0, st, x, out, (const bf16_t*)w1h,
-                     (const bf16_t*)w1l, b1, (const bf16_t*)w2h, (const bf16_t*)w2l, b2, B);
-  return (int)hipGetLastError();
+  return split_out ? launch_stage0_x3<true>(x, out, w1h, w1l, b1, w2h, w2l, b2, B, grid, st)
+                   : launch_stage0_x3<false>(x, out, w1h, w1l, b1, w2h, w2l, b2, B, grid, st);
 }
 
 extern "C" int dnn_cifar_fc1_x3(const float* A, int lda, const void* Wh, const void* Wl, int ldw, const float* bias,
-                                float* C, int ldc, int M, int N, int K, hipStream_t st) {
+                                float* C, int ldc, int M, int N, int K, hipStream_t st, int a_split) {
   if (M <= 0) return 0;
   if (N % F1_T != 0 || K % F1_K != 0 || lda % 4 != 0 || ldw % 8 != 0 || ldc % 4 != 0) return -1;
   const int blocks = ((M + F1_T - 1) / F1_T) * (N / F1_T);
-  hipLaunchKernelGGL(cifar_fc1_x3_kernel, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
-                     (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
+  if (a_split)
+    hipLaunchKernelGGL(cifar_fc1_x3_kernel<true>, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
+                       (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
+  else
+    hipLaunchKernelGGL(cifar_fc1_x3_kernel<false>, dim3(blocks), dim3(512), 0, st, A, lda, (const bf16_t*)Wh,
+                       (const bf16_t*)Wl, ldw, bias, C, ldc, M, N, K);
   return (int)hipGetLastError();
 }
 
-extern "C" int dnn_cifar_split3(const float* a, int lda, void* o, int ldo, int M, int K, hipStream_t st) {
+extern "C" int dnn_cifar_split_blocked(const float* a, float* o, int M, int K, int dir, hipStream_t st) {
   if (M <= 0) return 0;
-  if (K % 8 != 0 || lda % 4 != 0 || ldo % 8 != 0 || ldo < 3 * K) return -1;
+  if (K % 32 != 0 || a == o) return -1;
   const long total = (long)M * (K / 8);
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(cifar_split3_kernel, dim3((int)blocks), dim3(256), 0, st, a, lda, (bf16_t*)o, ldo, M, K);
+  hipLaunchKernelGGL(cifar_split_blocked_kernel, dim3((int)blocks), dim3(256), 0, st, a, o, M, K, dir);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dnn_cifar_split3(const float* a, int lda, void* o, int ldo, int M, int K, hipStream_t st, int blocked) {
+  if (M <= 0) return 0;
+  if (K % 8 != 0 || lda % 4 != 0 || ldo % 8 != 0 || ldo < 3 * K || (blocked && K % 32 != 0)) return -1;
+  const long total = (long)M * (K / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cifar_split3_kernel, dim3((int)blocks), dim3(256), 0, st, a, lda, (bf16_t*)o, ldo, M, K, blocked);
   return (int)hipGetLastError();
 }
 

@@ -11,6 +11,16 @@ fp32 modules to the device):
   registers while staged to LDS (A read once as fp32, no split copy); at small
   batch (too few 256-row tiles to fill the chip) it runs as ONE skinny/128^2
   bf16 GEMM over K' = 3*4096 on ``[A_hi | A_hi | A_lo]`` x ``[W_hi | W_lo | W_hi]``.
+  Optional boundary encoding ``boundary="split"`` (fp32 only, both ends of
+  the hop must be these kernels): the same 16 KiB/img, each row as 32-k blocks
+  of 32 bf16 hi then 32 bf16 lo — the very hi/lo operands the x3 MFMAs consume
+  (hi + lo = the fp32 value to ~2^-17) — written by the stage-0 epilogue and
+  staged into LDS by DMA in fc1 (no register split pass): fc1 0.710 -> 0.632
+  ms at B=65536 with bit-identical outputs (profiles/r3_fc1_split_ab.jsonl),
+  but the split stores cost the stage-0 epilogue as much, so the 2-stage step
+  is unchanged (2.541 vs 2.548 ms, profiles/r3_boundary_ab.jsonl) and the
+  pipelines keep plain fp32 (also the wire format a reference peer expects).
+  ``decode_boundary`` / ``encode_boundary`` convert.
 * ``bf16``: ``csrc/kernels/cifar_fused.hip`` (v4 persistent kernel), bf16
   boundary, an explicitly reduced-precision mode.
 
@@ -154,9 +164,36 @@ def _check_act(t: torch.Tensor, shape, dtype, what: str) -> None:
                          f"got {t.dtype} {tuple(t.shape)}")
 
 
+BOUNDARIES = ("fp32", "split")
+
+
+def _split_boundary(boundary: str, precision: str) -> int:
+    if boundary not in BOUNDARIES:
+        raise ValueError(f"boundary must be one of {BOUNDARIES}, got {boundary!r}")
+    if boundary == "split" and precision != "fp32":
+        raise ValueError("the split boundary encoding exists for the fp32 precision only")
+    return int(boundary == "split")
+
+
+def encode_boundary(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 (B,K) -> the blocked hi/lo boundary encoding (same shape and dtype)."""
+    out = torch.empty_like(h) if out is None else out
+    check(lib().cifar_split_blocked(ptr(h), ptr(out), h.shape[0], h.shape[1], 0, stream_ptr()), "encode_boundary")
+    return out
+
+
+def decode_boundary(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Blocked hi/lo boundary encoding -> fp32 values (hi + lo)."""
+    out = torch.empty_like(h) if out is None else out
+    check(lib().cifar_split_blocked(ptr(h), ptr(out), h.shape[0], h.shape[1], 1, stream_ptr()), "decode_boundary")
+    return out
+
+
 def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.Tensor] = None,
-                   grid: int = 0) -> torch.Tensor:
-    """Units 0-1: x (B,3,32,32) fp32 contiguous -> (B,4096) fp32 (or bf16 in bf16 mode)."""
+                   grid: int = 0, boundary: str = "fp32") -> torch.Tensor:
+    """Units 0-1: x (B,3,32,32) fp32 contiguous -> (B,4096) fp32 (or bf16 in bf16 mode;
+    ``boundary="split"``: the blocked hi/lo encoding in the fp32 tensor)."""
+    split = _split_boundary(boundary, w.precision)
     grid = grid or STAGE0_GRID
     _check_act(x, (3, 32, 32), torch.float32, "stage0 input")
     B = x.shape[0]
@@ -167,7 +204,7 @@ def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.T
         raise ValueError("stage0: bad output buffer")
     if w.precision == "fp32":
         check(lib().cifar_stage0_x3(ptr(x), ptr(out), ptr(w.w1h), ptr(w.w1l), ptr(w.b1), ptr(w.w2h), ptr(w.w2l),
-                                    ptr(w.b2), B, grid, stream_ptr()), "cifar_stage0_x3")
+                                    ptr(w.b2), B, grid, stream_ptr(), split), "cifar_stage0_x3")
     else:
         check(lib().cifar_stage0_v4(ptr(x), ptr(out), ptr(w.w1), ptr(w.b1), ptr(w.w2), ptr(w.b2), B, grid,
                                     stream_ptr()), "cifar_stage0_v4")
@@ -175,9 +212,11 @@ def stage0_forward(x: torch.Tensor, w: CifarStage0Weights, out: Optional[torch.T
 
 
 def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor] = None,
-                scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+                scratch: Optional[torch.Tensor] = None, boundary: str = "fp32") -> torch.Tensor:
     """Unit 2: (B,4096) -> relu(fc1) (B,512) on the MFMA GEMM (fp32: split operand,
-    ``scratch`` = (>=B, 12288) bf16 for the [hi | hi | lo] rows)."""
+    ``scratch`` = (>=B, 12288) bf16 for the [hi | hi | lo] rows; ``boundary``:
+    the encoding of ``h``)."""
+    split = _split_boundary(boundary, w.precision)
     dt = act_dtype(w.precision)
     _check_act(h, (4096,), dt, "fc1 input")
     B = h.shape[0]
@@ -187,12 +226,12 @@ def fc1_forward(h: torch.Tensor, w: CifarHeadWeights, out: Optional[torch.Tensor
         if out is None:
             out = torch.empty((B, 512), dtype=torch.float32, device=h.device)
         check(lib().cifar_fc1_x3(ptr(h), 4096, ptr(w.w_fc1h), ptr(w.w_fc1l), 4096, ptr(w.b_fc1), ptr(out), 512,
-                                 B, 512, 4096, stream_ptr()), "cifar_fc1_x3")
+                                 B, 512, 4096, stream_ptr(), split), "cifar_fc1_x3")
         return out
     if scratch is None or scratch.shape[0] < B or tuple(scratch.shape[1:]) != (3 * 4096,):
         scratch = torch.empty((B, 3 * 4096), dtype=torch.bfloat16, device=h.device)
     a3 = scratch[:B]
-    check(lib().cifar_split3(ptr(h), 4096, ptr(a3), 3 * 4096, B, 4096, stream_ptr()), "cifar_split3")
+    check(lib().cifar_split3(ptr(h), 4096, ptr(a3), 3 * 4096, B, 4096, stream_ptr(), split), "cifar_split3")
     if out is None:
         out = torch.empty((B, 512), dtype=torch.float32, device=h.device)
     return linear(a3, w.w_fc1, w.b_fc1, act=ACT_RELU, out=out)
@@ -215,8 +254,8 @@ def head_tail(hid: torch.Tensor, w: CifarHeadWeights, probs: Optional[torch.Tens
 
 
 def head_forward(h: torch.Tensor, w: CifarHeadWeights, hid: Optional[torch.Tensor] = None,
-                 probs: Optional[torch.Tensor] = None, pred: Optional[torch.Tensor] = None
-                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+                 probs: Optional[torch.Tensor] = None, pred: Optional[torch.Tensor] = None,
+                 boundary: str = "fp32") -> Tuple[torch.Tensor, torch.Tensor]:
     """Units 2-3: h (B,4096) -> (probs (B,10) fp32, pred (B,) int32)."""
-    hid = fc1_forward(h, w, out=hid)
+    hid = fc1_forward(h, w, out=hid, boundary=boundary)
     return head_tail(hid, w, probs, pred)

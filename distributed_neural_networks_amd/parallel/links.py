@@ -1,13 +1,20 @@
-"""Stage-to-stage links over ``torch.distributed`` point-to-point.
+"""Stage-to-stage links.
 
 The reference moves every activation GPU -> host -> protobuf -> TCP -> host ->
 GPU through a new gRPC channel per request (``node.py:45-55,73-89``).  Here a
-``P2PLink`` is one direction-agnostic peer of this rank: RCCL (backend
-``"nccl"``) over the direct xGMI link between the two stage GPUs, or gloo on
-CPU.  On RCCL:
+link is one direction-agnostic peer of this rank:
+
+* ``RcclLink`` (GPU stages, the default): this package's own RCCL channel per
+  rank pair (``parallel/rccl.py`` over ``csrc/comm/p2p.cpp``) — device
+  buffers straight over the xGMI link between the two stage GPUs;
+* ``P2PLink``: ``torch.distributed`` isend/irecv — gloo on CPU, or
+  ProcessGroupNCCL with ``DNN_P2P=torch``;
+* ``HostStagedLink``: gloo between ranks that compute on a GPU (``gloo_gpu``).
+
+All share one contract, stated here for RCCL:
 
 * device buffers move GPU -> GPU, no host staging and no serialisation;
-* ProcessGroupNCCL runs P2P on its own stream per peer pair, ordered after the
+* each peer pair's transfers run on their own stream, ordered after the
   work already queued on the compute stream when the op is posted, and
   ``Work.wait()`` orders the compute stream after the transfer without
   blocking the host — so a stage never waits on the host for a hop;

@@ -59,18 +59,28 @@ class CifarHipStage(StageCompute):
     pipeline, parallel/partition.py ``cifar_cut``).
 
     ``precision`` "fp32" (default, the reference's: fp32 in, fp32 boundary,
-    3-term bf16 split products accumulated in fp32) or "bf16"."""
+    3-term bf16 split products accumulated in fp32) or "bf16".
+
+    ``boundary`` (fp32, the conv|fc cut): "fp32" values on the 16 KiB/img
+    boundary (default; what a reference peer expects over gRPC), or "split" —
+    the blocked hi/lo encoding of the same 16 KiB (``ops/cifar.py``;
+    bit-identical results, measured neutral end to end).  Both stages of a hop
+    must agree."""
 
     SUPPORTED = {(0, 1), (2, 3), (0, 3), (0, 2), (2, 2), (3, 3)}
 
     def __init__(self, sd: Dict[str, torch.Tensor], start: int, end: int, device: torch.device,
-                 precision: str = "fp32"):
+                 precision: str = "fp32", boundary: str = "fp32"):
         from ..ops import cifar as cops
         if (start, end) not in self.SUPPORTED:
             raise ValueError(f"HIP CIFAR backend supports unit ranges {sorted(self.SUPPORTED)}, got ({start},{end})")
         self.start, self.end, self.device = start, end, torch.device(device)
         self.first, self.last = start == 0, end == cifar.NUM_UNITS - 1
         self.precision = precision
+        if boundary not in cops.BOUNDARIES:
+            raise ValueError(f"boundary must be one of {cops.BOUNDARIES}")
+        # the encoding only exists on the 4096-wide conv|fc boundary of the fp32 path
+        self.boundary = boundary if precision == "fp32" else "fp32"
         self._cops = cops
         self.adt = cops.act_dtype(precision)
         self.w0 = cops.pack_stage0(sd, self.device, precision) if start == 0 else None
@@ -114,14 +124,15 @@ class CifarHipStage(StageCompute):
         if self.first:
             if h.dtype != torch.float32:
                 h = h.float()
-            h = self._cops.stage0_forward(h.contiguous(), self.w0, buf["mid"] if self.end >= 2 else out)
+            h = self._cops.stage0_forward(h.contiguous(), self.w0, buf["mid"] if self.end >= 2 else out,
+                                          boundary=self.boundary)
             if self.end == 1:
                 return h
         elif h.dtype != self.adt:
             h = h.to(self.adt)
         if self.start <= 2 <= self.end:
             h = self._cops.fc1_forward(h.contiguous(), self.wh, out if self.end == 2 else buf["hid"],
-                                       scratch=buf.get("split"))
+                                       scratch=buf.get("split"), boundary=self.boundary)
             if self.end == 2:
                 return h
         probs, pred = self._cops.head_tail(h.contiguous(), self.wh, out, buf["pred"])

@@ -226,7 +226,8 @@ def test_cifar_fp32_stage0_and_head(B):
     assert torch.equal(pred.cpu().long(), probs.cpu().argmax(1))
 
 
-def test_cifar_fp32_pipeline_4096_images_matches_reference():
+@pytest.mark.parametrize("boundary", ["fp32", "split"])
+def test_cifar_fp32_pipeline_4096_images_matches_reference(boundary):
     """Acceptance: the 2-stage pipeline at the reference's
     precision on 4096 images: max |dprob| <= 1e-5 vs fp32 torch
     (cifar_model_parts.py:7-26) and 100 % argmax agreement (rows whose golden
@@ -234,7 +235,7 @@ def test_cifar_fp32_pipeline_4096_images_matches_reference():
     from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
     from distributed_neural_networks_amd.runtime.stages import CifarHipStage
     sd, x, _, ref = _cifar_golden(2, 4096)
-    st = [CifarHipStage(sd, 0, 1, DEV), CifarHipStage(sd, 2, 3, DEV)]
+    st = [CifarHipStage(sd, 0, 1, DEV, boundary=boundary), CifarHipStage(sd, 2, 3, DEV, boundary=boundary)]
     assert st[0].out_spec(4) == ((4, 4096), torch.float32)
     out = ColocatedPipeline(st, 4096)(x.to(DEV))
     torch.cuda.synchronize()
@@ -267,20 +268,23 @@ def test_cifar_stage_cuts(cut, precision):
     assert st[0].out_spec(8) == ((8, 4096 if cut == 1 else 512), dt)
 
 
+@pytest.mark.parametrize("split_in", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(300, 256, 64), (1000, 512, 4096), (16384 + 77, 512, 4096)])
-def test_cifar_fc1_x3_kernel(M, N, K):
-    """Fused fp32 fc1 (split in registers while staging): relu(A W^T + b) vs
-    fp32 torch, relative error at the ~2^-16 level of the 3-term split."""
+def test_cifar_fc1_x3_kernel(M, N, K, split_in):
+    """Fused fp32 fc1 (A split in registers while staging, or A in the blocked
+    hi/lo encoding staged by DMA): relu(A W^T + b) vs fp32 torch, relative
+    error at the ~2^-16 level of the 3-term split."""
     from distributed_neural_networks_amd.ops import _lib
-    from distributed_neural_networks_amd.ops.cifar import split_bf16
+    from distributed_neural_networks_amd.ops.cifar import encode_boundary, split_bf16
     torch.manual_seed(M)
     a = torch.randn(M, K, device=DEV)
     w = torch.randn(N, K, device=DEV) / K ** 0.5
     b = torch.randn(N, device=DEV) * 0.1
     wh, wl = split_bf16(w)
     out = torch.empty(M, N, device=DEV)
-    rc = _lib.lib().cifar_fc1_x3(a.data_ptr(), K, wh.data_ptr(), wl.data_ptr(), K, b.data_ptr(), out.data_ptr(), N,
-                                 M, N, K, torch.cuda.current_stream().cuda_stream)
+    a_in = encode_boundary(a) if split_in else a
+    rc = _lib.lib().cifar_fc1_x3(a_in.data_ptr(), K, wh.data_ptr(), wl.data_ptr(), K, b.data_ptr(), out.data_ptr(),
+                                 N, M, N, K, torch.cuda.current_stream().cuda_stream, split_in)
     assert rc == 0
     torch.cuda.synchronize()
     ref = torch.relu(a.double() @ w.double().t() + b.double())
@@ -288,7 +292,8 @@ def test_cifar_fc1_x3_kernel(M, N, K):
     assert err <= 2e-5 * ref.abs().max().item(), err
 
 
-def test_cifar_fp32_pipeline_large_batch_fused_fc1():
+@pytest.mark.parametrize("boundary", ["fp32", "split"])
+def test_cifar_fp32_pipeline_large_batch_fused_fc1(boundary):
     """The large-batch fp32 head (fused fc1) on 20000 images: max |dprob| <= 1e-5
     vs the fp32 torch model and argmax agreement on every decidable row."""
     from distributed_neural_networks_amd.ops import cifar as cops
@@ -297,7 +302,7 @@ def test_cifar_fp32_pipeline_large_batch_fused_fc1():
     B = 20000
     assert B >= cops.FC1_X3_MIN_ROWS
     sd, x, _, ref = _cifar_golden(3, B)
-    st = [CifarHipStage(sd, 0, 1, DEV), CifarHipStage(sd, 2, 3, DEV)]
+    st = [CifarHipStage(sd, 0, 1, DEV, boundary=boundary), CifarHipStage(sd, 2, 3, DEV, boundary=boundary)]
     out = ColocatedPipeline(st, B)(x.to(DEV))
     torch.cuda.synchronize()
     dp = (out.probs.cpu() - ref).abs().max().item()
@@ -306,3 +311,33 @@ def test_cifar_fp32_pipeline_large_batch_fused_fc1():
     decidable = (top2[:, 0] - top2[:, 1]) > 1e-6
     agree = out.pred.cpu().long() == ref.argmax(1)
     assert bool(agree[decidable].all()), int((~agree[decidable]).sum())
+
+
+@pytest.mark.parametrize("B", [1, 300, 16384 + 77])
+def test_cifar_split_boundary_bit_identical(B):
+    """The blocked hi/lo boundary encoding is exactly the split of the fp32
+    boundary (stage-0 epilogue == encode of the fp32 output, bitwise), decodes
+    to it within 2^-16, and the pipeline's probabilities and predictions are
+    bitwise those of the fp32 boundary (small-batch split3 path and the fused
+    fc1 path)."""
+    from distributed_neural_networks_amd.ops import cifar as cops
+    from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
+    from distributed_neural_networks_amd.runtime.stages import CifarHipStage
+    torch.manual_seed(B)
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
+    sd = NeuralNetwork().state_dict()
+    x = torch.randn(B, 3, 32, 32, device=DEV)
+    w0 = cops.pack_stage0(sd, DEV, "fp32")
+    h32 = cops.stage0_forward(x, w0, boundary="fp32")
+    hsp = cops.stage0_forward(x, w0, boundary="split")
+    assert torch.equal(cops.encode_boundary(h32).view(torch.int32), hsp.view(torch.int32))
+    back = cops.decode_boundary(hsp)
+    assert ((back - h32).abs() <= h32.abs() * 2 ** -16).all()
+    outs = {}
+    for bd in ("fp32", "split"):
+        st = [CifarHipStage(sd, 0, 1, DEV, boundary=bd), CifarHipStage(sd, 2, 3, DEV, boundary=bd)]
+        o = ColocatedPipeline(st, B)(x)
+        outs[bd] = (o.probs.clone(), o.pred.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs["fp32"][0], outs["split"][0])
+    assert torch.equal(outs["fp32"][1], outs["split"][1])
