@@ -7,8 +7,9 @@ ProcessGroupNCCL's P2P.
 * ``Channel``: one RCCL communicator (a peer pair or a 1-rank loopback) with
   its own high-priority transfer stream and a ring of completion events.  The
   lower rank of a pair draws the RCCL unique id and publishes it in the
-  process group's TCP store; both ranks then start the collective init on a
-  background thread (``async``), so a rank may open its channels in any order
+  process group's TCP store; the higher rank reads it, and both run the
+  collective init, on a background thread, so opening a channel never blocks
+  and a rank may open its channels in any order, interleaved with collectives
   — ProcessGroupNCCL instead inits a pair's communicator lazily and blocking
   inside the first op, which deadlocks when two stages meet their links in
   different orders.
@@ -63,39 +64,58 @@ def _nbytes(t: torch.Tensor) -> int:
 
 
 class Channel:
-    """One RCCL communicator with its transfer stream (``csrc/comm/p2p.cpp``)."""
+    """One RCCL communicator with its transfer stream (``csrc/comm/p2p.cpp``).
 
-    def __init__(self, uid: bytes, nranks: int, rank: int, device: torch.device, key=None):
+    Construction never blocks: the unique id fetch (``uid_fn``, the higher rank
+    of a pair reads it from the store) and the collective communicator init run
+    on a background thread; ``ready()`` joins it.  So no ordering of channel
+    creation against collectives or other channels can deadlock."""
+
+    def __init__(self, uid: Optional[bytes], nranks: int, rank: int, device: torch.device, key=None, uid_fn=None):
         if device.type != "cuda":
             raise ValueError("RCCL channels need a GPU device")
         self.nranks, self.rank, self.device, self.key = nranks, rank, device, key
-        self.h = _lib().comm_create(uid, nranks, rank, device.index, 1)
+        self.h = None
+        self._err: Optional[BaseException] = None
         self._ready = False
         self._keep = collections.deque()  # (token, tensor): buffers alive until their op completed
         self.closed = False
+
+        def init():
+            try:
+                u = uid if uid is not None else bytes(uid_fn())
+                self.h = _lib().comm_create(u, nranks, rank, device.index, 0)  # blocking init, GIL released
+                if _lib().comm_wait_ready(self.h, 0) != 0:  # the init's verdict (message: this thread's last error)
+                    raise RuntimeError(_lib().comm_last_error())
+            except BaseException as e:  # noqa: BLE001 — re-raised by ready()
+                self._err = e
+
+        self._thread = threading.Thread(target=init, name=f"rccl-init-{key}", daemon=True)
+        self._thread.start()
 
     # -- lifecycle -----------------------------------------------------------------
     def ready(self, timeout_s: float = INIT_TIMEOUT_S) -> "Channel":
         if self._ready:
             return self
-        rc = _lib().comm_wait_ready(self.h, int(timeout_s * 1000))
-        if rc == 1:
+        self._thread.join(timeout_s)
+        if self._thread.is_alive():
             raise TimeoutError(f"RCCL channel {self.key}: communicator init not finished after {timeout_s:.0f} s "
                                "(peer rank never opened its end?)")
-        if rc != 0:
-            raise RuntimeError(f"RCCL channel {self.key}: {_lib().comm_last_error()}")
+        if self._err is not None:
+            raise RuntimeError(f"RCCL channel {self.key}: init failed: {self._err}") from self._err
         self._ready = True
         return self
 
     def abort(self) -> None:
-        if not self.closed:
+        if not self.closed and self.h is not None:
             _lib().comm_abort(self.h)
 
     def destroy(self) -> None:
         if not self.closed:
             self.closed = True
             self._keep.clear()
-            _lib().comm_destroy(self.h)
+            if self.h is not None:
+                _lib().comm_destroy(self.h)
 
     # -- ops -------------------------------------------------------------------------
     def _stream(self, stream) -> int:
@@ -200,9 +220,10 @@ def pair_channel(my_rank: int, peer: int, device: torch.device, tag: str = "worl
         if my_rank == ranks[0]:
             uid = _lib().comm_unique_id()
             st.set(skey, uid)
-        else:
-            uid = st.get(skey)  # the lower rank publishes without waiting on anyone: no ordering cycle
-        ch = _CHANNELS[key] = Channel(bytes(uid), 2, ranks.index(my_rank), device, key=key)
+            ch = Channel(uid, 2, 0, device, key=key)
+        else:  # the id is read on the init thread: opening a channel never blocks
+            ch = Channel(None, 2, 1, device, key=key, uid_fn=lambda: st.get(skey))
+        _CHANNELS[key] = ch
         return ch
 
 
