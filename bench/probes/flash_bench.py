@@ -27,8 +27,11 @@ def timeit(fn, iters=20):
 def main():
     from distributed_neural_networks_amd.ops import transformer_ops as T_
     dev = torch.device("cuda", 0)
-    for (B, T, H, Hkv, hd) in [(64, 512, 12, 12, 64), (8, 2048, 12, 12, 64), (32, 512, 32, 8, 128),
-                               (4, 4096, 32, 8, 128)]:
+    shapes = [(64, 512, 12, 12, 64), (8, 2048, 12, 12, 64), (32, 512, 32, 8, 128), (4, 4096, 32, 8, 128)]
+    pick = os.environ.get("FLASH_SHAPES")  # e.g. "0" (GPT-2 B=64 T=512 only, for PMC passes)
+    if pick:
+        shapes = [shapes[int(i)] for i in pick.split(",")]
+    for (B, T, H, Hkv, hd) in shapes:
         qkv = torch.randn(B * T, (H + 2 * Hkv) * hd, device=dev).bfloat16()
         kc = torch.zeros(B, Hkv, T, hd, device=dev, dtype=torch.bfloat16)
         vc = torch.zeros_like(kc)
@@ -47,9 +50,14 @@ def main():
         ref = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)  # noqa: E731
         flop = 4.0 * B * H * T * T * hd / 2
         t_o, t_r = timeit(ours), timeit(ref)
+        pfs = {}
+        for pf in (1, 2):  # prefetch-depth A/B in the same process (attention.hip flash_pf)
+            os.environ["DNN_FLASH_PF"] = str(pf)
+            pfs[f"pf{pf}_ms"] = round(min(timeit(ours) for _ in range(3)), 4)
+        os.environ.pop("DNN_FLASH_PF", None)
         print(json.dumps({"B": B, "T": T, "H": H, "Hkv": Hkv, "hd": hd, "ours_ms": round(t_o, 4),
                           "ours_tflops": round(flop / t_o / 1e9, 1), "torch_sdpa_ms": round(t_r, 4),
-                          "torch_tflops": round(flop / t_r / 1e9, 1)}), flush=True)
+                          "torch_tflops": round(flop / t_r / 1e9, 1), **pfs}), flush=True)
 
 
 if __name__ == "__main__":

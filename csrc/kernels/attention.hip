@@ -149,7 +149,7 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
-template <int HD, bool QKV = false, bool KV8 = false>
+template <int HD, bool QKV = false, bool KV8 = false, int PF = 1>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
@@ -222,12 +222,15 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const bf16_t* kbase = kc + ((size_t)b * Hkv + kvh) * S * HD;
   const bf16_t* vbase = vc + ((size_t)b * Hkv + kvh) * S * HD;
 
-  // K/V blocks are register double-buffered: block kb0+64 is fetched from
-  // global memory while block kb0 is computed, then written to LDS after the
-  // trailing barrier, so the load latency hides under the MFMA/softmax work.
+  // K/V blocks are register-prefetched PF blocks ahead: block kb0 + PF*64 is
+  // fetched from global memory while block kb0 is computed, then written to LDS
+  // after the trailing barrier.  PF = 1 left the loop waiting on its fetch: at
+  // GPT-2 prefill (768 workgroups of 128 queries x 2-8 blocks) a block's MFMA +
+  // softmax work (~1 us) is shorter than the loaded-chip global latency, and the
+  // PMC showed the MFMA pipe 11 % busy, VALU 30 %, the waves waiting the rest.
   constexpr int NIT = (FA_KB * CH) / 256;
-  i32x4 pk[NIT], pv[NIT];  // ext vectors: uint4 structs do not promote out of scratch
-  auto fetch = [&](int kb0) __attribute__((always_inline)) {
+  i32x4 pkA[NIT], pvA[NIT], pkB[NIT], pvB[NIT];  // ext vectors: uint4 structs do not promote out of scratch
+  auto fetch = [&](int kb0, i32x4(&pk)[NIT], i32x4(&pv)[NIT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int e = it * 256 + tid;
@@ -247,8 +250,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       }
     }
   };
-  if (kv_end > 0) fetch(0);
-  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
+  auto block = [&](int kb0, i32x4(&pk)[NIT], i32x4(&pv)[NIT]) __attribute__((always_inline)) {
     // ---- stage K (swizzled) and V (padded rows) from the prefetch registers ----
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       *reinterpret_cast<i32x4*>(vs + key * SM::V_STRIDE + c * 16) = pv[it];
     }
     __syncthreads();
-    if (kb0 + FA_KB < kv_end) fetch(kb0 + FA_KB);
+    if (kb0 + PF * FA_KB < kv_end) fetch(kb0 + PF * FA_KB, pk, pv);
     if (kb0 <= wave_qmax) {
       // ---- S^T for two 32-key tiles ----
       f32x16 sacc[2];
@@ -354,6 +356,17 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
         }
     }
     __syncthreads();
+  };
+  if constexpr (PF == 1) {
+    if (kv_end > 0) fetch(0, pkA, pvA);
+    for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) block(kb0, pkA, pvA);
+  } else {
+    if (kv_end > 0) fetch(0, pkA, pvA);
+    if (FA_KB < kv_end) fetch(FA_KB, pkB, pvB);
+    for (int kb0 = 0; kb0 < kv_end; kb0 += 2 * FA_KB) {
+      block(kb0, pkA, pvA);
+      if (kb0 + FA_KB < kv_end) block(kb0 + FA_KB, pkB, pvB);
+    }
   }
   // ---- normalise + store: lane = query, regs = d ----
   if (qrow < T) {
@@ -807,6 +820,319 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   DEC_PROBE(7, 0);
 }
 
+// ---------------------------------------------------------------------------
+// One-pass decode attention (round 3): every key and value row of a split is
+// requested before the first score is formed, so a workgroup's whole K/V
+// range is in flight at once instead of one batch per round trip.
+//
+// attn_decode_kernel above runs K batch -> scores -> softmax pass -> V batch
+// -> P.V -> V batch ...: at Llama-3 8B B=32 (B*Hkv = 256, 3 splits of ~180
+// keys) that chain ran at 3.5 TB/s plus a 4.8 us combine launch, at GPT-2
+// B=64 at 5.0 TB/s.  Here, for a split of at most CAP = NW*KT*16 keys:
+//   1. q / new key / new value (first in the vmcnt queue), then every K tile
+//      of the wave (KT x HD/32 16-B loads per lane), then the first VE value
+//      rows of the thread;
+//   2. scores on MFMA as K lands (16 keys x 16 head columns per tile, lane =
+//      key row, B = q^T), written to LDS, and each wave's per-head max kept
+//      in registers -> LDS (no separate max pass);
+//   3. the remaining value rows are issued as soon as the K registers are
+//      free, then one barrier;
+//   4. P.V on v_dot2 (thread = 8 dims of VU rows), exponentials taken where
+//      they are used, row sums carried beside the accumulators;
+//   5. one LDS reduction over the row groups, output written directly (one
+//      split) or as the (o, m, l) partial decode_combine_kernel merges.
+// Cache rows past the runtime length are never scored: their loads are
+// clamped to the last valid row (same address: coalesced).
+template <int HD, int G, int FM, bool NT, int NW, int KT, int VE, int VU, bool RS = false, bool KNT = NT>
+__global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                               bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                               float* __restrict__ ws, int H, int Hkv, int S,
+                                                               const int* __restrict__ lens,
+                                                               const float* __restrict__ cosT,
+                                                               const float* __restrict__ sinT, float scale_log2,
+                                                               bf16_t* __restrict__ o_direct) {
+  // RS: scores in the row layout (thread = 8 dims of key rows grp + GPB*u, dot2
+  // + DPP row sum, as the value rows) instead of MFMA key tiles; KNT: the key
+  // loads non-temporal (NT: the value loads)
+  constexpr bool FUSED = FM != 0, ROPE = FM == 2;
+  constexpr int NTH = NW * 64;
+  constexpr int LPK = HD / 8;          // lanes per value row (16 B = 8 dims each)
+  constexpr int GPB = NTH / LPK;       // value row groups
+  constexpr int NKC = HD / 32;         // MFMA k-steps of a key tile
+  constexpr int CAP = RS ? GPB * VU : NW * KT * 16;  // keys per split (host-checked)
+  constexpr int KR = RS ? VU : 1;      // key rows per thread (RS)
+  static_assert(GPB * VU >= CAP, "value rows must cover the key tiles");
+  static_assert(VE <= VU && VU % 2 == 0 && G <= 16, "bad shape");
+  __shared__ float sc[G][CAP];         // scaled scores
+  __shared__ float wmax[NW][G];        // per-wave score max per head
+  extern __shared__ __attribute__((aligned(16))) float red1p[];  // [GPB][G][HD] + [GPB][G]
+
+  const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
+  const int b = bk / Hkv, kvh = bk % Hkv;
+  const int p_new = FUSED ? lens[b] : 0;
+  const int len = FUSED ? min(p_new + 1, S) : min(lens[b], S);
+  const int chunk = (len + NS - 1) / NS;
+  const int k0 = split * chunk, k1 = min(len, k0 + chunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hj = lane & 15, c4 = lane >> 4;
+  const int sub = tid % LPK, grp = tid / LPK;
+  float* wsp = ws + ((size_t)bk * NS + split) * G * (HD + 2);
+  if (k0 >= k1) {  // empty split (short context): neutral partial
+    for (int i = tid; i < G * (HD + 2); i += NTH) wsp[i] = (i % (HD + 2)) == HD ? -INFINITY : 0.f;
+    return;
+  }
+  const int n = k1 - k0;
+  bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * S * HD + (size_t)k0 * HD;
+  bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * S * HD + (size_t)k0 * HD;
+  const bool own_new = FUSED && p_new < S && p_new >= k0 && p_new < k1;
+  const int knew = own_new ? p_new - k0 : -1;
+  const int pr = min(p_new, S - 1);
+
+  // ---- 1. q (MFMA: q^T B operand with columns >= G zero, new key in A layout;
+  // RS: bf16 pairs of this thread's 8 dims per head), new k/v (row layout)
+  bf16x8 qB[NKC], nkA[NKC];
+  uint32_t qp[RS ? G : 1][4];
+  if constexpr (!RS) {
+#pragma unroll
+    for (int m = 0; m < NKC; ++m) {
+      float t8[8];
+      const int hq = min(hj, G - 1);
+      if constexpr (FUSED) {
+        load_head8<HD, ROPE>(q + (size_t)b * ldq + (kvh * G + hq) * HD, c4 + 4 * m, cosT, sinT, pr, t8);
+      } else {
+        const bf16x8 pq =
+            *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + hq) * HD + (c4 + 4 * m) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t8[j] = bf2f_s(pq[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qB[m][j] = hj < G ? (short)f2bf(t8[j]) : (short)0;
+      if constexpr (FUSED) {
+        load_head8<HD, ROPE>(q + (size_t)b * ldq + (H + kvh) * HD, c4 + 4 * m, cosT, sinT, pr, t8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nkA[m][j] = (short)f2bf(t8[j]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float t8[8];
+      if constexpr (FUSED) {
+        load_head8<HD, ROPE>(q + (size_t)b * ldq + (kvh * G + g) * HD, sub, cosT, sinT, pr, t8);
+      } else {
+        const bf16x8 pq = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * H + kvh * G + g) * HD + sub * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t8[j] = bf2f_s(pq[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qp[g][j] = pack2bf(t8[2 * j], t8[2 * j + 1]);
+    }
+  }
+  uint32_t nkp[4] = {0, 0, 0, 0}, nvp[4] = {0, 0, 0, 0};  // this thread's 8 dims of the new row (bf16 pairs)
+  if constexpr (FUSED) {
+    float nk[8], nv[8];
+    load_head8<HD, ROPE>(q + (size_t)b * ldq + (H + kvh) * HD, sub, cosT, sinT, pr, nk);
+    load_head8<HD, false>(q + (size_t)b * ldq + (H + Hkv + kvh) * HD, sub, nullptr, nullptr, 0, nv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      nkp[j] = pack2bf(nk[2 * j], nk[2 * j + 1]);
+      nvp[j] = pack2bf(nv[2 * j], nv[2 * j + 1]);
+    }
+  }
+  // ---- K: MFMA tiles t = wave + NW*i (lane loads key row t*16 + hj, dims
+  // (c4 + 4m)*8), or RS rows grp + GPB*u (dims sub*8)
+  bf16x8 ka[RS ? 1 : KT][NKC];
+  bf16x8 kr[KR];
+  if constexpr (!RS) {
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      const int kk = min((wave + NW * i) * 16 + hj, n - 1);
+#pragma unroll
+      for (int m = 0; m < NKC; ++m) {
+        const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)kk * HD + (c4 + 4 * m) * 8);
+        ka[i][m] = KNT ? __builtin_nontemporal_load(kp) : *kp;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
+      kr[u] = KNT ? __builtin_nontemporal_load(kp) : *kp;
+    }
+  }
+  // ---- first VE value rows (row grp + GPB*u, dims sub*8)
+  bf16x8 vr[VU];
+#pragma unroll
+  for (int u = 0; u < VE; ++u) {
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
+    vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- 2. scores (scaled to log2 units) + this wave's max per head
+  if constexpr (!RS) {
+    float mx = -INFINITY;  // lane's head hj
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      const int t = wave + NW * i;
+      if (t * 16 >= n) break;  // wave-uniform
+      if (FUSED && t * 16 + hj == knew) {
+#pragma unroll
+        for (int m = 0; m < NKC; ++m) ka[i][m] = nkA[m];
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < NKC; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[i][m], qB[m], acc, 0, 0, 0);
+      if (hj < G) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = t * 16 + c4 * 4 + r;
+          if (key < n) {
+            const float s = acc[r] * scale_log2;
+            sc[hj][key] = s;
+            mx = fmaxf(mx, s);
+          }
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (lane < G) wmax[wave][lane] = mx;
+  } else {
+    float mx[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) mx[g] = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      if (GPB * u >= n) break;  // workgroup-uniform
+      const int row = grp + GPB * u;
+      uint32_t kp[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kp[j] = (uint32_t)(uint16_t)kr[u][2 * j] | ((uint32_t)(uint16_t)kr[u][2 * j + 1] << 16);
+      if (FUSED && row == knew) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kp[j] = nkp[j];
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qp[g][j]), __builtin_bit_cast(bf16x2v, kp[j]),
+                                              d, false);
+        d = group_sum<LPK>(d) * scale_log2;
+        if (row < n) {
+          if (sub == 0) sc[g][row] = d;
+          mx[g] = fmaxf(mx[g], d);
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float m = wave_max(mx[g]);
+      if (lane == 0) wmax[wave][g] = m;
+    }
+  }
+  // ---- 3. the remaining value rows (the K registers are free now)
+#pragma unroll
+  for (int u = VE; u < VU; ++u) {
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
+    vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  float mg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float m = wmax[0][g];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, wmax[w][g]);
+    mg[g] = m;
+  }
+  // ---- 4. P.V: key pairs (u, u+1) share this thread's 8 dims
+  float acc[G][8], ls[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    ls[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < VU; u += 2) {
+    if (GPB * u >= n) break;  // workgroup-uniform
+    const int ka_ = grp + GPB * u, kz = ka_ + GPB;
+    uint32_t wa[4], wz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
+      wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
+    }
+    if (FUSED && ka_ == knew) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wa[j] = nvp[j];
+    }
+    if (FUSED && kz == knew) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wz[j] = nvp[j];
+    }
+    uint32_t prr[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      prr[2 * j] = __builtin_amdgcn_perm(wz[j], wa[j], 0x05040100u);
+      prr[2 * j + 1] = __builtin_amdgcn_perm(wz[j], wa[j], 0x07060302u);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float pa = ka_ < n ? __builtin_amdgcn_exp2f(sc[g][ka_] - mg[g]) : 0.f;
+      const float pz = kz < n ? __builtin_amdgcn_exp2f(sc[g][kz] - mg[g]) : 0.f;
+      ls[g] += pa + pz;
+      const bf16x2v pp = __builtin_bit_cast(bf16x2v, pack2bf(pa, pz));
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[g][j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2v, prr[j]), acc[g][j], false);
+    }
+  }
+  // ---- 5. reduce over the row groups
+  float* red = red1p;                       // [GPB][G][HD]
+  float* lred = red1p + GPB * G * HD;       // [GPB][G]
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    f32x4* dst = reinterpret_cast<f32x4*>(red + ((size_t)grp * G + g) * HD + sub * 8);
+    dst[0] = f32x4{acc[g][0], acc[g][1], acc[g][2], acc[g][3]};
+    dst[1] = f32x4{acc[g][4], acc[g][5], acc[g][6], acc[g][7]};
+    if (sub == 0) lred[grp * G + g] = ls[g];
+  }
+  __syncthreads();
+  for (int i = tid; i < G * HD; i += NTH) {
+    const int g = i / HD, d = i % HD;
+    float s = 0.f, l = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < GPB; ++r) {
+      s += red[((size_t)r * G + g) * HD + d];
+      l += lred[r * G + g];
+    }
+    if (NS == 1) {
+      o_direct[(size_t)b * H * HD + (kvh * G + g) * HD + d] = f2bf(l > 0.f ? s / l : 0.f);
+    } else {
+      wsp[g * (HD + 2) + d] = s;
+      if (d == 0) {
+        wsp[g * (HD + 2) + HD] = mg[g];
+        wsp[g * (HD + 2) + HD + 1] = l;
+      }
+    }
+  }
+  // the new key / value row into the cache, last (behind every K/V load of this wave)
+  if (own_new && grp == 0) {
+    uint4 wk, wv;
+    wk.x = nkp[0]; wk.y = nkp[1]; wk.z = nkp[2]; wk.w = nkp[3];
+    wv.x = nvp[0]; wv.y = nvp[1]; wv.z = nvp[2]; wv.w = nvp[3];
+    bf16_t* kr = kc + ((size_t)b * Hkv + kvh) * S * HD + (size_t)p_new * HD + sub * 8;
+    bf16_t* vrp = vc + ((size_t)b * Hkv + kvh) * S * HD + (size_t)p_new * HD + sub * 8;
+    *reinterpret_cast<uint4*>(kr) = wk;
+    *reinterpret_cast<uint4*>(vrp) = wv;
+  }
+}
+
 // (Folding this pass into the attention kernel — the last-arriving split
 // combines, tickets behind an agent-scope release / acquire — measured 20 %
 // slower on Llama-3 8B B=32 decode, 4.49 -> 5.39 ms/step: every split pays the
@@ -851,28 +1177,42 @@ extern "C" int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B
   return (int)hipGetLastError();
 }
 
+// K/V prefetch depth of the flash kernel: DNN_FLASH_PF=1/2 (A/B), default below
+static int flash_pf() {
+  const char* e = getenv("DNN_FLASH_PF");
+  return e != nullptr ? atoi(e) : 1;
+}
+template <int HD, bool QKV, bool KV8>
+static void launch_flash(int pf, dim3 grid, hipStream_t st, const bf16_t* q, const bf16_t* kc, const bf16_t* vc,
+                         bf16_t* o, int T, int H, int Hkv, int S, const int* pos, float sl2, int ldq, bf16_t* kco,
+                         bf16_t* vco) {
+  if (pf == 2)
+    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, 2>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos,
+                       sl2, ldq, kco, vco);
+  else
+    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, 1>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos,
+                       sl2, ldq, kco, vco);
+}
+
 extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,
                               int hd, int S, const int* pos, float scale, hipStream_t st, int kv8) {
   if (H % Hkv != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
+  const int pf = flash_pf();
+  const bf16_t *q_ = (const bf16_t*)q, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
+  bf16_t* o_ = (bf16_t*)o;
   if (kv8) {  // e4m3 cache: every key / value row widened as it is fetched
     if (hd == 64)
-      hipLaunchKernelGGL((flash_attn_kernel<64, false, true>), grid, dim3(256), 0, st, (const bf16_t*)q,
-                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+      launch_flash<64, false, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
     else if (hd == 128)
-      hipLaunchKernelGGL((flash_attn_kernel<128, false, true>), grid, dim3(256), 0, st, (const bf16_t*)q,
-                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+      launch_flash<128, false, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
     else
       return -2;
-    return (int)hipGetLastError();
-  }
-  if (hd == 64) {
-    hipLaunchKernelGGL((flash_attn_kernel<64>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
-                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+  } else if (hd == 64) {
+    launch_flash<64, false, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
   } else if (hd == 128) {
-    hipLaunchKernelGGL((flash_attn_kernel<128>), grid, dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)kc,
-                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2);
+    launch_flash<128, false, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
   } else {
     return -2;
   }
@@ -885,28 +1225,98 @@ extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc
   if (H % Hkv != 0 || ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
+  const int pf = flash_pf();
+  const bf16_t *q_ = (const bf16_t*)qkv, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
+  bf16_t *o_ = (bf16_t*)o, *ko = (bf16_t*)kc, *vo = (bf16_t*)vc;
   if (kv8) {  // e4m3 cache (unit scale)
     if (hd == 64)
-      hipLaunchKernelGGL((flash_attn_kernel<64, true, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
-                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc,
-                         (bf16_t*)vc);
+      launch_flash<64, true, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
     else if (hd == 128)
-      hipLaunchKernelGGL((flash_attn_kernel<128, true, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
-                         (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc,
-                         (bf16_t*)vc);
+      launch_flash<128, true, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
     else
       return -2;
-    return (int)hipGetLastError();
-  }
-  if (hd == 64) {
-    hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)kc,
-                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc, (bf16_t*)vc);
+  } else if (hd == 64) {
+    launch_flash<64, true, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
   } else if (hd == 128) {
-    hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)kc,
-                       (const bf16_t*)vc, (bf16_t*)o, T, H, Hkv, S, pos, sl2, ldqkv, (bf16_t*)kc, (bf16_t*)vc);
+    launch_flash<128, true, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
   } else {
     return -2;
   }
+  return (int)hipGetLastError();
+}
+
+struct Dec1pArgs {
+  const bf16_t* q;
+  int ldq;
+  bf16_t *kc, *vc;
+  float* ws;
+  int H, Hkv, S;
+  const int* lens;
+  const float *cosT, *sinT;
+  float sl2;
+  bf16_t* o;
+};
+template <int HD, int G, int NW, int KT, int VE, int VU, bool RS, int FM, bool NT, bool KNT>
+static void launch_1p_k(const Dec1pArgs& a, dim3 grid, hipStream_t st) {
+  constexpr int GPB = NW * 64 / (HD / 8);
+  const size_t smem = sizeof(float) * (size_t)GPB * G * (HD + 1);
+  hipLaunchKernelGGL((attn_decode_1p_kernel<HD, G, FM, NT, NW, KT, VE, VU, RS, KNT>), grid, dim3(NW * 64), smem, st,
+                     a.q, a.ldq, a.kc, a.vc, a.ws, a.H, a.Hkv, a.S, a.lens, a.cosT, a.sinT, a.sl2, a.o);
+}
+template <int HD, int G, int NW, int KT, int VE, int VU, bool RS, int FM>
+static void launch_1p_f(const Dec1pArgs& a, bool nt, bool knt, dim3 grid, hipStream_t st) {
+  if (!nt)
+    launch_1p_k<HD, G, NW, KT, VE, VU, RS, FM, false, false>(a, grid, st);
+  else if (knt)
+    launch_1p_k<HD, G, NW, KT, VE, VU, RS, FM, true, true>(a, grid, st);
+  else
+    launch_1p_k<HD, G, NW, KT, VE, VU, RS, FM, true, false>(a, grid, st);
+}
+template <int HD, int G, int NW, int KT, int VE, int VU, bool RS>
+static void launch_1p(const Dec1pArgs& a, int fm, bool nt, bool knt, dim3 grid, hipStream_t st) {
+  if (fm == 2)
+    launch_1p_f<HD, G, NW, KT, VE, VU, RS, 2>(a, nt, knt, grid, st);
+  else if (fm == 1)
+    launch_1p_f<HD, G, NW, KT, VE, VU, RS, 1>(a, nt, knt, grid, st);
+  else
+    launch_1p_f<HD, G, NW, KT, VE, VU, RS, 0>(a, nt, knt, grid, st);
+}
+
+// One-pass decode attention (bf16 cache): returns 1 when the shape is not
+// covered (the caller falls back to the batched kernel).  Splits of at most
+// DEC1P_CAP keys; more than one split only when the caller's workspace holds
+// them; grids below 128 workgroups keep the split-K kernel (its splits fill
+// the chip at batch 1).
+constexpr int DEC1P_CAP = 640;
+static int attn_decode_1p_launch(const void* q, int ldq, void* kc, void* vc, void* o, int B, int H, int Hkv, int hd,
+                                 int S, const int* lens, const float* cosT, const float* sinT, float sl2, int splits,
+                                 float* ws, int fm, bool nt, bool force, hipStream_t st) {
+  const int G = H / Hkv;
+  const int ns = (S + DEC1P_CAP - 1) / DEC1P_CAP;
+  if (ns > 1 && ns > splits) return 1;
+  if (!force && (long)B * Hkv * ns < 128) return 1;
+  dim3 grid(B * Hkv, ns);
+  // row-layout scores for MHA, MFMA key tiles for GQA: at MHA hd 64 an MFMA tile
+  // uses 1 of 16 head columns and its half-row key loads ran 10 % slower than
+  // whole rows (GPT-2 B=64 22.0 vs 19.9 us, profiles/r3_attn_1p_probe.jsonl)
+  const char* rs_e = getenv("DNN_DECODE_1P_RS");    // A/B override: 0 MFMA tiles, 1 row layout
+  const char* kn_e = getenv("DNN_DECODE_1P_KNT");   // key loads non-temporal (A/B; default: as the values)
+  const bool rs = rs_e != nullptr ? atoi(rs_e) == 1 : G == 1;
+  const bool knt = nt && !(kn_e != nullptr && atoi(kn_e) == 0);
+  Dec1pArgs a{(const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, (bf16_t*)o};
+  // hd 128 GQA (Llama-3 G = 4, llama3-tiny G = 2): 8 waves x 5 key tiles; hd 64 MHA (GPT-2): 4 waves x 10
+  if (hd == 128 && G == 4)
+    launch_1p<128, 4, 8, 5, 8, 20, false>(a, fm, nt, knt, grid, st);
+  else if (hd == 128 && G == 2)
+    launch_1p<128, 2, 8, 5, 8, 20, false>(a, fm, nt, knt, grid, st);
+  else if (hd == 64 && G == 1 && rs)
+    launch_1p<64, 1, 4, 10, 2, 20, true>(a, fm, nt, knt, grid, st);
+  else if (hd == 64 && G == 1)
+    launch_1p<64, 1, 4, 10, 6, 20, false>(a, fm, nt, knt, grid, st);
+  else
+    return 1;
+  if (ns > 1)
+    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, ns);
   return (int)hipGetLastError();
 }
 
@@ -915,6 +1325,19 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
                               float* ws, bool fused, hipStream_t st, bool kv8 = false) {
   const int G = H / Hkv;
   if (H % Hkv != 0 || G > DEC_MAXG || splits <= 0) return -1;
+  if (!kv8) {
+    // DNN_DECODE_1P=0 keeps the batched kernel everywhere (A/B), =2 takes the
+    // one-pass kernel on small grids too (tests)
+    const char* e1 = getenv("DNN_DECODE_1P");
+    const int m1 = e1 != nullptr ? atoi(e1) : 1;
+    if (m1 != 0) {
+      const bool nt1 = (double)B * Hkv * S * hd * 4.0 > 32.0 * 1024 * 1024;
+      const int r = attn_decode_1p_launch(q, ldq, kc, vc, o, B, H, Hkv, hd, S, lens, cosT, sinT,
+                                          scale * 1.4426950408889634f, splits, ws,
+                                          fused ? (cosT != nullptr ? 2 : 1) : 0, nt1, m1 == 2, st);
+      if (r != 1) return r;
+    }
+  }
   if (kv8 && G != 1 && hd != 128) return -4;  // e4m3 cache: MHA, or GQA at hd 128 (Llama-3)
   const int chunk_cap = (S + splits - 1) / splits;
   const int gpb = 256 / (hd / (kv8 ? 16 : 8));

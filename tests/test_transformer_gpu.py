@@ -116,6 +116,35 @@ def test_flash_attn_qkv_matches_split(B, Tn, H, Hkv, hd, pos0):
     assert torch.equal(out[rows], ref[rows])
 
 
+@pytest.mark.parametrize("B,Tn,H,Hkv,hd,pos0", [(2, 64, 4, 4, 64, 0), (3, 200, 12, 12, 64, 0), (2, 77, 8, 2, 128, 0),
+                                                 (1, 33, 4, 1, 128, 40), (3, 130, 2, 2, 64, 17), (2, 517, 4, 2, 64, 0)])
+def test_flash_prefetch_depth_bit_identical(B, Tn, H, Hkv, hd, pos0, monkeypatch):
+    """K/V prefetch two blocks ahead (DNN_FLASH_PF=2) is the same arithmetic as one
+    block ahead: outputs and written caches bit-identical, head-major and QKV mode."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(4)
+    S = pos0 + Tn + 8
+    kc0 = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc0 = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    qkv = torch.randn(B * Tn, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    pos = torch.full((B,), pos0, device=DEV, dtype=torch.int32)
+    q = torch.empty(B * H * Tn * hd, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for pf in ("1", "2"):
+        monkeypatch.setenv("DNN_FLASH_PF", pf)
+        kc, vc = kc0.clone(), vc0.clone()
+        T.qkv_split(qkv, q, kc, vc, B, Tn, H, Hkv, hd, pos)
+        o1 = torch.empty(B * Tn, H * hd, device=DEV, dtype=torch.bfloat16)
+        T.flash_attn(q, kc, vc, o1, B, Tn, H, Hkv, hd, pos)
+        kc2, vc2 = kc0.clone(), vc0.clone()
+        o2 = torch.empty_like(o1)
+        T.flash_attn_qkv(qkv, kc2, vc2, o2, B, Tn, H, Hkv, hd, pos)
+        outs.append((o1, o2, kc2, vc2))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 def test_flash_attn_spike_rescale():
     """Force the online-softmax rescale: one huge key score late in the sequence (guide §5.4 rule 26)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
@@ -132,16 +161,28 @@ def test_flash_attn_spike_rescale():
     assert _rel(out, ref) < 2e-2
 
 
+def _decode_path(monkeypatch, path):
+    """'0' / '1': the batched kernel with DPP / MFMA scores; '1p': the one-pass
+    kernel, forced onto grids of any size."""
+    if path in ("1p", "1p_rs"):
+        monkeypatch.setenv("DNN_DECODE_1P", "2")
+        monkeypatch.setenv("DNN_DECODE_1P_RS", "1" if path == "1p_rs" else "0")
+    else:
+        monkeypatch.setenv("DNN_DECODE_1P", "0")
+        monkeypatch.setenv("DNN_DECODE_MFMA", path)
+
+
 @pytest.mark.parametrize("B,H,Hkv,hd,S,lens", [(2, 12, 12, 64, 1024, [1, 700]), (3, 32, 8, 128, 2048, [5, 1000, 2048]),
                                                (1, 4, 2, 128, 300, [299]), (4, 25, 25, 64, 512, [17, 64, 65, 512]),
                                                (1, 32, 8, 128, 131072, [120001]),   # long context: LDS-bound splits
                                                (2, 12, 12, 64, 65536, [65536, 9000])])
-@pytest.mark.parametrize("mfma", ["0", "1"])
+@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs"])
 def test_attn_decode(B, H, Hkv, hd, S, lens, mfma, monkeypatch):
-    """Both score paths of the decode kernel: DPP row reductions and MFMA key
-    tiles (the GQA default), forced by DNN_DECODE_MFMA."""
+    """Both score paths of the batched decode kernel (DPP row reductions and
+    MFMA key tiles, forced by DNN_DECODE_MFMA) and the one-pass kernel (forced
+    by DNN_DECODE_1P=2 on these small grids; long caches fall back)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
-    monkeypatch.setenv("DNN_DECODE_MFMA", mfma)
+    _decode_path(monkeypatch, mfma)
     torch.manual_seed(2)
     q = torch.randn(B, H, hd, device=DEV).bfloat16()
     kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
@@ -157,6 +198,56 @@ def test_attn_decode(B, H, Hkv, hd, S, lens, mfma, monkeypatch):
         k = kc[b, :, :n].float().repeat_interleave(H // Hkv, 0)
         v = vc[b, :, :n].float().repeat_interleave(H // Hkv, 0)
         s = torch.einsum("hd,hkd->hk", q[b].float(), k) / math.sqrt(hd)
+        ref = torch.einsum("hk,hkd->hd", s.softmax(-1), v).reshape(-1)
+        assert _rel(out[b], ref) < 2e-2, b
+
+
+@pytest.mark.parametrize("B,H,Hkv,hd,S,rope", [(32, 32, 8, 128, 600, True), (64, 12, 12, 64, 560, False),
+                                               (64, 25, 25, 64, 1300, False)])
+def test_attn_decode_one_pass_bench_shapes(B, H, Hkv, hd, S, rope, monkeypatch):
+    """The benchmark decode shapes (Llama-3 8B B=32, GPT-2 B=64, GPT-2 XL with a
+    cache past one 640-key split) take the one-pass kernel by default: fused
+    step vs the batched kernel and vs the fp32 softmax on ragged positions."""
+    from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(11)
+    kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv = torch.randn(B, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    p = torch.randint(0, S, (B,), device=DEV, dtype=torch.int32)
+    p[0], p[-1] = 0, S - 1
+    cos = sin = None
+    if rope:
+        import dataclasses
+        cfg = LLAMA_CONFIGS["llama3-tiny"]
+        cos, sin = rope_tables(dataclasses.replace(cfg, n_embd=hd * cfg.n_head), S)
+        cos, sin = cos.to(DEV), sin.to(DEV)
+    G = H // Hkv
+    splits = max(T.decode_splits(S, B, Hkv, G), -(-S // 640))
+    ws = torch.empty(B * Hkv * splits * G * (hd + 2), device=DEV)
+    out = torch.empty(B, H * hd, device=DEV, dtype=torch.bfloat16)
+    monkeypatch.delenv("DNN_DECODE_1P", raising=False)
+    T.attn_decode_qkv(qkv, kc, vc, out, B, H, Hkv, hd, p, ws, splits, cos, sin)
+    monkeypatch.setenv("DNN_DECODE_1P", "0")
+    out2 = torch.empty_like(out)
+    T.attn_decode_qkv(qkv, kc2, vc2, out2, B, H, Hkv, hd, p, ws, splits, cos, sin)
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert _rel(out, out2) < 5e-3
+    qr = qkv[:, :H * hd].view(B, H, hd).float()
+    if rope:
+        pc = p.long()
+        c, s_ = cos[pc], sin[pc]
+        h2 = hd // 2
+        x1, x2 = qr[..., :h2], qr[..., h2:]
+        qr = torch.cat([x1 * c[:, None] - x2 * s_[:, None], x2 * c[:, None] + x1 * s_[:, None]], -1)
+    qr = qr.bfloat16().float()
+    for b in list(range(0, B, 7)) + [B - 1]:
+        n = int(p[b]) + 1
+        k = kc[b, :, :n].float().repeat_interleave(G, 0)
+        v = vc[b, :, :n].float().repeat_interleave(G, 0)
+        s = torch.einsum("hd,hkd->hk", qr[b], k) / math.sqrt(hd)
         ref = torch.einsum("hk,hkd->hd", s.softmax(-1), v).reshape(-1)
         assert _rel(out[b], ref) < 2e-2, b
 
@@ -516,14 +607,14 @@ def test_linear_norm_strided_rows():
     (1, 32, 8, 128, 200, [150], True, 1), (3, 12, 12, 64, 300, [0, 17, 299], False, 2),
     (2, 8, 2, 128, 1024, [700, 1023], True, 4), (2, 4, 4, 64, 64, [63, 64], False, 1),
     (1, 32, 8, 128, 600, [140], True, 1), (1, 32, 8, 128, 600, [599], True, 3)])
-@pytest.mark.parametrize("mfma", ["0", "1"])
+@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs"])
 def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits, mfma, monkeypatch):
     """Fused decode step (split + RoPE + cache write + attention) == qkv_split
     then attn_decode, and the cache row it wrote matches; pos >= S (overflow)
     writes nothing and attends to the S cached keys."""
     from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
     from distributed_neural_networks_amd.ops import transformer_ops as T
-    monkeypatch.setenv("DNN_DECODE_MFMA", mfma)
+    _decode_path(monkeypatch, mfma)
     torch.manual_seed(9)
     kc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
     vc = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
