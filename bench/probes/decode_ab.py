@@ -40,8 +40,6 @@ def apply(switch: str, v: int) -> None:
         gemm.set_stream_gemm(v)
     elif switch == "decode_1p":  # one-pass decode attention: 0 batched kernel, 1 default, 2 forced (attention.hip)
         os.environ["DNN_DECODE_1P"] = str(v)
-    elif switch == "flash_pf":  # flash prefill K/V prefetch depth in blocks (attention.hip flash_pf)
-        os.environ["DNN_FLASH_PF"] = str(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

@@ -50,14 +50,9 @@ def main():
         ref = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)  # noqa: E731
         flop = 4.0 * B * H * T * T * hd / 2
         t_o, t_r = timeit(ours), timeit(ref)
-        pfs = {}
-        for pf in (1, 2):  # prefetch-depth A/B in the same process (attention.hip flash_pf)
-            os.environ["DNN_FLASH_PF"] = str(pf)
-            pfs[f"pf{pf}_ms"] = round(min(timeit(ours) for _ in range(3)), 4)
-        os.environ.pop("DNN_FLASH_PF", None)
         print(json.dumps({"B": B, "T": T, "H": H, "Hkv": Hkv, "hd": hd, "ours_ms": round(t_o, 4),
                           "ours_tflops": round(flop / t_o / 1e9, 1), "torch_sdpa_ms": round(t_r, 4),
-                          "torch_tflops": round(flop / t_r / 1e9, 1), **pfs}), flush=True)
+                          "torch_tflops": round(flop / t_r / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -149,7 +149,7 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
-template <int HD, bool QKV = false, bool KV8 = false, int PF = 1>
+template <int HD, bool QKV = false, bool KV8 = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
@@ -222,14 +222,14 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   const bf16_t* kbase = kc + ((size_t)b * Hkv + kvh) * S * HD;
   const bf16_t* vbase = vc + ((size_t)b * Hkv + kvh) * S * HD;
 
-  // K/V blocks are register-prefetched PF blocks ahead: block kb0 + PF*64 is
-  // fetched from global memory while block kb0 is computed, then written to LDS
-  // after the trailing barrier.  PF = 1 left the loop waiting on its fetch: at
-  // GPT-2 prefill (768 workgroups of 128 queries x 2-8 blocks) a block's MFMA +
-  // softmax work (~1 us) is shorter than the loaded-chip global latency, and the
-  // PMC showed the MFMA pipe 11 % busy, VALU 30 %, the waves waiting the rest.
+  // K/V blocks are register double-buffered: block kb0+64 is fetched from
+  // global memory while block kb0 is computed, then written to LDS after the
+  // trailing barrier.  (Fetching two blocks ahead measured neutral at GPT-2
+  // prefill, 0.1058 -> 0.1051 ms, and slower at hd 128, 1.121 -> 1.218 ms at
+  // T = 4096: profiles/r3_flash_prefetch_depth.jsonl.  The PMC there: MFMA
+  // pipe 11 % busy, VALU ~30 %, waves waiting the rest.)
   constexpr int NIT = (FA_KB * CH) / 256;
-  i32x4 pkA[NIT], pvA[NIT], pkB[NIT], pvB[NIT];  // ext vectors: uint4 structs do not promote out of scratch
+  i32x4 pkA[NIT], pvA[NIT];  // ext vectors: uint4 structs do not promote out of scratch
   auto fetch = [&](int kb0, i32x4(&pk)[NIT], i32x4(&pv)[NIT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       *reinterpret_cast<i32x4*>(vs + key * SM::V_STRIDE + c * 16) = pv[it];
     }
     __syncthreads();
-    if (kb0 + PF * FA_KB < kv_end) fetch(kb0 + PF * FA_KB, pk, pv);
+    if (kb0 + FA_KB < kv_end) fetch(kb0 + FA_KB, pk, pv);
     if (kb0 <= wave_qmax) {
       // ---- S^T for two 32-key tiles ----
       f32x16 sacc[2];
@@ -357,17 +357,8 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
     }
     __syncthreads();
   };
-  if constexpr (PF == 1) {
-    if (kv_end > 0) fetch(0, pkA, pvA);
-    for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) block(kb0, pkA, pvA);
-  } else {
-    if (kv_end > 0) fetch(0, pkA, pvA);
-    if (FA_KB < kv_end) fetch(FA_KB, pkB, pvB);
-    for (int kb0 = 0; kb0 < kv_end; kb0 += 2 * FA_KB) {
-      block(kb0, pkA, pvA);
-      if (kb0 + FA_KB < kv_end) block(kb0 + FA_KB, pkB, pvB);
-    }
-  }
+  if (kv_end > 0) fetch(0, pkA, pvA);
+  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) block(kb0, pkA, pvA);
   // ---- normalise + store: lane = query, regs = d ----
   if (qrow < T) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
@@ -1177,21 +1168,11 @@ extern "C" int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B
   return (int)hipGetLastError();
 }
 
-// K/V prefetch depth of the flash kernel: DNN_FLASH_PF=1/2 (A/B), default below
-static int flash_pf() {
-  const char* e = getenv("DNN_FLASH_PF");
-  return e != nullptr ? atoi(e) : 1;
-}
 template <int HD, bool QKV, bool KV8>
-static void launch_flash(int pf, dim3 grid, hipStream_t st, const bf16_t* q, const bf16_t* kc, const bf16_t* vc,
-                         bf16_t* o, int T, int H, int Hkv, int S, const int* pos, float sl2, int ldq, bf16_t* kco,
-                         bf16_t* vco) {
-  if (pf == 2)
-    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, 2>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos,
-                       sl2, ldq, kco, vco);
-  else
-    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, 1>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos,
-                       sl2, ldq, kco, vco);
+static void launch_flash(dim3 grid, hipStream_t st, const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o,
+                         int T, int H, int Hkv, int S, const int* pos, float sl2, int ldq, bf16_t* kco, bf16_t* vco) {
+  hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos, sl2,
+                     ldq, kco, vco);
 }
 
 extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,
@@ -1199,20 +1180,19 @@ extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, voi
   if (H % Hkv != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
-  const int pf = flash_pf();
   const bf16_t *q_ = (const bf16_t*)q, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
   bf16_t* o_ = (bf16_t*)o;
   if (kv8) {  // e4m3 cache: every key / value row widened as it is fetched
     if (hd == 64)
-      launch_flash<64, false, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
+      launch_flash<64, false, true>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
     else if (hd == 128)
-      launch_flash<128, false, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
+      launch_flash<128, false, true>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
     else
       return -2;
   } else if (hd == 64) {
-    launch_flash<64, false, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
+    launch_flash<64, false, false>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
   } else if (hd == 128) {
-    launch_flash<128, false, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
+    launch_flash<128, false, false>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, 0, nullptr, nullptr);
   } else {
     return -2;
   }
@@ -1225,20 +1205,19 @@ extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc
   if (H % Hkv != 0 || ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
   dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
   const float sl2 = scale * 1.4426950408889634f;
-  const int pf = flash_pf();
   const bf16_t *q_ = (const bf16_t*)qkv, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
   bf16_t *o_ = (bf16_t*)o, *ko = (bf16_t*)kc, *vo = (bf16_t*)vc;
   if (kv8) {  // e4m3 cache (unit scale)
     if (hd == 64)
-      launch_flash<64, true, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
+      launch_flash<64, true, true>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
     else if (hd == 128)
-      launch_flash<128, true, true>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
+      launch_flash<128, true, true>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
     else
       return -2;
   } else if (hd == 64) {
-    launch_flash<64, true, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
+    launch_flash<64, true, false>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
   } else if (hd == 128) {
-    launch_flash<128, true, false>(pf, grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
+    launch_flash<128, true, false>(grid, st, q_, k_, v_, o_, T, H, Hkv, S, pos, sl2, ldqkv, ko, vo);
   } else {
     return -2;
   }
