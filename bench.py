@@ -531,9 +531,13 @@ def main():
         return gpt_bench.main(args)
     info = dist_setup(args.gpus, args.cpu)
     N = info.world
+    p2p = "none"
     if N > 1:
         from distributed_neural_networks_amd.parallel import comm
+        from distributed_neural_networks_amd.parallel.links import native_preflight
         comm.back_group()  # collective: the back-edge communicator (latency path, decode rings)
+        # native RCCL channels checked on a ring first; any failure -> ProcessGroupNCCL P2P
+        p2p = native_preflight(info.device)
     args._cut = pick_cut(args, info)
     spare = args.s0_spare_cus if args.s0_spare_cus >= 0 else (16 if N > 1 else 0)
     if info.device.type != "cuda":
@@ -574,7 +578,7 @@ def main():
                        "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
                        "stages": 2, "microbatches": args.microbatches if N > 1 else 1,
                        "receiver_fill_images_per_step": fill,
-                       "stage0_spare_cus": spare,
+                       "stage0_spare_cus": spare, "p2p": p2p,
                        "stage_cut": {1: f"conv|fc (reference split, {hop_kib} KiB/img hop)",
                                      2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},
         }

@@ -99,6 +99,9 @@ def run(args=None, shutdown: bool = True):
         info = comm.init("gloo")
     elif N > 1 or "WORLD_SIZE" in os.environ:
         info = comm.init("nccl")
+        if info.world > 1:  # native RCCL channels checked on a ring; any failure -> ProcessGroupNCCL P2P
+            from distributed_neural_networks_amd.parallel.links import native_preflight
+            native_preflight(info.device)
     else:
         torch.cuda.set_device(0)
         info = comm.DistInfo(0, 1, 0, "none", torch.device("cuda", 0))

@@ -29,11 +29,13 @@ SHAPES = {  # name: (B, H, Hkv, hd, S capacity, pos, rope)
 VARIANTS = {  # name: env
     "batched": {"DNN_DECODE_1P": "0"},
     "1p": {"DNN_DECODE_1P": "1"},
-    "1p_kdef": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KNT": "0"},
-    "1p_rs": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_RS": "1"},
-    "1p_rs_kdef": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_RS": "1", "DNN_DECODE_1P_KNT": "0"},
+    "1p_kf0": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KF": "0"},
+    "1p_kf1": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KF": "1"},
+    "1p_knt0": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KNT": "0"},
+    "1p_knt1": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KNT": "1"},
+    "1p_rs0": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_RS": "0"},
 }
-KEYS = ("DNN_DECODE_1P", "DNN_DECODE_1P_KNT", "DNN_DECODE_1P_RS")
+KEYS = ("DNN_DECODE_1P", "DNN_DECODE_1P_KNT", "DNN_DECODE_1P_RS", "DNN_DECODE_1P_KF")
 
 
 def main():

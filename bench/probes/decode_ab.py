@@ -40,6 +40,10 @@ def apply(switch: str, v: int) -> None:
         gemm.set_stream_gemm(v)
     elif switch == "decode_1p":  # one-pass decode attention: 0 batched kernel, 1 default, 2 forced (attention.hip)
         os.environ["DNN_DECODE_1P"] = str(v)
+    elif switch == "decode_1p_kf":  # one-pass decode attention: K/V loads issued before q (attention.hip KF)
+        os.environ["DNN_DECODE_1P_KF"] = str(v)
+    elif switch == "rowstats_r":  # prefill row statistics rows per wave (norm_embed.hip dnn_row_stats)
+        os.environ["DNN_ROWSTATS_R"] = str(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

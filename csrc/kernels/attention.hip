@@ -834,7 +834,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 //      split) or as the (o, m, l) partial decode_combine_kernel merges.
 // Cache rows past the runtime length are never scored: their loads are
 // clamped to the last valid row (same address: coalesced).
-template <int HD, int G, int FM, bool NT, int NW, int KT, int VE, int VU, bool RS = false, bool KNT = NT>
+template <int HD, int G, int FM, bool NT, int NW, int KT, int VE, int VU, bool RS = false, bool KNT = NT,
+          bool KF = false>
 __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* __restrict__ q, int ldq,
                                                                bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                                                float* __restrict__ ws, int H, int Hkv, int S,
@@ -854,7 +855,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
   constexpr int KR = RS ? VU : 1;      // key rows per thread (RS)
   static_assert(GPB * VU >= CAP, "value rows must cover the key tiles");
   static_assert(VE <= VU && VU % 2 == 0 && G <= 16, "bad shape");
-  __shared__ float sc[G][CAP];         // scaled scores
+  __shared__ __attribute__((aligned(16))) float sc[CAP * G];  // scaled scores, [key][head] (one LDS read per key)
   __shared__ float wmax[NW][G];        // per-wave score max per head
   extern __shared__ __attribute__((aligned(16))) float red1p[];  // [GPB][G][HD] + [GPB][G]
 
@@ -878,6 +879,43 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
   const bool own_new = FUSED && p_new < S && p_new >= k0 && p_new < k1;
   const int knew = own_new ? p_new - k0 : -1;
   const int pr = min(p_new, S - 1);
+
+  // ---- K: MFMA tiles t = wave + NW*i (lane loads key row t*16 + hj, dims
+  // (c4 + 4m)*8), or RS rows grp + GPB*u (dims sub*8); then the first VE value
+  // rows (row grp + GPB*u, dims sub*8).  KF: issued before q, so the K/V
+  // stream starts without waiting for q (and the RoPE tables); q then lands
+  // behind them in the vmcnt queue, which the scores wait for anyway
+  bf16x8 ka[RS ? 1 : KT][NKC];
+  bf16x8 kr[KR];
+  bf16x8 vr[VU];
+  auto issue_kv = [&]() __attribute__((always_inline)) {
+    if constexpr (!RS) {
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        const int kk = min((wave + NW * i) * 16 + hj, n - 1);
+#pragma unroll
+        for (int m = 0; m < NKC; ++m) {
+          const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)kk * HD + (c4 + 4 * m) * 8);
+          ka[i][m] = KNT ? __builtin_nontemporal_load(kp) : *kp;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
+        kr[u] = KNT ? __builtin_nontemporal_load(kp) : *kp;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < VE; ++u) {
+      const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
+      vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
+    }
+  };
+  if constexpr (KF) {
+    issue_kv();
+    __builtin_amdgcn_sched_barrier(0);
+  }
 
   // ---- 1. q (MFMA: q^T B operand with columns >= G zero, new key in A layout;
   // RS: bf16 pairs of this thread's 8 dims per head), new k/v (row layout)
@@ -930,34 +968,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
       nvp[j] = pack2bf(nv[2 * j], nv[2 * j + 1]);
     }
   }
-  // ---- K: MFMA tiles t = wave + NW*i (lane loads key row t*16 + hj, dims
-  // (c4 + 4m)*8), or RS rows grp + GPB*u (dims sub*8)
-  bf16x8 ka[RS ? 1 : KT][NKC];
-  bf16x8 kr[KR];
-  if constexpr (!RS) {
-#pragma unroll
-    for (int i = 0; i < KT; ++i) {
-      const int kk = min((wave + NW * i) * 16 + hj, n - 1);
-#pragma unroll
-      for (int m = 0; m < NKC; ++m) {
-        const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)kk * HD + (c4 + 4 * m) * 8);
-        ka[i][m] = KNT ? __builtin_nontemporal_load(kp) : *kp;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int u = 0; u < KR; ++u) {
-      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
-      kr[u] = KNT ? __builtin_nontemporal_load(kp) : *kp;
-    }
-  }
-  // ---- first VE value rows (row grp + GPB*u, dims sub*8)
-  bf16x8 vr[VU];
-#pragma unroll
-  for (int u = 0; u < VE; ++u) {
-    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vb + (size_t)min(grp + GPB * u, n - 1) * HD + sub * 8);
-    vr[u] = NT ? __builtin_nontemporal_load(vp) : *vp;
-  }
+  if constexpr (!KF) issue_kv();
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- 2. scores (scaled to log2 units) + this wave's max per head
@@ -980,7 +991,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
           const int key = t * 16 + c4 * 4 + r;
           if (key < n) {
             const float s = acc[r] * scale_log2;
-            sc[hj][key] = s;
+            sc[key * G + hj] = s;
             mx = fmaxf(mx, s);
           }
         }
@@ -1013,7 +1024,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
                                               d, false);
         d = group_sum<LPK>(d) * scale_log2;
         if (row < n) {
-          if (sub == 0) sc[g][row] = d;
+          if (sub == 0) sc[row * G + g] = d;
           mx[g] = fmaxf(mx[g], d);
         }
       }
@@ -1040,7 +1051,20 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
     for (int w = 1; w < NW; ++w) m = fmaxf(m, wmax[w][g]);
     mg[g] = m;
   }
-  // ---- 4. P.V: key pairs (u, u+1) share this thread's 8 dims
+  // ---- 4. probabilities, once per (key, head): the whole workgroup
+  // exponentiates the score array in place (a thread of P.V would otherwise
+  // take the same exponential as the other LPK - 1 lanes of its row)
+  for (int i = tid; i < n * G; i += NTH) {
+    const int g = i % G;
+    float m = mg[0];
+#pragma unroll
+    for (int gg = 1; gg < G; ++gg) m = g == gg ? mg[gg] : m;
+    sc[i] = __builtin_amdgcn_exp2f(sc[i] - m);
+  }
+  __syncthreads();
+  // ---- 5. P.V: key pairs (u, u+1) share this thread's 8 dims; the
+  // probabilities of 4 rows are read together (one ds_read per row) so the
+  // LDS round trips overlap instead of one read -> wait -> use per head
   float acc[G][8], ls[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -1048,42 +1072,63 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
+  static_assert(VU % 4 == 0, "P.V reads probabilities 4 rows at a time");
 #pragma unroll
-  for (int u = 0; u < VU; u += 2) {
-    if (GPB * u >= n) break;  // workgroup-uniform
-    const int ka_ = grp + GPB * u, kz = ka_ + GPB;
-    uint32_t wa[4], wz[4];
+  for (int u0 = 0; u0 < VU; u0 += 4) {
+    if (GPB * u0 >= n) break;  // workgroup-uniform
+    float pr4[4][G];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
-      wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
-    }
-    if (FUSED && ka_ == knew) {
+    for (int q = 0; q < 4; ++q) {
+      const int row = grp + GPB * (u0 + q);
+      const float* sp = sc + min(row, n - 1) * G;
+      if constexpr (G == 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(sp);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wa[j] = nvp[j];
-    }
-    if (FUSED && kz == knew) {
+        for (int g = 0; g < 4; ++g) pr4[q][g] = row < n ? v[g] : 0.f;
+      } else if constexpr (G == 2) {
+        const f32x2 v = *reinterpret_cast<const f32x2*>(sp);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wz[j] = nvp[j];
-    }
-    uint32_t prr[8];
+        for (int g = 0; g < 2; ++g) pr4[q][g] = row < n ? v[g] : 0.f;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      prr[2 * j] = __builtin_amdgcn_perm(wz[j], wa[j], 0x05040100u);
-      prr[2 * j + 1] = __builtin_amdgcn_perm(wz[j], wa[j], 0x07060302u);
+        for (int g = 0; g < G; ++g) pr4[q][g] = row < n ? sp[g] : 0.f;
+      }
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float pa = ka_ < n ? __builtin_amdgcn_exp2f(sc[g][ka_] - mg[g]) : 0.f;
-      const float pz = kz < n ? __builtin_amdgcn_exp2f(sc[g][kz] - mg[g]) : 0.f;
-      ls[g] += pa + pz;
-      const bf16x2v pp = __builtin_bit_cast(bf16x2v, pack2bf(pa, pz));
+    for (int u = u0; u < u0 + 4; u += 2) {
+      const int ka_ = grp + GPB * u, kz = ka_ + GPB;
+      uint32_t wa[4], wz[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[g][j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2v, prr[j]), acc[g][j], false);
+      for (int j = 0; j < 4; ++j) {
+        wa[j] = (uint32_t)(uint16_t)vr[u][2 * j] | ((uint32_t)(uint16_t)vr[u][2 * j + 1] << 16);
+        wz[j] = (uint32_t)(uint16_t)vr[u + 1][2 * j] | ((uint32_t)(uint16_t)vr[u + 1][2 * j + 1] << 16);
+      }
+      if (FUSED && ka_ == knew) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wa[j] = nvp[j];
+      }
+      if (FUSED && kz == knew) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wz[j] = nvp[j];
+      }
+      uint32_t prr[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        prr[2 * j] = __builtin_amdgcn_perm(wz[j], wa[j], 0x05040100u);
+        prr[2 * j + 1] = __builtin_amdgcn_perm(wz[j], wa[j], 0x07060302u);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pa = pr4[u - u0][g], pz = pr4[u - u0 + 1][g];
+        ls[g] += pa + pz;
+        const bf16x2v pp = __builtin_bit_cast(bf16x2v, pack2bf(pa, pz));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[g][j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2v, prr[j]), acc[g][j], false);
+      }
     }
   }
-  // ---- 5. reduce over the row groups
+  // ---- 6. reduce over the row groups
   float* red = red1p;                       // [GPB][G][HD]
   float* lred = red1p + GPB * G * HD;       // [GPB][G]
 #pragma unroll
@@ -1234,13 +1279,18 @@ struct Dec1pArgs {
   const float *cosT, *sinT;
   float sl2;
   bf16_t* o;
+  bool kf;  // K/V loads issued before q (attn_decode_1p_kernel KF)
 };
 template <int HD, int G, int NW, int KT, int VE, int VU, bool RS, int FM, bool NT, bool KNT>
 static void launch_1p_k(const Dec1pArgs& a, dim3 grid, hipStream_t st) {
   constexpr int GPB = NW * 64 / (HD / 8);
   const size_t smem = sizeof(float) * (size_t)GPB * G * (HD + 1);
-  hipLaunchKernelGGL((attn_decode_1p_kernel<HD, G, FM, NT, NW, KT, VE, VU, RS, KNT>), grid, dim3(NW * 64), smem, st,
-                     a.q, a.ldq, a.kc, a.vc, a.ws, a.H, a.Hkv, a.S, a.lens, a.cosT, a.sinT, a.sl2, a.o);
+  if (a.kf)
+    hipLaunchKernelGGL((attn_decode_1p_kernel<HD, G, FM, NT, NW, KT, VE, VU, RS, KNT, true>), grid, dim3(NW * 64),
+                       smem, st, a.q, a.ldq, a.kc, a.vc, a.ws, a.H, a.Hkv, a.S, a.lens, a.cosT, a.sinT, a.sl2, a.o);
+  else
+    hipLaunchKernelGGL((attn_decode_1p_kernel<HD, G, FM, NT, NW, KT, VE, VU, RS, KNT, false>), grid, dim3(NW * 64),
+                       smem, st, a.q, a.ldq, a.kc, a.vc, a.ws, a.H, a.Hkv, a.S, a.lens, a.cosT, a.sinT, a.sl2, a.o);
 }
 template <int HD, int G, int NW, int KT, int VE, int VU, bool RS, int FM>
 static void launch_1p_f(const Dec1pArgs& a, bool nt, bool knt, dim3 grid, hipStream_t st) {
@@ -1281,9 +1331,16 @@ static int attn_decode_1p_launch(const void* q, int ldq, void* kc, void* vc, voi
   const char* rs_e = getenv("DNN_DECODE_1P_RS");    // A/B override: 0 MFMA tiles, 1 row layout
   const char* kn_e = getenv("DNN_DECODE_1P_KNT");   // key loads non-temporal (A/B; default: as the values)
   const bool rs = rs_e != nullptr ? atoi(rs_e) == 1 : G == 1;
-  const bool knt = nt && !(kn_e != nullptr && atoi(kn_e) == 0);
-  Dec1pArgs a{(const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, (bf16_t*)o};
+  // key loads: non-temporal for MHA, default policy for GQA (Llama-3 B=32
+  // 19.54 -> 19.11 us; GPT-2 B=64 19.28 -> 20.01 the other way)
+  const bool knt = nt && (kn_e != nullptr ? atoi(kn_e) != 0 : G == 1);
+  // K/V loads before q for GQA (Llama-3 B=32 19.40 -> 19.12 us, decode 3.930 -> 3.902 ms/step), after q for
+  // MHA (GPT-2 B=64 19.50 -> 19.91 us the other way; profiles/r3_attn_1p_probe_v3.jsonl)
+  const char* kf_e = getenv("DNN_DECODE_1P_KF");    // A/B override: 1 before q, 0 after
+  const bool kf = kf_e != nullptr ? atoi(kf_e) == 1 : G > 1;
+  Dec1pArgs a{(const bf16_t*)q, ldq, (bf16_t*)kc, (bf16_t*)vc, ws, H, Hkv, S, lens, cosT, sinT, sl2, (bf16_t*)o, kf};
   // hd 128 GQA (Llama-3 G = 4, llama3-tiny G = 2): 8 waves x 5 key tiles; hd 64 MHA (GPT-2): 4 waves x 10
+  // (row-layout scores for GQA measured 22.3 vs 19.0 us at Llama-3 B=32: not built)
   if (hd == 128 && G == 4)
     launch_1p<128, 4, 8, 5, 8, 20, false>(a, fm, nt, knt, grid, st);
   else if (hd == 128 && G == 2)

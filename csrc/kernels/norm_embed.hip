@@ -9,6 +9,8 @@
 // memory so one HIP graph serves every decode step.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dnn {
 
 template <int NC, bool RMS>
@@ -95,39 +97,47 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16_t* __restrict__ x,
 // mean / variance (no E[x^2] - mean^2 cancellation); writes {rstd, -mean rstd}
 // per row (RMS: {rstd, 0}).  Reads the activation once and writes 8 B per row
 // instead of the normalised copy the norm kernel writes and the GEMM re-reads.
-template <int NC, bool RMS>
+//
+// R rows per wave (prefill, M in the tens of thousands): all R rows' loads are
+// issued before the first reduction, so a wave pays one load round trip for R
+// rows and the grid is R times smaller — one row per wave left 32768 waves in
+// four residency rounds of a latency-bound load + two wave sums each.
+template <int NC, bool RMS, int R = 1>
 __global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict__ x, int ldx, float2* __restrict__ st,
                                                         int M, int N, float eps) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const bf16_t* xr = x + (size_t)row * ldx;
-  float v[NC][8];
-  float s = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
+  bf16x8 raw[R][NC];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < N) {
-      const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+  for (int r = 0; r < R; ++r) {
+    const bf16_t* xr = x + (size_t)min(row0 + r, M - 1) * ldx;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      raw[r][i] = c < N ? *reinterpret_cast<const bf16x8*>(xr + c) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-  const float mean = RMS ? 0.f : wave_sum(s) / N;
-  float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < N) {
+  for (int r = 0; r < R; ++r) {
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
+    for (int i = 0; i < NC; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += bf2f_s(raw[r][i][j]);
+    const float mean = RMS ? 0.f : wave_sum(s) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = bf2f_s(raw[r][i][j]) - mean; q += d * d; }
+      }
     }
+    const float rstd = rsqrtf(wave_sum(q) / N + eps);
+    if (lane == 0 && row0 + r < M) st[row0 + r] = make_float2(rstd, -mean * rstd);
   }
-  const float rstd = rsqrtf(wave_sum(q) / N + eps);
-  if (lane == 0) st[row] = make_float2(rstd, -mean * rstd);
 }
 
 // Normalise + quantise in one pass (fp8 prefill): the normalised row (fp32,
@@ -257,13 +267,26 @@ extern "C" int dnn_layernorm(const void* x, int ldx, const float* w, const float
 extern "C" int dnn_row_stats(const void* x, int ldx, float* stats, int M, int N, float eps, int rms, hipStream_t st) {
   if (N % 8 != 0 || N > 8192 || M <= 0) return M <= 0 ? 0 : -1;
   const int nc = (N / 8 + 63) / 64;
-  dim3 grid((M + 3) / 4), blk(256);
+  // 4 rows per wave once the grid would exceed one residency round (8192 waves);
+  // DNN_ROWSTATS_R=1 forces one row per wave (A/B)
+  const char* re = getenv("DNN_ROWSTATS_R");
+  const int R = re != nullptr ? atoi(re) : (M >= 8192 && nc <= 4 ? 4 : 1);
+  dim3 blk(256);
 #define L(NCV)                                                                                                       \
   if (nc <= NCV) {                                                                                                   \
-    if (rms) hipLaunchKernelGGL((row_stats_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx,             \
-                                reinterpret_cast<float2*>(stats), M, N, eps);                                        \
-    else hipLaunchKernelGGL((row_stats_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx,                \
-                            reinterpret_cast<float2*>(stats), M, N, eps);                                            \
+    if (R == 4 && NCV <= 4) {                                                                                        \
+      dim3 grid((M + 15) / 16);                                                                                      \
+      if (rms) hipLaunchKernelGGL((row_stats_kernel<NCV, true, 4>), grid, blk, 0, st, (const bf16_t*)x, ldx,        \
+                                  reinterpret_cast<float2*>(stats), M, N, eps);                                      \
+      else hipLaunchKernelGGL((row_stats_kernel<NCV, false, 4>), grid, blk, 0, st, (const bf16_t*)x, ldx,           \
+                              reinterpret_cast<float2*>(stats), M, N, eps);                                          \
+    } else {                                                                                                         \
+      dim3 grid((M + 3) / 4);                                                                                        \
+      if (rms) hipLaunchKernelGGL((row_stats_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx,           \
+                                  reinterpret_cast<float2*>(stats), M, N, eps);                                      \
+      else hipLaunchKernelGGL((row_stats_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx,              \
+                              reinterpret_cast<float2*>(stats), M, N, eps);                                          \
+    }                                                                                                                \
     return (int)hipGetLastError();                                                                                   \
   }
   L(1) L(2) L(4) L(8) L(16)

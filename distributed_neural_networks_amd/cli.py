@@ -407,6 +407,11 @@ def run_dist(ctx: NodeContext, args, device) -> int:
         torch.cuda.set_device(device)
         info = dataclasses.replace(info, device=device)
     comm.back_group()  # collective: the back-edge's own communicator
+    if pipe.transport == "rccl":
+        from .parallel.links import native_preflight
+        mode = native_preflight(info.device)
+        if mode != "native":
+            log(f"[{nid}] stage hops: {mode}")
     fam = model_info(pipe.model).family
     # the watchdog runs from here on, so a rank that fails while loading its
     # weights takes the pipeline down within heartbeat_timeout_s instead of

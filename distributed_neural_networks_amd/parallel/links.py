@@ -247,6 +247,61 @@ def make_link(peer: int, device: torch.device, group=None) -> P2PLink:
     return P2PLink(peer, device, group)
 
 
+_PREFLIGHT_SEQ = [0]
+
+
+def native_preflight(device: torch.device, timeout_s: float = 90.0, store=None) -> str:
+    """Check the native RCCL channels before a multi-GPU run and fall back to
+    ProcessGroupNCCL P2P when they do not work, so a run still produces its
+    numbers: every rank exchanges 16 bytes with both ring neighbours over its
+    own pair channels (even ranks send first, odd ranks receive first, so the
+    two ops of a 2-rank ring on one channel match), each op bounded by
+    ``timeout_s``.  The verdict is agreed through the process group's TCP
+    store (no collective: it must work when RCCL itself is what failed).  Any
+    failure on any rank aborts the native channels and sets
+    ``DNN_P2P=torch`` on every rank.  Returns the mode in effect:
+    ``"native"``, ``"torch (native preflight failed: ...)"``, or the backend
+    name when native channels do not apply (gloo, one rank, CPU)."""
+    if not dist.is_initialized() or dist.get_world_size() < 2:
+        return "none"
+    if dist.get_backend() != "nccl" or device.type != "cuda":
+        return dist.get_backend()
+    if p2p_mode() != "native":
+        return p2p_mode()
+    r, n = dist.get_rank(), dist.get_world_size()
+    err = ""
+    try:
+        nxt, prv = make_link((r + 1) % n, device), make_link((r - 1) % n, device)
+        for link in (nxt, prv):
+            link.ch.ready(timeout_s)
+        a = torch.full((4,), r, dtype=torch.int32, device=device)
+        b = torch.full((4,), -1, dtype=torch.int32, device=device)
+        works = [nxt.isend(a), prv.irecv(b)] if r % 2 == 0 else [prv.irecv(b), nxt.isend(a)]
+        for w in works:
+            w.synchronize(timeout_s)
+        got = int(b[0].item())
+        if got != (r - 1) % n:
+            raise RuntimeError(f"ring payload {got}, expected {(r - 1) % n}")
+    except Exception as e:  # noqa: BLE001 — any failure means: fall back
+        err = f"rank {r}: {type(e).__name__}: {e}"[:200]
+    from . import rccl
+    st = store or rccl._store()
+    seq = _PREFLIGHT_SEQ[0]
+    _PREFLIGHT_SEQ[0] += 1
+    st.set(f"dnn/preflight/{seq}/{r}", err or "ok")
+    errs = []
+    for q in range(n):
+        v = st.get(f"dnn/preflight/{seq}/{q}").decode(errors="replace")
+        if v != "ok":
+            errs.append(v)
+    if not errs:
+        return "native"
+    rccl.abort_all()
+    rccl.destroy_all()
+    os.environ["DNN_P2P"] = "torch"
+    return f"torch (native preflight failed: {errs[0]})"
+
+
 class SplitLink:
     """One logical stage hop over several peers: a tensor sent through it is
     cut into ``len(links)`` equal row slices, slice j going to ``links[j]``; a

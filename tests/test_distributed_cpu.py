@@ -264,6 +264,7 @@ def test_bench_pp2_schedule_cpu(n):
     assert d["dtype"].startswith("fp32") and "bf16x3" in d["dtype"] and d["scaling"] == "weak"
     assert d["config"]["stage_cut"] == "conv|fc (reference split, 16 KiB/img hop)"
     assert d["config"]["receiver_fill_images_per_step"] == 0
+    assert d["config"]["p2p"] == "gloo"  # native RCCL preflight applies to nccl runs only
     assert d["config"]["parallelism"].startswith(f"pp2-rccl-{n // 2}x{n // 2}")
     assert d["config"]["global_batch"] == (n // 2) * 16
     assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}

@@ -135,3 +135,34 @@ def test_pair_channel_two_processes(tmp_path):
     assert all(r.startswith(("ok", "init_error")) for r in res), (res, logs)
     if res[1].startswith("ok"):
         assert res[1] == "ok 0", res  # the receiver got exactly the sender's bytes
+
+
+def test_native_preflight_two_processes(tmp_path):
+    """links.native_preflight on a 2-rank nccl group sharing GPU 0: RCCL
+    refuses the pair, both ranks agree through the TCP store to fall back to
+    ProcessGroupNCCL P2P (DNN_P2P=torch) with the failing rank's message
+    (or, where RCCL accepts the pair, both report native)."""
+    port = str(_free_port())
+    outs = [str(tmp_path / f"p{r}.txt") for r in range(2)]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("DNN_P2P", None)
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "preflight_worker.py"), str(r), port,
+                               outs[r]], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(2)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=150)[0].decode(errors="replace")[-2000:])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    res = [open(o).read().strip() if os.path.exists(o) else "missing" for o in outs]
+    print("preflight results:", res)
+    modes = [r.split("|")[0] for r in res]
+    assert modes[0] == modes[1], (res, logs)
+    if modes[0] == "native":
+        assert all(r.endswith("|native") for r in res), res
+    else:
+        assert modes[0].startswith("torch (native preflight failed: rank"), (res, logs)
+        assert all(r.endswith("|torch") for r in res), res

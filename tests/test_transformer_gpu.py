@@ -116,6 +116,32 @@ def test_flash_attn_qkv_matches_split(B, Tn, H, Hkv, hd, pos0):
     assert torch.equal(out[rows], ref[rows])
 
 
+@pytest.mark.parametrize("M,N,rms", [(8192, 768, False), (10001, 1600, False), (9000, 4096, True), (20000, 768, True)])
+def test_row_stats_rows_per_wave(M, N, rms, monkeypatch):
+    """Prefill row statistics with 4 rows per wave (large M) are bit-identical
+    to one row per wave and match the fp32 two-pass statistics, including a
+    row count that is not a multiple of 16 and large-mean rows."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(8)
+    x = torch.randn(M, N, device=DEV)
+    x[::7] += 60.0  # |mean| / std >> 1 on some rows
+    x = x.bfloat16()
+    outs = []
+    for r in ("1", "4"):
+        monkeypatch.setenv("DNN_ROWSTATS_R", r)
+        st = torch.full((M, 2), float("nan"), device=DEV)
+        T.row_stats(x, st, 1e-5, rms)
+        outs.append(st)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    xf = x.float()
+    mean = torch.zeros(M, device=DEV) if rms else xf.mean(-1)
+    var = xf.pow(2).mean(-1) if rms else xf.var(-1, unbiased=False)
+    rstd = torch.rsqrt(var + 1e-5)
+    assert torch.allclose(outs[1][:, 0], rstd, rtol=1e-4, atol=0)
+    assert torch.allclose(outs[1][:, 1], -mean * rstd, rtol=1e-4, atol=1e-4)
+
+
 def test_flash_attn_spike_rescale():
     """Force the online-softmax rescale: one huge key score late in the sequence (guide §5.4 rule 26)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
@@ -135,9 +161,14 @@ def test_flash_attn_spike_rescale():
 def _decode_path(monkeypatch, path):
     """'0' / '1': the batched kernel with DPP / MFMA scores; '1p': the one-pass
     kernel, forced onto grids of any size."""
-    if path in ("1p", "1p_rs"):
+    if path in ("1p", "1p_rs", "1p_kf"):
         monkeypatch.setenv("DNN_DECODE_1P", "2")
         monkeypatch.setenv("DNN_DECODE_1P_RS", "1" if path == "1p_rs" else "0")
+        monkeypatch.setenv("DNN_DECODE_1P_KF", "1" if path == "1p_kf" else "0")
+    elif path == "1p_default":
+        monkeypatch.setenv("DNN_DECODE_1P", "2")
+        for k in ("DNN_DECODE_1P_RS", "DNN_DECODE_1P_KF", "DNN_DECODE_1P_KNT"):
+            monkeypatch.delenv(k, raising=False)
     else:
         monkeypatch.setenv("DNN_DECODE_1P", "0")
         monkeypatch.setenv("DNN_DECODE_MFMA", path)
@@ -147,7 +178,7 @@ def _decode_path(monkeypatch, path):
                                                (1, 4, 2, 128, 300, [299]), (4, 25, 25, 64, 512, [17, 64, 65, 512]),
                                                (1, 32, 8, 128, 131072, [120001]),   # long context: LDS-bound splits
                                                (2, 12, 12, 64, 65536, [65536, 9000])])
-@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs"])
+@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs", "1p_kf", "1p_default"])
 def test_attn_decode(B, H, Hkv, hd, S, lens, mfma, monkeypatch):
     """Both score paths of the batched decode kernel (DPP row reductions and
     MFMA key tiles, forced by DNN_DECODE_MFMA) and the one-pass kernel (forced
@@ -624,7 +655,7 @@ def test_linear_norm_strided_rows():
     (1, 32, 8, 128, 200, [150], True, 1), (3, 12, 12, 64, 300, [0, 17, 299], False, 2),
     (2, 8, 2, 128, 1024, [700, 1023], True, 4), (2, 4, 4, 64, 64, [63, 64], False, 1),
     (1, 32, 8, 128, 600, [140], True, 1), (1, 32, 8, 128, 600, [599], True, 3)])
-@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs"])
+@pytest.mark.parametrize("mfma", ["0", "1", "1p", "1p_rs", "1p_kf", "1p_default"])
 def test_attn_decode_qkv_fused(B, H, Hkv, hd, S, pos, rope, splits, mfma, monkeypatch):
     """Fused decode step (split + RoPE + cache write + attention) == qkv_split
     then attn_decode, and the cache row it wrote matches; pos >= S (overflow)
