@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--w8", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--arms", default="stream,skinny", help="stream (plan), skinny, forced (every shape streamed)")
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
@@ -85,11 +86,15 @@ def main():
                 return a.elapsed_time(b) / (3 * args.iters) * 1e3
 
             res = {"shape": name, "M": M, "N": N, "K": K, "w8": args.w8, "norm": norm, "MB": round(wbytes / 1e6, 1)}
-            ts = {"stream": [], "skinny": []}
+            arms = {"stream": 1, "skinny": 0, "forced": 2, "f2": 2, "f3": 2, "f4": 2, "f6": 2}
+            ts = {k: [] for k in args.arms.split(",")}
             for _ in range(args.rounds):
-                for k, on in (("stream", 1), ("skinny", 0)):
-                    set_stream_gemm(on, 8 << 20)
+                for k in ts:
+                    set_stream_gemm(arms[k], 8 << 20)
+                    if k[0] == "f" and k[1:].isdigit():  # forced with a pinned split count
+                        os.environ["DNN_STREAM_SPLITK"] = k[1:]
                     ts[k].append(timed())
+                    os.environ.pop("DNN_STREAM_SPLITK", None)
             set_stream_gemm(1, 8 << 20)
             for k in ts:
                 us = min(ts[k])

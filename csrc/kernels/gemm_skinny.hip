@@ -388,6 +388,10 @@ static bool stream_plan(int MP, int N, int kbytes, bool have_ws, long long ws_by
   if (ntiles < STREAM_MIN_WGS && have_ws) {
     const int by_steps = g_stream_on == 2 ? steps : max(1, steps / STREAM_MIN_STEPS);  // forced: split anything
     splitk = min(min((256 + ntiles - 1) / ntiles, STREAM_MAX_SPLIT), by_steps);
+    if (g_stream_on == 2) {  // forced (A/B probes): DNN_STREAM_SPLITK pins the split count
+      const char* e = getenv("DNN_STREAM_SPLITK");
+      if (e != nullptr && atoi(e) > 0) splitk = min(atoi(e), steps);
+    }
     auto need = [&](int sk) {
       return (long long)sk * MP * ntiles * BN * 4 + (long long)ntiles * sk * MP * 2 * 4 + STREAM_CNT_BYTES;
     };
