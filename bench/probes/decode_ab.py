@@ -42,6 +42,8 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_DECODE_1P"] = str(v)
     elif switch == "decode_1p_kf":  # one-pass decode attention: K/V loads issued before q (attention.hip KF)
         os.environ["DNN_DECODE_1P_KF"] = str(v)
+    elif switch == "flash_db":  # flash prefill with double-buffered K/V LDS (attention.hip DNN_FLASH_DB)
+        os.environ["DNN_FLASH_DB"] = str(v)
     elif switch == "rowstats_r":  # prefill row statistics rows per wave (norm_embed.hip dnn_row_stats)
         os.environ["DNN_ROWSTATS_R"] = str(v)
     elif switch == "argmax_split":

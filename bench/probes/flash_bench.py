@@ -50,9 +50,15 @@ def main():
         ref = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)  # noqa: E731
         flop = 4.0 * B * H * T * T * hd / 2
         t_o, t_r = timeit(ours), timeit(ref)
+        dbs = {}
+        for db in (0, 1, 0, 1):  # double-buffered K/V LDS A/B in one process (attention.hip DNN_FLASH_DB)
+            os.environ["DNN_FLASH_DB"] = str(db)
+            t = timeit(ours)
+            dbs[f"db{db}_ms"] = round(min(t, dbs.get(f"db{db}_ms", 1e9)), 4)
+        os.environ.pop("DNN_FLASH_DB", None)
         print(json.dumps({"B": B, "T": T, "H": H, "Hkv": Hkv, "hd": hd, "ours_ms": round(t_o, 4),
                           "ours_tflops": round(flop / t_o / 1e9, 1), "torch_sdpa_ms": round(t_r, 4),
-                          "torch_tflops": round(flop / t_r / 1e9, 1)}), flush=True)
+                          "torch_tflops": round(flop / t_r / 1e9, 1), **dbs}), flush=True)
 
 
 if __name__ == "__main__":

@@ -149,7 +149,7 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
-template <int HD, bool QKV = false, bool KV8 = false>
+template <int HD, bool QKV = false, bool KV8 = false, bool DB = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
@@ -157,7 +157,9 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
                                                             bf16_t* __restrict__ kc_out = nullptr,
                                                             bf16_t* __restrict__ vc_out = nullptr) {
   using SM = FaSmem<HD>;
-  __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL];
+  // DB: two K/V buffers, one barrier per block (the block after next is staged
+  // into the other buffer while this one is read)
+  __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL * (DB ? 2 : 1)];
   char* ks = smem;
   char* vs = smem + SM::K_BYTES;
   constexpr int NKS = HD / 16;  // k-steps of the QK^T contraction
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       }
     }
   };
-  auto block = [&](int kb0, i32x4(&pk)[NIT], i32x4(&pv)[NIT]) __attribute__((always_inline)) {
+  auto stage = [&](i32x4(&pk)[NIT], i32x4(&pv)[NIT]) __attribute__((always_inline)) {
     // ---- stage K (swizzled) and V (padded rows) from the prefetch registers ----
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -259,8 +261,8 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       *reinterpret_cast<i32x4*>(ks + key * HD * 2 + (k_swz<HD>(key, c) << 4)) = pk[it];
       *reinterpret_cast<i32x4*>(vs + key * SM::V_STRIDE + c * 16) = pv[it];
     }
-    __syncthreads();
-    if (kb0 + FA_KB < kv_end) fetch(kb0 + FA_KB, pk, pv);
+  };
+  auto compute = [&](int kb0) __attribute__((always_inline)) {
     if (kb0 <= wave_qmax) {
       // ---- S^T for two 32-key tiles ----
       f32x16 sacc[2];
@@ -355,10 +357,38 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
           }
         }
     }
-    __syncthreads();
   };
-  if (kv_end > 0) fetch(0, pkA, pvA);
-  for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) block(kb0, pkA, pvA);
+  if constexpr (!DB) {
+    if (kv_end > 0) fetch(0, pkA, pvA);
+    for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
+      stage(pkA, pvA);
+      __syncthreads();
+      if (kb0 + FA_KB < kv_end) fetch(kb0 + FA_KB, pkA, pvA);
+      compute(kb0);
+      __syncthreads();
+    }
+  } else {
+    if (kv_end > 0) {
+      fetch(0, pkA, pvA);
+      stage(pkA, pvA);
+      if (FA_KB < kv_end) fetch(FA_KB, pkA, pvA);
+    }
+    int buf = 0;
+    for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
+      // block kb0 is in buffer `buf` and every wave is done with the other one
+      __syncthreads();
+      ks = smem + buf * SM::TOTAL;
+      vs = ks + SM::K_BYTES;
+      compute(kb0);
+      if (kb0 + FA_KB < kv_end) {
+        ks = smem + (buf ^ 1) * SM::TOTAL;
+        vs = ks + SM::K_BYTES;
+        stage(pkA, pvA);
+        if (kb0 + 2 * FA_KB < kv_end) fetch(kb0 + 2 * FA_KB, pkA, pvA);
+      }
+      buf ^= 1;
+    }
+  }
   // ---- normalise + store: lane = query, regs = d ----
   if (qrow < T) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
@@ -1216,8 +1246,16 @@ extern "C" int dnn_qkv_split(const void* qkv, void* q, void* kc, void* vc, int B
 template <int HD, bool QKV, bool KV8>
 static void launch_flash(dim3 grid, hipStream_t st, const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* o,
                          int T, int H, int Hkv, int S, const int* pos, float sl2, int ldq, bf16_t* kco, bf16_t* vco) {
-  hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S, pos, sl2,
-                     ldq, kco, vco);
+  // double-buffered K/V LDS, one barrier per block (default): GPT-2 B=64 T=512 0.1075 -> 0.1063 ms,
+  // hd 128 T=512 0.251 -> 0.243, T=4096 1.123 -> 1.092 (profiles/r3_flash_double_buffer.jsonl);
+  // DNN_FLASH_DB=0 keeps the single buffer (A/B)
+  const char* e = getenv("DNN_FLASH_DB");
+  if (e == nullptr || atoi(e) != 0)
+    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, true>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S,
+                       pos, sl2, ldq, kco, vco);
+  else
+    hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, false>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S,
+                       pos, sl2, ldq, kco, vco);
 }
 
 extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,

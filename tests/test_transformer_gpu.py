@@ -142,6 +142,36 @@ def test_row_stats_rows_per_wave(M, N, rms, monkeypatch):
     assert torch.allclose(outs[1][:, 1], -mean * rstd, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("B,Tn,H,Hkv,hd,pos0", [(2, 64, 4, 4, 64, 0), (3, 200, 12, 12, 64, 0), (2, 77, 8, 2, 128, 0),
+                                                 (1, 33, 4, 1, 128, 40), (3, 130, 2, 2, 64, 17), (2, 517, 4, 2, 64, 0)])
+def test_flash_double_buffer_bit_identical(B, Tn, H, Hkv, hd, pos0, monkeypatch):
+    """Double-buffered K/V LDS with one barrier per block (DNN_FLASH_DB=1) is the
+    same arithmetic as the single buffer: outputs and written caches
+    bit-identical, head-major and QKV mode, chunked prefill and GQA."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    torch.manual_seed(4)
+    S = pos0 + Tn + 8
+    kc0 = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    vc0 = torch.randn(B, Hkv, S, hd, device=DEV).bfloat16()
+    qkv = torch.randn(B * Tn, (H + 2 * Hkv) * hd, device=DEV).bfloat16()
+    pos = torch.full((B,), pos0, device=DEV, dtype=torch.int32)
+    q = torch.empty(B * H * Tn * hd, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for db in ("0", "1"):
+        monkeypatch.setenv("DNN_FLASH_DB", db)
+        kc, vc = kc0.clone(), vc0.clone()
+        T.qkv_split(qkv, q, kc, vc, B, Tn, H, Hkv, hd, pos)
+        o1 = torch.empty(B * Tn, H * hd, device=DEV, dtype=torch.bfloat16)
+        T.flash_attn(q, kc, vc, o1, B, Tn, H, Hkv, hd, pos)
+        kc2, vc2 = kc0.clone(), vc0.clone()
+        o2 = torch.empty_like(o1)
+        T.flash_attn_qkv(qkv, kc2, vc2, o2, B, Tn, H, Hkv, hd, pos)
+        outs.append((o1, o2, kc2, vc2))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 def test_flash_attn_spike_rescale():
     """Force the online-softmax rescale: one huge key score late in the sequence (guide §5.4 rule 26)."""
     from distributed_neural_networks_amd.ops import transformer_ops as T
