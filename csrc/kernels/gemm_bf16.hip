@@ -140,8 +140,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn_kernel(
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     if (ACT == ACT_SILU_MUL) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        epi_silu_t4<OUT_F32>(acc[i][j], m, (n0 + wn * 64 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
+      for (int jp = 0; jp < 2; ++jp)
+        epi_silu_pair<OUT_F32>(acc[i][2 * jp], acc[i][2 * jp + 1], m, (n0 + wn * 64 + jp * 32) / 2, M, N / 2, Cv,
+                               ldc, vec, lane);
     } else if (!OUT_F32 && pair) {
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
@@ -446,9 +447,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
         const int nb = n0 + nq * 128 + wc * 32;
         if (ACT == ACT_SILU_MUL) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            epi_silu_t4<OUT_F32>(acc[mq][nq][i][j], m, (nb + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
+          epi_silu_pair<OUT_F32>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb / 2, M, N / 2, Cv, ldc, vec, lane);
         } else if (SCATTER) {
           // widened 16-B stores as in epi_pair_bf16, to the head-major / cache
           // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
@@ -627,8 +626,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
         if (SCATTER) {
           if (nb < N) epi_pair_scatter(v[0], v[1], m, nb, M, bias, lane, scat);
         } else if (ACT == ACT_SILU_MUL) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) epi_silu_t4<false>(v[j], m, (nb + j * 16) / 2, M, N / 2, C, ldc, vec, lane);
+          epi_silu_pair<false>(v[0], v[1], m, nb / 2, M, N / 2, C, ldc, vec, lane);
         } else if (rpre) {
           epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane, rr[mq][nq][i][0],
                                    rr[mq][nq][i][1]);

@@ -189,4 +189,41 @@ __device__ __forceinline__ void epi_silu_t4(const f32x4& acc, int m, int ncol0, 
     }
 }
 
+// SwiGLU epilogue of two adjacent 16-column tiles j, j+1 at full lane use: one
+// v_permlane32_swap per dword hands lanes 0-31 tile j's (gate, up) and lanes
+// 32-63 tile j+1's (epi_silu_t4 exchanged with ds_bpermute and left half the
+// lanes idle), and silu is x * rcp(1 + 2^(-x log2 e)) instead of an IEEE
+// divide.  Every lane writes output columns ncol0 + 4*(lane>>4) .. +3 of row m
+// (ncol0 = tile j's first output column).
+template <bool OUT_F32>
+__device__ __forceinline__ void epi_silu_pair(const f32x4& a0, const f32x4& a1, int m, int ncol0, int M, int NO,
+                                              void* __restrict__ Cv, int ldc, bool vec, int lane) {
+  f32x4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0[r]), __float_as_uint(a1[r]), false, false);
+    const float g = __uint_as_float(s[0]), u = __uint_as_float(s[1]);
+    v[r] = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g * -1.4426950408889634f)) * u;
+  }
+  if (m >= M) return;
+  const int ncol = ncol0 + (lane >> 4) * 4;
+  if (vec && ncol + 3 < NO) {
+    if (OUT_F32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + (size_t)m * ldc + ncol) = v;
+    } else {
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + ncol) = pk;
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (ncol + r < NO) {
+      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + ncol + r] = v[r];
+      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + ncol + r] = f2bf(v[r]);
+    }
+}
+
 }  // namespace dnn

@@ -164,6 +164,27 @@ def test_gemm_gelu_erf_accuracy():
     assert (y - ref).abs().max().item() < 2e-6 * 12
 
 
+@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("M,N,K", [(300, 2048, 768), (1000, 528, 256), (4096, 1024, 512)])
+def test_gemm_silu_mul_tiles(tile, M, N, K):
+    """SwiGLU epilogue of the tiled GEMMs (paired-tile permlane32 exchange),
+    forced 128^2 and 256^2, partial tiles included."""
+    from distributed_neural_networks_amd.ops.gemm import linear, pack_gate_up, set_gemm_tile
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    g = (torch.randn(N // 2, K, device=DEV) * 0.05).bfloat16()
+    u = (torch.randn(N // 2, K, device=DEV) * 0.05).bfloat16()
+    set_gemm_tile(tile)
+    try:
+        y = linear(x, pack_gate_up(g, u), act="silu_mul")
+        torch.cuda.synchronize()
+    finally:
+        set_gemm_tile(0)
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    assert y.shape == (M, N // 2)
+    assert _rel(y, ref) < 1e-2
+
+
 def test_gemm_silu_mul():
     from distributed_neural_networks_amd.ops.gemm import linear, pack_gate_up
     torch.manual_seed(1)
