@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SHAPES = {
     "llama": [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)],
     "gpt2": [(2304, 768), (768, 768), (3072, 768), (768, 3072)],
+    "gpt2head": [(50304, 768)],
     "gpt2xl": [(4800, 1600), (1600, 1600), (6400, 1600), (1600, 6400), (50304, 1600)],
 }
 
