@@ -25,6 +25,8 @@ SHAPES = {  # name: (B, H, Hkv, hd, S capacity, pos, rope)
     "gpt2_b64": (64, 12, 12, 64, 567, 540, False),
     "gpt2xl_b64": (64, 25, 25, 64, 567, 540, False),
     "llama_b32": (32, 32, 8, 128, 567, 540, True),
+    "llama_b32_p270": (32, 32, 8, 128, 567, 270, True),   # fixed vs per-byte cost
+    "llama_b64": (64, 32, 8, 128, 567, 540, True),        # two workgroups per CU
 }
 VARIANTS = {  # name: env
     "batched": {"DNN_DECODE_1P": "0"},
