@@ -26,11 +26,13 @@ SHAPES = {  # name: (B, H, Hkv, hd, S capacity, pos, rope)
     "gpt2xl_b64": (64, 25, 25, 64, 567, 540, False),
     "llama_b32": (32, 32, 8, 128, 567, 540, True),
     "llama_b32_p270": (32, 32, 8, 128, 567, 270, True),   # fixed vs per-byte cost
+    "llama_b48": (48, 32, 8, 128, 567, 540, True),
     "llama_b64": (64, 32, 8, 128, 567, 540, True),        # two workgroups per CU
 }
 VARIANTS = {  # name: env
     "batched": {"DNN_DECODE_1P": "0"},
     "1p": {"DNN_DECODE_1P": "1"},
+    "1p_force": {"DNN_DECODE_1P": "2"},
     "1p_kf0": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KF": "0"},
     "1p_kf1": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KF": "1"},
     "1p_knt0": {"DNN_DECODE_1P": "1", "DNN_DECODE_1P_KNT": "0"},

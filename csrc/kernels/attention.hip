@@ -1362,6 +1362,11 @@ static int attn_decode_1p_launch(const void* q, int ldq, void* kc, void* vc, voi
   const int ns = (S + DEC1P_CAP - 1) / DEC1P_CAP;
   if (ns > 1 && ns > splits) return 1;
   if (!force && (long)B * Hkv * ns < 128) return 1;
+  // GQA past one workgroup per CU: the 86 KiB of LDS per workgroup keeps one
+  // resident per CU, so a second round of workgroups runs serially and the
+  // batched kernel wins (Llama-3 B=64: 36.5 vs 30.9 us,
+  // profiles/r3_attn_1p_shapes.jsonl); MHA's 4-wave workgroups are small
+  if (!force && G > 1 && (long)B * Hkv * ns > 256) return 1;
   dim3 grid(B * Hkv, ns);
   // row-layout scores for MHA, MFMA key tiles for GQA: at MHA hd 64 an MFMA tile
   // uses 1 of 16 head columns and its half-row key loads ran 10 % slower than
