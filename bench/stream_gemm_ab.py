@@ -24,6 +24,8 @@ SHAPES = {
               ("head", 128256, 4096, 1)],
     "gpt2xl": [("qkv", 4800, 1600, 2), ("o", 1600, 1600, 0), ("fc", 6400, 1600, 2), ("proj", 1600, 6400, 0),
                ("head", 50304, 1600, 2)],
+    "gpt2": [("qkv", 2304, 768, 2), ("o", 768, 768, 0), ("fc", 3072, 768, 2), ("proj", 768, 3072, 0),
+             ("head", 50304, 768, 2)],
 }
 
 
