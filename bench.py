@@ -85,6 +85,8 @@ def parse():
                     help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = per placement")
     ap.add_argument("--extra_budget_s", type=float, default=420.0,
                     help="N>1: wall-clock budget of the extra keys (a hang only drops keys)")
+    ap.add_argument("--launch_timeout", type=float, default=1800.0,
+                    help="N>1 without a launcher: wall-clock limit of the self-launched job")
     return ap.parse_args()
 
 
@@ -525,11 +527,18 @@ def precision_check(dev, precision: str, n_img: int = 4096) -> dict:
 
 def main():
     args = parse()
+    from distributed_neural_networks_amd.parallel import selflaunch
+    # `python bench.py --gpus N` with no launcher: spawn the N ranks here (the
+    # parent never touches the GPU) and relay rank 0's line
+    rc = selflaunch.maybe_self_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], args.launch_timeout)
+    if rc is not None:
+        return rc
     if args.model != "cifar10":
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
         import gpt_bench
         return gpt_bench.main(args)
     info = dist_setup(args.gpus, args.cpu)
+    selflaunch.check_world(args.gpus, info.world)
     N = info.world
     p2p = "none"
     if N > 1:
@@ -550,15 +559,17 @@ def main():
         n_cu = torch.cuda.get_device_properties(info.device).multi_processor_count
         cops.set_stage0_grid(max(1, n_cu - spare))
     fill = 0.0
-    if N == 1:
-        el, imgs_per_gpu, p50, par = bench_colocated(args, info)
-    elif args.placement == "interleaved":
-        el, imgs_per_gpu, p50, par = bench_interleaved(args, info)
-    elif args.placement == "fc1cut":
-        el, imgs_per_gpu, fill, par = bench_fc1cut(args, info)
-        p50 = float("nan")
-    else:
-        el, imgs_per_gpu, p50, par = bench_pp2(args, info)
+    from distributed_neural_networks_amd.parallel import rccl
+    with rccl.scope(info.device):  # this placement's native channels close when it is measured
+        if N == 1:
+            el, imgs_per_gpu, p50, par = bench_colocated(args, info)
+        elif args.placement == "interleaved":
+            el, imgs_per_gpu, p50, par = bench_interleaved(args, info)
+        elif args.placement == "fc1cut":
+            el, imgs_per_gpu, fill, par = bench_fc1cut(args, info)
+            p50 = float("nan")
+        else:
+            el, imgs_per_gpu, p50, par = bench_pp2(args, info)
     el = max_over_ranks(info, el)
     total = imgs_per_gpu * N * args.steps
     value = total / el
@@ -621,7 +632,7 @@ def multi_gpu_extras(args, info, line):
     import threading
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
     import gpt_bench
-    from distributed_neural_networks_amd.parallel import comm
+    from distributed_neural_networks_amd.parallel import comm, rccl
     current = ["fc1cut"]
 
     def bail():
@@ -637,7 +648,8 @@ def multi_gpu_extras(args, info, line):
         try:
             a = copy.copy(args)
             a.latency_iters = 3
-            el, imgs, fill, par = bench_fc1cut(a, info)
+            with rccl.scope(info.device):
+                el, imgs, fill, par = bench_fc1cut(a, info)
             el = max_over_ranks(info, el)
             if line is not None:
                 line["fc1cut_images_per_s"] = round(imgs * info.world * args.steps / el, 1)
@@ -656,7 +668,8 @@ def multi_gpu_extras(args, info, line):
                                                   ["--cpu", "--steps", "3", "--warmup", "1", "--batch", "2",
                                                    "--prompt", "8", "--prefill_iters", "1"] + argv_cpu)
             try:
-                g = gpt_bench.run(gpt_bench.parse(argv), shutdown=False)
+                with rccl.scope(info.device):  # each ring's channels close when the ring is measured
+                    g = gpt_bench.run(gpt_bench.parse(argv), shutdown=False)
             except Exception as e:  # noqa: BLE001
                 if line is not None:
                     line[key + "_error"] = f"{type(e).__name__}: {e}"[:200]

@@ -50,6 +50,12 @@ def parse(argv=None):
                     help="fp8 KV cache scale: per-layer, from the first prefill's amax, or unit")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
+    ap.add_argument("--gloo_gpu", action="store_true",
+                    help="every rank on GPU 0 (HIP kernels + graphs), hops staged through host memory over gloo "
+                         "(the 1-GPU box's multi-process schedule test; RCCL refuses two ranks on one GPU)")
+    ap.add_argument("--prepost_ab", type=int, default=0,
+                    help="after the timed run: this many interleaved A/B pairs of decode runs without / with "
+                         "the pre-posted next-microbatch receive (DecodeRing.prepost)")
     return ap.parse_args(argv)
 
 
@@ -95,7 +101,11 @@ def run(args=None, shutdown: bool = True):
     from distributed_neural_networks_amd.parallel.links import make_link
 
     N = args.gpus
-    if getattr(args, "cpu", False):
+    if getattr(args, "gloo_gpu", False):
+        info = comm.init("gloo")
+        torch.cuda.set_device(0)
+        info = comm.DistInfo(info.rank, info.world, info.local_rank, "gloo", torch.device("cuda", 0))
+    elif getattr(args, "cpu", False):
         info = comm.init("gloo")
     elif N > 1 or "WORLD_SIZE" in os.environ:
         info = comm.init("nccl")
@@ -105,6 +115,8 @@ def run(args=None, shutdown: bool = True):
     else:
         torch.cuda.set_device(0)
         info = comm.DistInfo(0, 1, 0, "none", torch.device("cuda", 0))
+    from distributed_neural_networks_amd.parallel.selflaunch import check_world
+    check_world(args.gpus, info.world)
     N, r, dev = info.world, info.rank, info.device
     model = args.model
     S = args.stages
@@ -171,13 +183,11 @@ def run(args=None, shutdown: bool = True):
     prefill_round()
     if ring is not None:
         ring.capture()
-    for _ in range(args.warmup):
-        if ring is not None:
-            ring.decode_round()
+    if ring is not None and args.warmup:
+        ring.decode_rounds(args.warmup)
     t0 = sync()
-    for _ in range(args.steps):
-        if ring is not None:
-            ring.decode_round()
+    if ring is not None:
+        ring.decode_rounds(args.steps)  # next microbatch's input received while this one computes
     if ring is not None:
         ring.drain()
     t1 = sync()
@@ -211,9 +221,31 @@ def run(args=None, shutdown: bool = True):
         if N == 1:
             return v
         import torch.distributed as dist
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        t = torch.tensor([v], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    ab = {}
+    if getattr(args, "prepost_ab", 0) and ring is not None:
+        # interleaved A/B of the decode schedule: each input received just before
+        # its use vs the next microbatch's receive posted before this one computes
+        k = max(2, args.steps // 2)
+        times = {False: [], True: []}
+        for _ in range(args.prepost_ab):
+            for pp in (False, True):
+                ring.prepost = pp
+                ta = sync()
+                ring.decode_rounds(k)
+                ring.drain()
+                times[pp].append(mx(sync() - ta) / k)
+        ring.prepost = True
+        ab = {"ab_rounds_per_arm": k, "ab_no_prepost_ms_per_step": [round(t * 1e3, 4) for t in times[False]],
+              "ab_prepost_ms_per_step": [round(t * 1e3, 4) for t in times[True]]}
+    elif getattr(args, "prepost_ab", 0):
+        for _ in range(args.prepost_ab * 2):
+            sync()
+            sync()
+            mx(0.0)
 
     prefill_s, decode_s = mx(prefill_s), mx(decode_s)
     out = None
@@ -235,10 +267,14 @@ def run(args=None, shutdown: bool = True):
                        "decode_lanes": len(ring.lanes) if ring is not None and ring.lanes else 1,
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},
         }
+        out.update(ab)
     if N > 1 and shutdown:
         comm.shutdown()
     return out if r == 0 else None
 
 
 if __name__ == "__main__":
-    sys.exit(main(parse()))
+    _args = parse()
+    from distributed_neural_networks_amd.parallel.selflaunch import maybe_self_launch
+    _rc = maybe_self_launch(_args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    sys.exit(_rc if _rc is not None else main(_args))

@@ -197,15 +197,18 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("comm_wait_ready", [](long long h, int timeout_ms) { return dnn_comm_wait_ready(h, timeout_ms); },
         py::call_guard<py::gil_scoped_release>());
+  // posts release the GIL: one waiting on a completed ring slot must never
+  // keep the watchdog thread from running abort_all
   m.def("comm_post", [](long long h, int kind, u64 ptr, long long bytes, int peer, u64 st, int on_stream) {
     return dnn_comm_post(h, kind, P(ptr), bytes, peer, ST(st), on_stream);
-  });
+  }, py::call_guard<py::gil_scoped_release>());
   m.def("comm_group", [](long long h, std::vector<int> kinds, std::vector<u64> ptrs, std::vector<long long> bytes,
                          std::vector<int> peers, u64 st, int on_stream) {
     const size_t n = kinds.size();
     if (ptrs.size() != n || bytes.size() != n || peers.size() != n) throw std::runtime_error("comm_group: ragged op lists");
     std::vector<void*> p(n);
     for (size_t i = 0; i < n; ++i) p[i] = P(ptrs[i]);
+    py::gil_scoped_release nogil;
     return dnn_comm_group(h, (int)n, kinds.data(), p.data(), bytes.data(), peers.data(), ST(st), on_stream);
   });
   m.def("comm_wait", [](long long h, long long tok, u64 st) { return dnn_comm_wait(h, tok, ST(st)); });

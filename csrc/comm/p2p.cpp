@@ -32,6 +32,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -109,6 +110,11 @@ struct DeviceGuard {
 struct Channel {
   static constexpr int RING = 1024;  // completion events in flight per channel
   int nranks = 0, rank = 0, device = 0;
+  // ops (post / group), abort's ncclCommAbort and destroy serialise on this;
+  // abort only *tries* it for a bounded time (a post can be stuck waiting on a
+  // dead peer's slot: it polls `aborted` and gives the lock back)
+  std::timed_mutex mu;
+  std::mutex join_mu;  // joining the init thread (several threads may ask)
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t in_ev[RING];
@@ -118,7 +124,8 @@ struct Channel {
   std::thread init;
   std::atomic<int> state{0};  // 0 pending, 1 ready, < 0 failed (-rc)
   std::string init_err;
-  bool aborted = false;
+  std::atomic<bool> aborted{false};
+  std::atomic<bool> init_detached{false};  // abort left a blocked init running: never delete this Channel
   long long sent_ops = 0, sent_bytes = 0, recv_ops = 0, recv_bytes = 0;
 };
 
@@ -127,25 +134,55 @@ static Channel* ch(long long h) { return reinterpret_cast<Channel*>(static_cast<
 static int ensure_ready(Channel* c, int timeout_ms) {
   const auto t0 = std::chrono::steady_clock::now();
   while (c->state.load(std::memory_order_acquire) == 0) {
+    if (c->aborted.load()) return fail("channel aborted during communicator init", -3);
     if (timeout_ms >= 0 &&
         std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
       return 1;
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
-  if (c->init.joinable()) c->init.join();
+  {
+    std::lock_guard<std::mutex> j(c->join_mu);
+    if (c->init.joinable() && !c->init_detached.load()) c->init.join();
+  }
   if (c->state.load() < 0) return fail("rccl communicator init failed: " + c->init_err, -2);
-  if (c->aborted) return fail("channel was aborted", -3);
+  if (c->aborted.load()) return fail("channel was aborted", -3);
   return 0;
 }
 
+static int slot_timeout_ms() {
+  static const int ms = [] {
+    const char* e = std::getenv("DNN_RCCL_SLOT_TIMEOUT_MS");
+    return e ? std::atoi(e) : 300000;
+  }();
+  return ms;
+}
+
 // Claim the next ring slot (the op that used it before must have completed).
+// The wait for that op is a bounded poll, never hipEventSynchronize: a peer
+// that died with ops in flight must surface as an error (or an abort from the
+// watchdog thread), not as a host thread blocked forever.
 static int next_slot(Channel* c, long long& tok) {
-  tok = ++c->seq;
-  const int s = (int)(tok % Channel::RING);
+  const long long want = c->seq + 1;
+  const int s = (int)(want % Channel::RING);
   if (c->done_tok[s] != 0) {
-    const hipError_t e = hipEventSynchronize(c->done_ev[s]);
-    if (e != hipSuccess) return fail(std::string("event sync: ") + hipGetErrorString(e));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(c->done_ev[s]);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) return fail(std::string("event query: ") + hipGetErrorString(e));
+      if (c->aborted.load()) return fail("channel was aborted", -3);
+      if (c->comm != nullptr) {
+        ncclResult_t ae = ncclSuccess;
+        api().CommGetAsyncError(c->comm, &ae);
+        if (ae != ncclSuccess && ae != ncclInProgress) return fail(rccl_msg("rccl async error", ae));
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(slot_timeout_ms()))
+        return fail("completion ring full: op " + std::to_string(c->done_tok[s]) + " not complete after " +
+                    std::to_string(slot_timeout_ms()) + " ms (peer dead?)");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
   }
+  tok = c->seq = want;
   c->done_tok[s] = tok;
   return s;
 }
@@ -166,9 +203,11 @@ static long long post_ops(long long h, int n, const int* kinds, void* const* ptr
                           const int* peers, hipStream_t st, int on_stream) {
   Channel* c = ch(h);
   if (c == nullptr) return fail("null channel");
-  // never block here (the caller may hold the GIL): Python waits for the init
-  // with dnn_comm_wait_ready, GIL released, before a channel's first op
+  // never block on the init here: Python waits for it with
+  // dnn_comm_wait_ready, GIL released, before a channel's first op
   if (int r = ensure_ready(c, 0)) return r == 1 ? fail("channel init still pending", -4) : r;
+  std::lock_guard<std::timed_mutex> lock(c->mu);
+  if (c->aborted.load() || c->comm == nullptr) return fail("channel was aborted", -3);
   for (int i = 0; i < n; ++i) {
     if (kinds[i] != 0 && kinds[i] != 1) return fail("op kind must be 0 (send) or 1 (recv)");
     if (peers[i] < 0 || peers[i] >= c->nranks) return fail("peer " + std::to_string(peers[i]) + " out of range");
@@ -318,22 +357,36 @@ int dnn_comm_sync(long long h, long long token, int timeout_ms) {
 int dnn_comm_abort(long long h) {
   Channel* c = ch(h);
   if (c == nullptr) return 0;
-  if (c->state.load() == 0) {  // init still blocked on a peer that may be dead: leave it, never join
-    if (c->init.joinable()) c->init.detach();
-    c->aborted = true;
-    return 0;
+  const bool was = c->aborted.exchange(true);  // a post waiting on a slot sees this and returns
+  {
+    std::lock_guard<std::mutex> j(c->join_mu);
+    if (c->state.load() == 0) {  // init still blocked on a peer that may be dead: leave it, never join
+      if (c->init.joinable()) {
+        c->init.detach();
+        c->init_detached.store(true);
+      }
+      return 0;
+    }
+    if (c->init.joinable() && !c->init_detached.load()) c->init.join();
   }
-  if (c->init.joinable()) c->init.join();
-  if (c->comm != nullptr && !c->aborted) api().CommAbort(c->comm);
-  c->aborted = true;
-  c->comm = nullptr;
+  std::unique_lock<std::timed_mutex> lock(c->mu, std::defer_lock);
+  if (!was && lock.try_lock_for(std::chrono::seconds(5)) && c->comm != nullptr) {
+    api().CommAbort(c->comm);
+    c->comm = nullptr;
+  }
   return 0;
 }
 
 int dnn_comm_destroy(long long h) {
   Channel* c = ch(h);
   if (c == nullptr) return 0;
-  if (c->init.joinable()) c->init.join();
+  {
+    std::lock_guard<std::mutex> j(c->join_mu);
+    if (c->state.load() == 0 && !c->init.joinable()) c->init_detached.store(true);
+    if (c->init_detached.load()) return 0;  // its init thread may still write into it: leak, never free
+    if (c->init.joinable()) c->init.join();
+  }
+  std::lock_guard<std::timed_mutex> lock(c->mu);
   int rc = 0;
   {
     DeviceGuard g(c->device);

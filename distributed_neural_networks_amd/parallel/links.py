@@ -270,21 +270,26 @@ def native_preflight(device: torch.device, timeout_s: float = 90.0, store=None) 
         return p2p_mode()
     r, n = dist.get_rank(), dist.get_world_size()
     err = ""
+    from . import comm, rccl
     try:
-        nxt, prv = make_link((r + 1) % n, device), make_link((r - 1) % n, device)
-        for link in (nxt, prv):
-            link.ch.ready(timeout_s)
-        a = torch.full((4,), r, dtype=torch.int32, device=device)
-        b = torch.full((4,), -1, dtype=torch.int32, device=device)
-        works = [nxt.isend(a), prv.irecv(b)] if r % 2 == 0 else [prv.irecv(b), nxt.isend(a)]
-        for w in works:
-            w.synchronize(timeout_s)
-        got = int(b[0].item())
-        if got != (r - 1) % n:
-            raise RuntimeError(f"ring payload {got}, expected {(r - 1) % n}")
+        # the forward tag and the back-edge tag (its own communicators); the
+        # ring's channels are closed again afterwards (scope), so pairs no
+        # pipeline uses do not keep a communicator, stream and event ring
+        with rccl.scope(device):
+            for tag, grp in (("world", None), ("back", comm.back_group())):
+                nxt, prv = make_link((r + 1) % n, device, grp), make_link((r - 1) % n, device, grp)
+                for link in (nxt, prv):
+                    link.ch.ready(timeout_s)
+                a = torch.full((4,), r, dtype=torch.int32, device=device)
+                b = torch.full((4,), -1, dtype=torch.int32, device=device)
+                works = [nxt.isend(a), prv.irecv(b)] if r % 2 == 0 else [prv.irecv(b), nxt.isend(a)]
+                for w in works:
+                    w.synchronize(timeout_s)
+                got = int(b[0].item())
+                if got != (r - 1) % n:
+                    raise RuntimeError(f"{tag} ring payload {got}, expected {(r - 1) % n}")
     except Exception as e:  # noqa: BLE001 — any failure means: fall back
         err = f"rank {r}: {type(e).__name__}: {e}"[:200]
-    from . import rccl
     st = store or rccl._store()
     seq = _PREFLIGHT_SEQ[0]
     _PREFLIGHT_SEQ[0] += 1

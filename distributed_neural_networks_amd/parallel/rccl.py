@@ -33,6 +33,7 @@ Reference behaviour replaced: the per-request gRPC channel of
 from __future__ import annotations
 
 import collections
+import contextlib
 import os
 import threading
 from typing import Dict, Optional, Sequence, Tuple
@@ -44,6 +45,7 @@ INIT_TIMEOUT_S = float(os.environ.get("DNN_RCCL_INIT_TIMEOUT_S", "300"))
 
 _CHANNELS: Dict[Tuple[str, Tuple[int, ...]], "Channel"] = {}
 _LOCK = threading.Lock()
+_SCOPES: list = []  # open scope() frames, innermost last: keys of the channels each one opened
 
 
 def _lib():
@@ -80,12 +82,20 @@ class Channel:
         self._ready = False
         self._keep = collections.deque()  # (token, tensor): buffers alive until their op completed
         self.closed = False
+        self._abort_requested = False
+        self._hlock = threading.Lock()
 
         def init():
             try:
                 u = uid if uid is not None else bytes(uid_fn())
-                self.h = _lib().comm_create(u, nranks, rank, device.index, 0)  # blocking init, GIL released
-                if _lib().comm_wait_ready(self.h, 0) != 0:  # the init's verdict (message: this thread's last error)
+                # async create: the handle exists before the collective init
+                # finishes, so abort() can reach a channel whose peer never comes
+                h = _lib().comm_create(u, nranks, rank, device.index, 1)
+                with self._hlock:
+                    self.h = h
+                    if self._abort_requested:
+                        _lib().comm_abort(h)
+                if _lib().comm_wait_ready(h, -1) != 0:  # the init's verdict (GIL released while waiting)
                     raise RuntimeError(_lib().comm_last_error())
             except BaseException as e:  # noqa: BLE001 — re-raised by ready()
                 self._err = e
@@ -107,8 +117,13 @@ class Channel:
         return self
 
     def abort(self) -> None:
-        if not self.closed and self.h is not None:
-            _lib().comm_abort(self.h)
+        """Make in-flight ops return; also reaches a channel whose init is
+        still waiting for its peer (the init then fails instead of blocking)."""
+        with self._hlock:
+            self._abort_requested = True
+            h = self.h
+        if not self.closed and h is not None:
+            _lib().comm_abort(h)
 
     def destroy(self) -> None:
         if not self.closed:
@@ -224,7 +239,45 @@ def pair_channel(my_rank: int, peer: int, device: torch.device, tag: str = "worl
         else:  # the id is read on the init thread: opening a channel never blocks
             ch = Channel(None, 2, 1, device, key=key, uid_fn=lambda: st.get(skey))
         _CHANNELS[key] = ch
+        _note_opened(key)
         return ch
+
+
+def _note_opened(key) -> None:
+    if _SCOPES:
+        _SCOPES[-1].append(key)
+
+
+def live_channels() -> int:
+    """Channels currently open in this process (communicator + stream + event ring each)."""
+    with _LOCK:
+        return sum(1 for c in _CHANNELS.values() if not c.closed)
+
+
+@contextlib.contextmanager
+def scope(device: Optional[torch.device] = None):
+    """Channels first opened inside the block are destroyed when it ends
+    (after the device has drained), so one measurement's channel set — a
+    placement's pairs, one decode ring's links — does not stay alive through
+    the next.  Channels that already existed are left alone.  Nestable."""
+    frame: list = []
+    _SCOPES.append(frame)
+    ok = False
+    try:
+        yield frame
+        ok = True
+    finally:
+        _SCOPES.remove(frame)
+        with _LOCK:
+            chans = [_CHANNELS.pop(k) for k in frame if k in _CHANNELS]
+        if chans and ok:
+            dev = device or chans[0].device
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+        for c in chans:
+            if not ok:  # an op may be stuck on a peer: make it return instead of draining the device
+                c.abort()
+            c.destroy()
 
 
 def loopback(device: torch.device) -> Channel:
@@ -235,6 +288,7 @@ def loopback(device: torch.device) -> Channel:
         ch = _CHANNELS.get(key)
         if ch is None or ch.closed:
             ch = _CHANNELS[key] = Channel(_lib().comm_unique_id(), 1, 0, device, key=key)
+            _note_opened(key)
         return ch
 
 

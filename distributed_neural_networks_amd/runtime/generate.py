@@ -85,8 +85,8 @@ def _timed_generate(ring: DecodeRing, prompts, T: int, steps: int, dev, chunk: i
         ring.capture()
     _sync(dev)
     t1 = time.perf_counter()
-    for _ in range(steps - 1):
-        ring.decode_round()
+    if steps > 1:
+        ring.decode_rounds(steps - 1)
     ring.drain()
     _sync(dev)
     t2 = time.perf_counter()

@@ -331,7 +331,14 @@ class DecodeRing:
         self.cur = [torch.zeros((B, 1), dtype=torch.int32, device=dev) for _ in range(M)] if self.first else None
         in_dt = _act_dtype(self.stages[0])
         out_dt = _act_dtype(self.stages[-1])
-        self.xin = torch.empty((B, self.d), dtype=in_dt, device=dev) if not self.first else None
+        # one input slot per microbatch: the receive of microbatch m+1 can land
+        # while microbatch m's graph still reads its own slot
+        self.xin = [torch.empty((B, self.d), dtype=in_dt, device=dev) for _ in range(M)] if not self.first else None
+        # pre-posted receive per microbatch: hidden states (non-first ranks) or
+        # the sampled token over the back-edge (group 0 with G > 1)
+        self.rwork: List[object] = [None] * M
+        self.rorder = SlotOrder("ring_in", M)
+        self.prepost = True  # False: each input is received just before its use (the A/B baseline)
         if self.last:
             self.out = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(M)]
         else:
@@ -360,7 +367,7 @@ class DecodeRing:
         return h
 
     def _decode_body(self, m: int):
-        x = self.cur[m] if self.first else self.xin
+        x = self.cur[m] if self.first else self.xin[m]
         # greedy last stage: the argmax launch also writes the next input ids
         # (one group) and advances the positions — no separate copy / add kernels
         if self.last and getattr(self.stages[-1], "fuses_step_tail", False):
@@ -395,10 +402,35 @@ class DecodeRing:
             if not self.pending[m]:
                 return  # already received (drain) — the ring resumes from cur[m]
             with trace.span("token_recv", "p2p", mb=m):
-                self.links.back_in.recv(self.cur[m].view(self.B))
+                self._wait_input(m)
             self.pending[m] = False
         if self.record:
             self.toks[m].append(self.cur[m].view(self.B).clone())
+
+    # -- pre-posted receives ----------------------------------------------------
+    def _has_input_link(self) -> bool:
+        return (not self.first) or self.G > 1
+
+    def _post_input(self, m: int) -> None:
+        """Post the receive of microbatch m's next input (hidden states from the
+        previous group, or the token over the back-edge).  On RCCL the
+        transfer is ordered after the work queued now, so the slot's last
+        reader — microbatch m's previous graph — must already be queued."""
+        if self.rwork[m] is not None or not self._has_input_link():
+            return
+        if self.first:
+            if not self.pending[m]:
+                return  # no token of m in flight (drained, or m not sent yet): nothing to receive
+            self.rwork[m] = self.links.back_in.irecv(self.cur[m].view(self.B))
+        else:
+            self.rwork[m] = self.links.prev.irecv(self.xin[m])
+        self.rorder.post(m, "recv", m)
+
+    def _wait_input(self, m: int) -> None:
+        self._post_input(m)  # not pre-posted: post it now
+        self.rwork[m].wait()  # stream-ordered: no host block on RCCL
+        self.rwork[m] = None
+        self.rorder.waited(m)
 
     # -- prefill ----------------------------------------------------------------
     def prefill(self, prompts: Optional[Sequence[torch.Tensor]], T: int, chunk: int = 0) -> None:
@@ -410,10 +442,11 @@ class DecodeRing:
 
         Stages with a calibrated fp8 KV cache that is not calibrated yet
         (``needs_kv_calibration``: the same on every rank, it follows the
-        config) first run this prefill at unit scale, set their per-layer
-        scales from the cache's K / V amax and clear it; then the prefill runs
-        for real.  Once per stage lifetime."""
-        if any(getattr(s, "needs_kv_calibration", False) for s in self.stages):
+        config) first run this prefill ``KV_CAL_ROUNDS`` times (a fixed count,
+        so every rank runs the same prefills and the ring hops match), setting
+        their per-layer scales from the cache's K / V amax after each and
+        clearing it; then the prefill runs for real.  Once per stage lifetime."""
+        while any(getattr(s, "needs_kv_calibration", False) for s in self.stages):
             self._prefill(prompts, T, chunk)
             self.drain()
             for s in self.stages:
@@ -491,15 +524,34 @@ class DecodeRing:
         list) advances one token on this rank's stages.  ``mbs=[0]`` after a
         ``drain`` lets one microbatch circulate alone: a round is then exactly
         one trip around the ring (per-token latency)."""
+        self.decode_rounds(1, mbs)
+
+    def decode_rounds(self, n: int, mbs: Optional[Sequence[int]] = None) -> None:
+        """``n`` decode rounds.  The input of the next microbatch in the
+        sequence (across round boundaries too, up to the last one of the
+        ``n`` rounds) is received into its own slot while this one computes:
+        its receive is posted *before* this microbatch's graph is launched
+        (``run_gpipe``'s depth-ahead receive), so on RCCL the hop of
+        microbatch m+1 overlaps the compute of m instead of being queued
+        behind it.  A receive is never posted for a microbatch whose previous
+        graph is not queued yet (one microbatch: no pre-post)."""
         if self.lanes and mbs is None:
-            return self._decode_round_lanes()
+            for _ in range(n):
+                self._decode_round_lanes()
+            return
+        order = list(range(self.M) if mbs is None else mbs)
+        seq = [m for _ in range(n) for m in order]
         G = self.G
-        for m in (range(self.M) if mbs is None else mbs):
+        for i, m in enumerate(seq):
             if self.first and G > 1:
                 self._recv_token(m)
             elif not self.first:
                 with trace.span("hidden_recv", "p2p", mb=m):
-                    self.links.prev.recv(self.xin)
+                    self._wait_input(m)
+            self.rorder.use(m, "ring input read", m)
+            nxt_m = seq[i + 1] if i + 1 < len(seq) else None
+            if self.prepost and nxt_m is not None and nxt_m != m and self._has_input_link():
+                self._post_input(nxt_m)  # its slot's last reader was queued in an earlier item
             self._out_ready(m)
             with trace.span("decode", "compute", mb=m, step=self.steps_done):
                 if m in self.graphs:
@@ -511,8 +563,9 @@ class DecodeRing:
                 self.pending[m] = True
             if self.first and G == 1 and self.record:
                 self.toks[m].append(self.cur[m].view(self.B).clone())
+            if i + 1 == len(seq) or (i + 1) % len(order) == 0:
+                self.steps_done += 1
             self.progress()
-        self.steps_done += 1
 
     def _decode_round_lanes(self) -> None:
         """One group, M microbatches on ``len(self.lanes)`` streams: the round
@@ -549,6 +602,7 @@ class DecodeRing:
                 self.swork[m] = None
                 self.sorder.waited(m)
         self.sorder.drained()
+        self.rorder.drained()  # decode_rounds never leaves a receive posted past its last item
 
     def generate(self, prompts, T: int, steps: int, chunk: int = 0) -> Optional[torch.Tensor]:
         """Prefill + ``steps - 1`` decode rounds (``steps`` tokens per sequence).
@@ -556,8 +610,8 @@ class DecodeRing:
         self.prefill(prompts, T, chunk)
         if steps > 1:
             self.capture()
-        for _ in range(steps - 1):
-            self.decode_round()
+        if steps > 1:
+            self.decode_rounds(steps - 1)
         self.drain()
         return self.tokens() if self.first else None
 

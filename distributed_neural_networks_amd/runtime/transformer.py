@@ -167,20 +167,45 @@ class TransformerStage(StageCompute):
         return self.kv_dtype == "fp8" and self.kv_scale_mode == "calibrated" and not self.kv_calibrated
 
     KV_TARGET = 224.0  # calibrated |K|, |V| max maps to <= 224 (half the e4m3 range: headroom for later tokens)
+    E4M3_MAX = 448.0
+    KV_CAL_ROUNDS = 2  # calibration prefills per stage lifetime: the same count on every rank (ring hops match)
+    KV_SAT_JUMP = 512.0  # a saturated first round retries at 512x the scale (|K| up to ~229 k measured exactly)
 
     def calibrate_kv(self) -> List[tuple]:
         """Per-tensor fp8 K / V scales from what the cache holds now (after a
-        unit-scale prefill): s = 2^ceil(log2(amax / KV_TARGET)) per layer, so
-        the values use the e4m3 normal range instead of its subnormals.  Then
-        clears the cache: the caller re-runs the prefill at the new scale."""
+        prefill at the current scales): s = 2^ceil(log2(amax / KV_TARGET)) per
+        layer, so the values use the e4m3 normal range instead of its
+        subnormals.  The KV store clamps to +-448 before converting, so a
+        cache amax of 448 means the true amax is unknown (larger): that layer
+        retries at ``KV_SAT_JUMP`` x its scale in the next round instead of
+        trusting the clamped value.  Always ``KV_CAL_ROUNDS`` rounds (a fixed
+        count, so every rank of a ring runs the same prefills); a layer still
+        saturated after the last one keeps its largest scale and is reported in
+        ``kv_saturated_layers``.  Clears the cache: the caller re-runs the
+        prefill at the new scales."""
         scales = []
+        self._kv_round = getattr(self, "_kv_round", 0) + 1
+        sat = []
         for li in range(len(self.layers)):
             sk0, sv0 = self.kv_scales[li]
-            ak = _e4m3_amax(self.kc[li]) * sk0
-            av = _e4m3_amax(self.vc[li]) * sv0
-            scales.append(tuple(2.0 ** math.ceil(math.log2(max(a, 1e-30) / self.KV_TARGET)) for a in (ak, av)))
+            new = []
+            for t, s0 in ((self.kc[li], sk0), (self.vc[li], sv0)):
+                a = _e4m3_amax(t)
+                if a >= self.E4M3_MAX:  # clamped: the real amax is above what the cache can show
+                    new.append(s0 * self.KV_SAT_JUMP)
+                    sat.append(li)
+                else:
+                    new.append(2.0 ** math.ceil(math.log2(max(a * s0, 1e-30) / self.KV_TARGET)))
+            scales.append(tuple(new))
+        last = self._kv_round >= self.KV_CAL_ROUNDS
+        if last and sat:  # still clamping after the retry: keep the previous (largest measured-safe) scales
+            import warnings
+            warnings.warn(f"fp8 KV calibration: layers {sorted(set(sat))} still saturate e4m3 after "
+                          f"{self._kv_round} rounds; their K/V clamp at +-448 x scale")
+            scales = [self.kv_scales[li] if li in sat else sc for li, sc in enumerate(scales)]
+        self.kv_saturated_layers = sorted(set(sat)) if last else []
         self.set_kv_scales(scales)
-        self.kv_calibrated = True
+        self.kv_calibrated = last
         self.reset()
         return scales
 

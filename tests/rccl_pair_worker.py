@@ -16,7 +16,7 @@ def main() -> int:
     rank, port, out = int(sys.argv[1]), sys.argv[2], sys.argv[3]
     dist.init_process_group("gloo", rank=rank, world_size=2, init_method=f"tcp://127.0.0.1:{port}")
     from distributed_neural_networks_amd.parallel import rccl
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", rank % max(1, torch.cuda.device_count()))  # one GPU per rank when there are two
     torch.cuda.set_device(dev)
     res = "fail unknown"
     try:
@@ -27,22 +27,33 @@ def main() -> int:
             res = f"init_error {e}"
             ch.abort()
             return 0
-        n = (1 << 20) + 5
-        if rank == 0:
-            x = torch.arange(n, device=dev, dtype=torch.int32) * 3 + 1
-            tok = ch.post(rccl.SEND, x, 1)
-        else:
-            x = torch.zeros(n, device=dev, dtype=torch.int32)
-            tok = ch.post(rccl.RECV, x, 0)
-        try:
-            ch.synchronize(tok, 30)
-        except TimeoutError as e:
-            ch.abort()
-            res = f"fail {e}"
-            return 1
-        torch.cuda.synchronize()
-        ref = torch.arange(n, device=dev, dtype=torch.int32) * 3 + 1
-        res = "ok " + str(int((x - ref).abs().sum().item()))
+        # several messages, 4 B .. 24 MiB + odd tails, all in flight at once,
+        # then the reverse direction; every byte checked on the receiver
+        sizes = [1, (1 << 20) + 5, 7, (6 << 20) + 3, 4096, 3 << 20]
+        bad = 0
+        for direction in (0, 1):
+            sender = direction
+            bufs, toks = [], []
+            for i, n in enumerate(sizes):
+                ref = (torch.arange(n, device=dev, dtype=torch.int32) * (3 + i) + direction) % 1000003
+                if rank == sender:
+                    bufs.append(ref)
+                    toks.append(ch.post(rccl.SEND, ref, 1 - rank))
+                else:
+                    b = torch.full((n,), -1, device=dev, dtype=torch.int32)
+                    bufs.append((b, ref))
+                    toks.append(ch.post(rccl.RECV, b, 1 - rank))
+            try:
+                for t in toks:
+                    ch.synchronize(t, 60)
+            except TimeoutError as e:
+                ch.abort()
+                res = f"fail {e}"
+                return 1
+            torch.cuda.synchronize()
+            if rank != sender:
+                bad += sum(int((b != ref).sum().item()) for b, ref in bufs)
+        res = "ok " + str(bad)
         ch.destroy()
         return 0
     except Exception as e:  # noqa: BLE001

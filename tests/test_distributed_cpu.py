@@ -242,24 +242,33 @@ def test_stream_schedule_gloo(world):
             assert torch.allclose(torch.from_numpy(out[i]), m(x), atol=1e-5)
 
 
-def _bench_cpu(n, *extra, timeout=420):
-    port = free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--cpu",
-           "--batch", "16", "--steps", "2", "--warmup", "1", "--microbatches", "2", "--latency_iters", "3", *extra]
+def _bench_cpu(n, *extra, timeout=420, launcher="torchrun", gpus=None):
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(gpus or n), "--cpu", "--batch", "16", "--steps", "2",
+            "--warmup", "1", "--microbatches", "2", "--latency_iters", "3", *extra]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args]
+    else:  # exactly as the driver invokes it: no launcher, bench.py spawns its own ranks
+        cmd = [sys.executable, *args]
     env = dict(ENV, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 prints exactly one line
+    return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("n", [2, 4, 8])
-def test_bench_pp2_schedule_cpu(n):
+@pytest.mark.parametrize("n,launcher", [(2, "torchrun"), (4, "self"), (8, "torchrun")])
+def test_bench_pp2_schedule_cpu(n, launcher):
     """bench.py's N > 1 headline with gloo on CPU (the driver's N = 2/4/8
     scaling runs use the same schedule over RCCL): the reference cut and
     metric at every N, a real p50 through the hop and back, and the extra
-    keys of BASELINE configs 3-5 (decode rings with per-token p50)."""
-    d = _bench_cpu(n)
+    keys of BASELINE configs 3-5 (decode rings with per-token p50).  N = 4
+    runs as the driver launches it, ``python bench.py --gpus 4`` with no
+    launcher: bench.py must spawn the 4 ranks itself."""
+    d = _bench_cpu(n, launcher=launcher)
     assert d["n_gpus"] == n and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
     assert d["dtype"].startswith("fp32") and "bf16x3" in d["dtype"] and d["scaling"] == "weak"
     assert d["config"]["stage_cut"] == "conv|fc (reference split, 16 KiB/img hop)"
@@ -276,6 +285,48 @@ def test_bench_pp2_schedule_cpu(n):
         assert d[key + "_decode_tok_s"] > 0 and d[key + "_prefill_tok_s"] > 0
         assert d[key + "_p50_token_ms"] > 0
         assert d[key + "_config"]["gpu_groups"] == groups
+
+
+def test_bench_gpus_must_match_world():
+    """Under a launcher, --gpus that disagrees with WORLD_SIZE is an error,
+    never a silently mislabelled number."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "4", "--cpu",
+           "--batch", "16", "--steps", "1", "--warmup", "1", "--no_extra"]
+    r = subprocess.run(cmd, env=dict(ENV, OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "--gpus 4 but the job has 2 rank(s)" in r.stdout + r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_self_launch_failing_rank_fails_job():
+    """A self-launched job whose ranks fail (pp2 needs an even GPU count)
+    exits non-zero and prints no result line."""
+    env = {k: v for k, v in ENV.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--cpu", "--batch", "16",
+                        "--steps", "1", "--warmup", "1", "--no_extra", "--launch_timeout", "120"],
+                       env=dict(env, OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=180)
+    assert r.returncode != 0
+    assert "even GPU count" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_self_launch_timeout_kills_ranks(tmp_path):
+    """The launcher's wall-clock limit ends a hung job with 124 and leaves no rank behind."""
+    from distributed_neural_networks_amd.parallel import selflaunch
+    script = tmp_path / "hang.py"
+    pidfile = tmp_path / "pids"
+    script.write_text("import os, time\n"
+                      f"open({str(pidfile)!r}, 'a').write(str(os.getpid()) + '\\n')\n"
+                      "time.sleep(600)\n")
+    rc = selflaunch.spawn_ranks(2, str(script), [], timeout_s=3)
+    assert rc == 124
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 2
+    for p in pids:
+        with pytest.raises(ProcessLookupError):
+            os.kill(p, 0)
 
 
 @pytest.mark.parametrize("placement,n,fill", [("fc1cut", 4, 8), ("interleaved", 2, 0)])

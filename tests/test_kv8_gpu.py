@@ -239,3 +239,43 @@ def test_llama_tiny_decode_kv8_close_to_bf16(kv_scale, tol_pf):
           f"tokens equal {(t16 == t8).float().mean().item():.3f}")
     assert (t16 == t8).float().mean().item() >= 0.75
     assert _rel(p8, p16) < tol_pf
+
+
+def test_kv8_calibration_recovers_from_saturation():
+    """K / V far above the e4m3 range (|K| ~ 10^4: the K and V rows of the QKV
+    projection scaled up 4096x, q rows and the output projection scaled down
+    to match, so the model's outputs are unchanged).  A unit-scale first
+    prefill stores a clamped cache whose amax reads 448; calibration must not
+    trust that value (it would pick scale 2 and keep clamping) but retry at a
+    larger scale and end with unsaturated layers and logits as close to the
+    bf16 cache as in the unscaled model."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import model_info
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    model = "llama3-tiny"
+    n = model_info(model).num_layers
+    V = model_info(model).cfg.vocab_size
+    B, T0 = 4, 48
+    prompt = torch.randint(0, V, (B, T0), generator=torch.Generator().manual_seed(5))
+    res = {}
+    for kv in ("bf16", "fp8"):
+        st = TransformerStage(model, ckpt.random_stage_state_dict(model, 0, n - 1, True, True, 7, nontrivial=True),
+                              0, n - 1, True, True, DEV, max_batch=B, max_seq=T0 + 4, kv_dtype=kv,
+                              kv_scale="calibrated")
+        big = 2.0 ** -12
+        st.set_kv_scales([(big, big)] * len(st.layers))  # K, V x4096 in the weights ...
+        st.kv_scales = [(1.0, 1.0)] * len(st.layers)     # ... while the cache believes unit scale
+        ring = DecodeRing([st], RingLinks(), 1, 1, B)
+        ring.prefill([prompt], T0)
+        torch.cuda.synchronize()
+        res[kv] = st.logits[:B, :V].float().cpu().clone()
+        if kv == "fp8":
+            assert st.kv_calibrated and st.kv_saturated_layers == [], st.kv_saturated_layers
+            assert all(min(sc) >= 64.0 for sc in st.kv_scales), st.kv_scales
+            amax = max(float(st.kc[:, :B].float().abs().max()), float(st.vc[:, :B].float().abs().max()))
+            assert amax < 448.0, amax  # nothing clamped in the real prefill
+        del st, ring
+    rel = _rel(res["fp8"], res["bf16"])
+    print(f"saturated-start calibration: prefill logits rel {rel:.4f}")
+    assert rel < 0.04

@@ -1,8 +1,10 @@
 """Multi-GPU paths over RCCL/xGMI: one process per GPU,
-launched the way the driver and users launch them.  Skipped below 2 visible
-GPUs (conftest: ``multigpu``); RCCL refuses two ranks on one device, so the
-1-GPU box cannot run these — the same schedules run on gloo in
-``test_distributed_cpu.py``.  Each test keeps to <= 4 ranks and small shapes."""
+launched exactly the way the driver launches the bench — ``python3 bench.py
+--gpus N`` with no launcher, so bench.py spawns its own ranks
+(``parallel/selflaunch.py``).  Skipped below 2 visible GPUs (conftest:
+``multigpu``); RCCL refuses two ranks on one device, so the 1-GPU box cannot
+run these — the same schedules run on gloo in ``test_distributed_cpu.py``.
+Each test keeps to <= 4 ranks and small shapes (except the full-extras one)."""
 import json
 import os
 import socket
@@ -14,7 +16,10 @@ import pytest
 pytestmark = [pytest.mark.gpu, pytest.mark.multigpu]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ENV = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+ENV = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+ENV.update(PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+
+REF_CUT = "conv|fc (reference split, 16 KiB/img hop)"
 
 
 def _port():
@@ -25,27 +30,52 @@ def _port():
     return p
 
 
-def _torchrun(n, script, *args, timeout=300):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, script), *args]
-    r = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+def _bench(*args, timeout=600):
+    """``python3 bench.py ...`` as the driver runs it; returns rank 0's one JSON line."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=ENV, capture_output=True,
+                       text=True, timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    return [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("placement", ["interleaved", "linear"])
-def test_bench_cifar_two_gpus(placement):
-    """The flagship bench on 2 GPUs (RCCL all-to-all / isend-irecv hops)."""
-    out = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "8192",
-                    "--placement", placement, "--latency_iters", "5")
-    d = out[-1]
+def test_bench_pp2_headline_two_gpus():
+    """The N > 1 headline: the reference cut, one stage per GPU, the hop over
+    this package's native RCCL channels (not a ProcessGroupNCCL fallback)."""
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "8192", "--latency_iters", "5",
+               "--no_extra")
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
+    assert d["config"]["p2p"] == "native"
+    assert d["config"]["stage_cut"] == REF_CUT
+    assert d["config"]["parallelism"] == "pp2-rccl-1x1"
+    assert d["p50_latency_ms"] is not None and d["p50_latency_ms"] > 0
+
+
+def test_bench_fc1cut_two_gpus():
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "8192", "--placement", "fc1cut",
+               "--no_extra")
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["p2p"] == "native"
+    assert d["config"]["stage_cut"].startswith("conv+fc1|fc2")
+
+
+def test_bench_full_line_two_gpus():
+    """The complete multi-GPU line the driver records: headline plus the
+    fc1-cut and the BASELINE config 3/4/5 decode rings over RCCL."""
+    d = _bench("--gpus", "2", "--steps", "5", "--warmup", "2", timeout=1100)
+    assert d["n_gpus"] == 2 and d["config"]["p2p"] == "native" and d["config"]["stage_cut"] == REF_CUT
+    assert "extras_error" not in d, d.get("extras_error")
+    assert d["fc1cut_images_per_s"] > 0
+    for key in ("gpt2_4stage", "llama3_8b_8stage_b32", "gpt2xl_fp8_8stage_b64"):
+        assert key + "_error" not in d, d.get(key + "_error")
+        assert d[key + "_decode_tok_s"] > 0 and d[key + "_prefill_tok_s"] > 0 and d[key + "_p50_token_ms"] > 0
+        assert d[key + "_config"]["gpu_groups"] == 2
 
 
 def test_bench_gpt2_pipeline_two_gpus():
     """GPT-2 small, 4 stages over 2 GPU groups: prefill + microbatched ring decode."""
-    out = _torchrun(2, "bench.py", "--model", "gpt2", "--gpus", "2", "--steps", "4", "--warmup", "1")
-    assert out[-1]["n_gpus"] == 2 and out[-1]["value"] > 0
+    d = _bench("--model", "gpt2", "--gpus", "2", "--steps", "4", "--warmup", "1")
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["gpu_groups"] == 2
 
 
 def test_cli_rccl_two_stage(tmp_path):

@@ -35,3 +35,93 @@ def test_library_resolves_rccl():
         pytest.skip("kernel library not built")
     from distributed_neural_networks_amd.parallel import rccl
     assert rccl.available()
+
+
+class _FakeChannel:
+    """Stands in for rccl.Channel (no device): records destroy/abort."""
+    destroyed = []
+
+    def __init__(self, uid, nranks, rank, device, key=None, uid_fn=None):
+        self.key, self.device, self.closed, self.aborted = key, device, False, False
+
+    def abort(self):
+        self.aborted = True
+
+    def destroy(self):
+        self.closed = True
+        _FakeChannel.destroyed.append(self.key)
+
+
+class _FakeStore:
+    def __init__(self):
+        self.kv = {}
+
+    def set(self, k, v):
+        self.kv[k] = v
+
+    def get(self, k):
+        return self.kv[k]
+
+
+@pytest.fixture
+def fake_rccl(monkeypatch):
+    from distributed_neural_networks_amd.parallel import rccl
+
+    class _Lib:
+        @staticmethod
+        def comm_unique_id():
+            return b"\0" * 128
+
+    monkeypatch.setattr(rccl, "Channel", _FakeChannel)
+    monkeypatch.setattr(rccl, "_lib", lambda: _Lib)
+    monkeypatch.setattr(rccl, "_CHANNELS", {})
+    _FakeChannel.destroyed = []
+    return rccl
+
+
+def test_channel_scopes_bound_the_live_set(fake_rccl):
+    """bench.py opens each measurement's channel set inside rccl.scope():
+    the N = 8 pp2 bipartite hop + back-edge, the preflight ring (forward and
+    back tags), then three decode rings with their back-edges — after every
+    scope the live channel count is back at the baseline, and a channel that
+    existed before a scope is not closed by it."""
+    rccl = fake_rccl
+    dev = torch.device("cpu")
+    st = _FakeStore()
+    pre = rccl.pair_channel(0, 1, dev, "world", store=st)  # opened outside any scope: survives
+    base = rccl.live_channels()
+    assert base == 1
+    with rccl.scope(dev):  # preflight: ring neighbours, forward + back
+        for tag in ("world", "back"):
+            rccl.pair_channel(0, 1, dev, tag, store=st)
+            rccl.pair_channel(0, 7, dev, tag, store=st)
+        assert rccl.live_channels() == base + 3  # (world, 0-1) already existed
+    assert rccl.live_channels() == base and not pre.closed
+    with rccl.scope(dev):  # pp2 at N = 8: stage-0 rank 0 -> stage-1 ranks 1, 3, 5, 7; back-edge 0-1
+        for p in (1, 3, 5, 7):
+            rccl.pair_channel(0, p, dev, "world", store=st)
+        rccl.pair_channel(0, 1, dev, "back", store=st)
+        assert rccl.live_channels() == base + 4
+    assert rccl.live_channels() == base
+    for ring in range(3):  # decode rings: prev/next + back-edge, one scope each
+        with rccl.scope(dev):
+            with rccl.scope(dev):  # nested scopes close their own channels only
+                rccl.pair_channel(0, 2, dev, "world", store=st)
+            assert rccl.live_channels() == base
+            rccl.pair_channel(0, 3, dev, "back", store=st)
+            assert rccl.live_channels() == base + 1
+        assert rccl.live_channels() == base
+    assert ("world", (0, 1)) not in _FakeChannel.destroyed
+
+
+def test_channel_scope_aborts_on_error(fake_rccl):
+    """A measurement that raises leaves no channel draining the device: the
+    scope aborts (in-flight ops return) before it destroys."""
+    rccl = fake_rccl
+    dev = torch.device("cpu")
+    st = _FakeStore()
+    with pytest.raises(RuntimeError):
+        with rccl.scope(dev):
+            c = rccl.pair_channel(2, 5, dev, "world", store=st)
+            raise RuntimeError("peer died")
+    assert c.aborted and c.closed and rccl.live_channels() == 0

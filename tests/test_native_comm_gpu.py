@@ -115,7 +115,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_pair_channel_two_processes(tmp_path):
+def _pair_results(tmp_path):
     port = str(_free_port())
     outs = [str(tmp_path / f"r{r}.txt") for r in range(2)]
     env = dict(os.environ, PYTHONPATH=ROOT)
@@ -132,9 +132,20 @@ def test_pair_channel_two_processes(tmp_path):
                 p.kill()
     res = [open(o).read().strip() if os.path.exists(o) else "missing" for o in outs]
     print("pair channel results:", res)
+    return res, logs
+
+
+def test_pair_channel_two_processes(tmp_path):
+    """Two processes, a pair channel bootstrapped through the TCP store,
+    six messages up to 6 MiB each way, every byte checked.  On a 1-GPU box
+    RCCL refuses two ranks on one device: that is reported as a SKIP (the
+    data path did not run), never as a pass."""
+    res, logs = _pair_results(tmp_path)
     assert all(r.startswith(("ok", "init_error")) for r in res), (res, logs)
-    if res[1].startswith("ok"):
-        assert res[1] == "ok 0", res  # the receiver got exactly the sender's bytes
+    if any(r.startswith("init_error") for r in res):
+        assert torch.cuda.device_count() < 2, (res, logs)  # with two GPUs the pair must work
+        pytest.skip(f"RCCL refused the pair on one device: {res}")
+    assert res == ["ok 0", "ok 0"], res  # both receivers got exactly the senders' bytes
 
 
 def test_native_preflight_two_processes(tmp_path):

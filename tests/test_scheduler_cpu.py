@@ -323,3 +323,63 @@ def test_decode_ring_single_microbatch_resume_gloo():
     assert len(toks[0][0]) == 6 and len(toks[1][0]) == 3
     assert toks[0] == _golden_tokens("gpt2-tiny", 4, 5, prompts[0], 6)
     assert toks[1] == _golden_tokens("gpt2-tiny", 4, 5, prompts[1], 3)
+
+
+def _ring_prepost_worker(rank, world, port, q, M, rounds):
+    os.environ["DNN_DEBUG_ORDER"] = "1"  # every slot transition of the pre-posted receives is checked
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import default_ranges
+    from distributed_neural_networks_amd.parallel import comm
+    from distributed_neural_networks_amd.parallel.links import P2PLink
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.stages import TorchStage
+    torch.set_num_threads(1)
+    info = comm.init("gloo", rank=rank, world=world, master_addr="127.0.0.1", master_port=port)
+    bg = comm.back_group()
+    a, b = default_ranges("gpt2-tiny", world)[rank]
+    first, last = rank == 0, rank == world - 1
+    st = TorchStage("gpt2-tiny", ckpt.random_stage_state_dict("gpt2-tiny", a, b, first, last, 5), a, b, first, last)
+    links = RingLinks(prev=P2PLink(rank - 1, info.device) if rank > 0 else None,
+                      nxt=P2PLink(rank + 1, info.device) if not last else None,
+                      back_out=P2PLink(0, info.device, bg) if last else None,
+                      back_in=P2PLink(world - 1, info.device, bg) if first else None)
+    ring = DecodeRing([st], links, world, M, 2)
+    assert ring.rorder.enabled
+    g = torch.Generator().manual_seed(9)
+    prompts = [torch.randint(0, 512, (2, 5), generator=g) for _ in range(M)] if first else None
+    ring.prefill(prompts, 5)
+    ring.decode_rounds(rounds)
+    ring.drain()
+    ring.decode_round([0])   # a lone single-microbatch round (the bench's latency rounds) between two runs
+    ring.drain()
+    ring.decode_rounds(2)
+    ring.drain()
+    if first:
+        q.put(([p.tolist() for p in prompts], [torch.stack(t, 1).tolist() for t in ring.toks]))
+    comm.barrier(info)
+    comm.shutdown()
+
+
+@pytest.mark.parametrize("world,M", [(3, 6), (2, 1), (4, 4)])
+def test_decode_ring_preposted_receives_gloo(world, M):
+    """decode_rounds posts the next microbatch's receive (hidden states, or the
+    token over the back-edge on group 0) before launching this microbatch:
+    with M > G, M = G and M = 1 (no pre-post possible), interleaved with a
+    single-microbatch round, every sequence's greedy tokens equal the golden
+    and DNN_DEBUG_ORDER finds no slot reused under a pending receive."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    rounds = 3
+    ps = [ctx.Process(target=_ring_prepost_worker, args=(r, world, port, q, M, rounds)) for r in range(world)]
+    for p in ps:
+        p.start()
+    prompts, toks = q.get(timeout=240)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for m in range(M):
+        n = 1 + rounds + (1 if m == 0 else 0) + 2
+        assert len(toks[m][0]) == n
+        assert toks[m] == _golden_tokens("gpt2-tiny", 4, 5, prompts[m], n)
