@@ -48,6 +48,9 @@ def parse(argv=None):
     ap.add_argument("--kv", default="bf16", choices=["bf16", "fp8"], help="KV cache dtype (fp8: OCP e4m3)")
     ap.add_argument("--kv_scale", default="calibrated", choices=["calibrated", "unit"],
                     help="fp8 KV cache scale: per-layer, from the first prefill's amax, or unit")
+    ap.add_argument("--fp8_prefill", default="split", choices=["split", "e4m3"],
+                    help="fp8 weights: prefill activations split (e4m3 hi + residual, ~0.1 %% logits error) or one "
+                         "e4m3 byte (2x faster prefill GEMMs, ~6 %% logits error)")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     ap.add_argument("--gloo_gpu", action="store_true",
@@ -59,7 +62,8 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16", kv_scale="calibrated"):
+def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16", kv_scale="calibrated",
+                 fp8_prefill="split"):
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import TorchStage
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
@@ -73,7 +77,8 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf1
             continue
         sd = ckpt.random_stage_state_dict(model, a, b, s == 0, s == S - 1, 0, device=dev)
         out.append(TransformerStage(model, sd, a, b, s == 0, s == S - 1, dev, max_batch=max_batch,
-                                    max_seq=max_seq, fp8=fp8, kv_dtype=kv, kv_scale=kv_scale))
+                                    max_seq=max_seq, fp8=fp8, kv_dtype=kv, kv_scale=kv_scale,
+                                    fp8_prefill=fp8_prefill))
         del sd
     return out
 
@@ -137,7 +142,8 @@ def run(args=None, shutdown: bool = True):
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
     kv = getattr(args, "kv", "bf16")
-    stages = (_build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv, getattr(args, "kv_scale", "calibrated"))
+    stages = (_build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv, getattr(args, "kv_scale", "calibrated"),
+                           getattr(args, "fp8_prefill", "split"))
               if stage_ids else [])
     base = rep * groups
     prev = make_link(base + grp - 1, dev) if grp > 0 else None
@@ -255,7 +261,9 @@ def run(args=None, shutdown: bool = True):
             "metric": f"tokens/sec {model} {S}-stage greedy decode", "value": round(value, 1), "unit": "tokens/s",
             "n_gpus": N, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(decode_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": ("fp8-e4m3 weights (decode: W8A16 on bf16 MFMA; prefill: W8A8 on fp8 MFMA), bf16 activations"
+            "dtype": (("fp8-e4m3 weights (decode: W8A16 on bf16 MFMA; prefill: fp8 MFMA on split activations, "
+                       "e4m3 hi + e4m3 residual), bf16 activations") if fp8 and args.fp8_prefill == "split" else
+                      "fp8-e4m3 weights (decode: W8A16 on bf16 MFMA; prefill: W8A8 on fp8 MFMA), bf16 activations"
                       if fp8 else "bf16") + ("; fp8-e4m3 KV cache" if kv == "fp8" else ""),
             "data": "synthetic prompts, random-init weights",
             "prefill_tokens_per_s": round(prefill_tok / prefill_s, 1),

@@ -62,6 +62,14 @@ PYBIND11_MODULE(_dnn_hip, m) {
      py::arg("ws_bytes") = 0);
   m.def("gemm_set_stream", [](int on, long long min_bytes, int fold) { return dnn_gemm_set_stream(on, min_bytes, fold); },
         py::arg("on"), py::arg("min_bytes"), py::arg("fold") = -1);
+  m.def("gemm_set_oneshot", [](int on, int mt, int ntw, int steps, int splitk) {
+    return dnn_gemm_set_oneshot(on, mt, ntw, steps, splitk);
+  }, py::arg("on"), py::arg("mt") = 0, py::arg("ntw") = 0, py::arg("steps") = 0, py::arg("splitk") = 0);
+  m.def("gemm_oneshot_sweep", [](u64 A, int lda, u64 Wsh, u64 sw, u64 C, int ldc, int M, int N, int K, int mt, int ntw,
+                                 int steps, int splitk, int w8, u64 ws, long long ws_bytes, u64 st) {
+    return dnn_gemm_oneshot_sweep(CP(A), lda, CP(Wsh), CFP(sw), P(C), ldc, M, N, K, mt, ntw, steps, splitk, w8, P(ws),
+                                  ws_bytes, ST(st));
+  });
   m.def("gemm_skinny_sweep", [](u64 A, int lda, u64 W, int ldw, u64 sw, u64 C, int ldc, int M, int N, int K, int nt,
                                 int u, int ks, int pipe, int w8, u64 st) {
     return dnn_gemm_skinny_sweep(CP(A), lda, CP(W), ldw, CFP(sw), P(C), ldc, M, N, K, nt, u, ks, pipe, w8, ST(st));
@@ -120,9 +128,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_layernorm(CP(x), ldx, CFP(w), CFP(b), P(y), ldy, M, N, eps, rms, ST(st));
   });
   m.def("layernorm_q8", [](u64 x, int ldx, u64 w, u64 b, u64 q, int ldq, u64 sq, int M, int N, int kpad, float eps,
-                           int rms, u64 st) {
-    return dnn_layernorm_q8(CP(x), ldx, CFP(w), CFP(b), P(q), ldq, FP(sq), M, N, kpad, eps, rms, ST(st));
-  });
+                           int rms, u64 st, int split) {
+    return dnn_layernorm_q8(CP(x), ldx, CFP(w), CFP(b), P(q), ldq, FP(sq), M, N, kpad, eps, rms, ST(st), split);
+  }, py::arg("x"), py::arg("ldx"), py::arg("w"), py::arg("b"), py::arg("q"), py::arg("ldq"), py::arg("sq"), py::arg("M"),
+     py::arg("N"), py::arg("kpad"), py::arg("eps"), py::arg("rms"), py::arg("st"), py::arg("split") = 0);
   m.def("embed_gpt2", [](u64 idx, u64 wte, u64 wpe, u64 out, int B, int T, int d, u64 pos, int V, int Pn, u64 st) {
     return dnn_embed_gpt2(CIP(idx), CP(wte), CP(wpe), P(out), B, T, d, CIP(pos), V, Pn, ST(st));
   });
@@ -167,9 +176,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st), IP(out2), IP(pos_inc), reinterpret_cast<void*>(static_cast<uintptr_t>(part)));
   }, py::arg("x"), py::arg("ld"), py::arg("M"), py::arg("N"), py::arg("out"), py::arg("f32in"), py::arg("st"),
      py::arg("out2") = 0, py::arg("pos_inc") = 0, py::arg("part") = 0);
-  m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, int kpad, u64 st) {
-    return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, kpad, ST(st));
-  });
+  m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, int kpad, u64 st, int split) {
+    return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, kpad, ST(st), split);
+  }, py::arg("x"), py::arg("ldx"), py::arg("q"), py::arg("scale"), py::arg("M"), py::arg("K"), py::arg("kpad"),
+     py::arg("st"), py::arg("split") = 0);
   m.def("gemm_fp8", [](u64 A, u64 sa, u64 W, u64 sw, u64 C, int ldc, u64 bias, u64 R, int ldr, int M, int N, int K,
                        int act, u64 st) {
     return dnn_gemm_fp8(CP(A), CFP(sa), CP(W), CFP(sw), P(C), ldc, CFP(bias), CP(R), ldr, M, N, K, act, ST(st));

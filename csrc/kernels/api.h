@@ -40,6 +40,12 @@ int dnn_gemm_skinny(const void* A, int lda, const float* sa, const void* W, int 
 // decode stream GEMM (gemm_stream.h) switch: 0 off / 1 auto / 2 forced, the weight-byte threshold (<= 0
 // keeps it), and the in-launch split-K combine (fold: 1 on, 0 reduce launch, -1 keep)
 int dnn_gemm_set_stream(int on, long long min_bytes, int fold = -1);
+// one-shot decode GEMM (gemm_oneshot.h): on 0 off / 1 planned shapes / 2 every eligible shape; a non-zero
+// (mt, ntw, steps, splitk) pins that config for every eligible call (A/B probes)
+int dnn_gemm_set_oneshot(int on, int mt, int ntw, int steps, int splitk);
+int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
+                           int K, int mt, int ntw, int steps, int splitk, int w8, void* ws, long long ws_bytes,
+                           hipStream_t st);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
@@ -55,8 +61,9 @@ int dnn_cifar_head_tail_x3(const float* hid, const void* w2h, const void* w2l, c
                            int B, hipStream_t st);
 int dnn_cifar_head_tail(const void* hid, const void* w2p, const float* b2, float* probs, int* pred, int B,
                         hipStream_t st);
+// split: rows of 2 kpad bytes, e4m3 hi plane then the residual plane (W8A8 prefill with split activations)
 int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq, int M, int N,
-                     int kpad, float eps, int rms, hipStream_t st);
+                     int kpad, float eps, int rms, hipStream_t st, int split = 0);
 int dnn_layernorm(const void* x, int ldx, const float* w, const float* b, void* y, int ldy, int M, int N, float eps,
                   int rms, hipStream_t st);
 int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, void* out, int B, int T, int d, const int* pos,
@@ -76,7 +83,8 @@ int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float tempera
                     const int* step, hipStream_t st);
 int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st, int* out2 = nullptr,
                     int* pos_inc = nullptr, void* part = nullptr);
-int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, int kpad, hipStream_t st);
+int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, int kpad, hipStream_t st,
+                       int split = 0);
 int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,
                  const void* R, int ldr, int M, int N, int K, int act, hipStream_t st);
 }

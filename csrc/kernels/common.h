@@ -107,6 +107,30 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_wave_base, 16, 0, 0);
 }
 
+// Split ("x2") activations for the W8A8 prefill: the e4m3 hi byte of y and
+// the e4m3 rounding of its residual (y - hi) * 16, written as a second K plane
+// (row bytes kpad..2 kpad-1).  Against [W | W / 16] along K the fp8 GEMM then
+// sums hi.W + lo.W/16 = y.W to ~2^-8 relative per activation instead of the
+// 2^-4 of one e4m3 byte (GPT-2 XL 2 blocks: logits 5.7 % -> 0.13 % from the
+// fp32 golden, emulated; measured on the device by tests/test_transformer_gpu.py).
+__device__ __forceinline__ void q8_split8(const float (&y)[8], int& h0, int& h1, int& l0, int& l1) {
+  h0 = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
+  h0 = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], h0, true);
+  h1 = __builtin_amdgcn_cvt_pk_fp8_f32(y[4], y[5], 0, false);
+  h1 = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], h1, true);
+  const float d[8] = {__builtin_amdgcn_cvt_f32_fp8(h0, 0), __builtin_amdgcn_cvt_f32_fp8(h0, 1),
+                      __builtin_amdgcn_cvt_f32_fp8(h0, 2), __builtin_amdgcn_cvt_f32_fp8(h0, 3),
+                      __builtin_amdgcn_cvt_f32_fp8(h1, 0), __builtin_amdgcn_cvt_f32_fp8(h1, 1),
+                      __builtin_amdgcn_cvt_f32_fp8(h1, 2), __builtin_amdgcn_cvt_f32_fp8(h1, 3)};
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (y[j] - d[j]) * 16.f;
+  l0 = __builtin_amdgcn_cvt_pk_fp8_f32(r[0], r[1], 0, false);
+  l0 = __builtin_amdgcn_cvt_pk_fp8_f32(r[2], r[3], l0, true);
+  l1 = __builtin_amdgcn_cvt_pk_fp8_f32(r[4], r[5], 0, false);
+  l1 = __builtin_amdgcn_cvt_pk_fp8_f32(r[6], r[7], l1, true);
+}
+
 // Bijective XCD-aware block remap: blocks that the dispatcher places on the same
 // XCD (b % 8 equal) get a contiguous range of logical tile ids (guide §5, T1).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

@@ -121,6 +121,8 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(const uint8_t* __restr
 }
 
 // Per-row absmax quantisation bf16 -> e4m3 (scale = amax / 448). One wave per row.
+// SPLIT: rows of 2 kpad bytes, the residual plane after the kpad bytes of hi.
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, int ldx, uint8_t* __restrict__ q,
                                                              float* __restrict__ scale, int M, int K, int kpad) {
   const int lane = threadIdx.x & 63;
@@ -137,10 +139,20 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
   const float s = amax > 0.f ? amax / 448.f : 1.f;
   const float inv = 1.f / s;
   if (lane == 0) scale[row] = s;
-  uint8_t* qr = q + (size_t)row * kpad;
+  uint8_t* qr = q + (size_t)row * kpad * (SPLIT ? 2 : 1);
   for (int c = lane * 8; c < kpad; c += 512) {
     bf16x8 p = {0, 0, 0, 0, 0, 0, 0, 0};  // zero K-padding (K -> multiple of 128)
     if (c < K) p = *reinterpret_cast<const bf16x8*>(xr + c);
+    if constexpr (SPLIT) {
+      float y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = bf2f_s(p[j]) * inv;
+      int h0, h1, l0, l1;
+      q8_split8(y, h0, h1, l0, l1);
+      *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)h0, (uint32_t)h1);
+      *reinterpret_cast<uint2*>(qr + kpad + c) = make_uint2((uint32_t)l0, (uint32_t)l1);
+      continue;
+    }
     int lo = 0, hi = 0;
     lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f_s(p[0]) * inv, bf2f_s(p[1]) * inv, lo, false);
     lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f_s(p[2]) * inv, bf2f_s(p[3]) * inv, lo, true);
@@ -189,9 +201,13 @@ extern "C" int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const
 }
 
 extern "C" int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, int kpad,
-                                  hipStream_t st) {
+                                  hipStream_t st, int split) {
   if (K % 8 != 0 || kpad % 8 != 0 || kpad < K) return -1;
-  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, ldx, (uint8_t*)q,
-                     scale, M, K, kpad);
+  if (split)
+    hipLaunchKernelGGL(quant_fp8_rows_kernel<true>, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, ldx,
+                       (uint8_t*)q, scale, M, K, kpad);
+  else
+    hipLaunchKernelGGL(quant_fp8_rows_kernel<false>, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, ldx,
+                       (uint8_t*)q, scale, M, K, kpad);
   return (int)hipGetLastError();
 }

@@ -1,0 +1,271 @@
+// One-shot decode GEMM for 17..64 rows ("oneshot" kernel):
+//   C[M,N] = epi(A[M,K] . W[N,K]^T), W in fragment order (ops/gemm.py
+//   shuffle_weight), bf16 or OCP e4m3 (W8A16), bf16 activations.
+//
+// Why a third decode GEMM.  At 32-64 rows the mid-size projections (GPT-2 /
+// GPT-2 XL, Llama-3 QKV / O) are neither compute- nor HBM-bound: a 2.5-10 MB
+// weight matrix is a few microseconds of HBM, but gemm_skinny streams each
+// wave's K slice in batches of U chunks, each batch a dependent memory round
+// trip (3-7 per wave, ~1-2 us each under load), with the activations loaded
+// fragment-shaped (16 rows x 64 B per instruction: twice the TA work of a
+// full-line load, guide §5 "x operand through LDS in full lines"); the sweep
+// (profiles/r1_skinny_sweep_shuf_fit.jsonl) puts every configuration at
+// 0.4-0.9 TB/s on those shapes.  gemm_stream fixes the A path but pipelines
+// K-steps, which only pays for >= 8 MB weights with >= 6 steps per slice.
+//
+// Here a workgroup issues EVERY load of its work at once and waits once:
+//   * tile = MP = 16 MT rows x BN = 16 NTW columns x one K slice; the 4 waves
+//     split the slice into contiguous quarters (no cross-wave operand sharing,
+//     so no barrier before the MFMAs);
+//   * each wave copies its A rows [MP][its quarter] into a private LDS image
+//     by LDS-DMA (global_load_lds_dwordx4, full 128-B lines: an instruction
+//     moves 2 rows x 512 B), in steps of 512 B per row with 16-B slot j of row
+//     r at j ^ (r & 15) — the stream kernel's image, conflict-free for every
+//     ds_read_b128 fragment read — the swizzle applied on the source address
+//     (LDS-DMA writes lane-linear);
+//   * each wave loads its quarter of the NTW weight tiles straight to VGPRs,
+//     non-temporally (read once), all chunks in flight;
+//   * one vmcnt(0), then MFMAs from LDS fragments x register weights; the 4
+//     partial sums meet in LDS (each wave reuses its own image region), and
+//     the epilogue runs in the workgroup (bias / GELU / residual / packed
+//     SwiGLU / fp8 channel scale / folded pre-norm from row statistics
+//     accumulated off the A fragments), or
+//   * SPLIT: fp32 partials of the slice in gemm_stream's slab layout
+//     [slice][MPT][Ns] (+ row statistics [tile][slice][MPT][2]), summed with
+//     the epilogue by gemm_stream_reduce.
+// The M split (MT < 4 at M = 64) puts the m-groups of one (tile, slice)
+// on consecutive logical ids of one XCD, so the weight slice comes from HBM
+// once and the other m-groups re-read it from that XCD's L2.
+#pragma once
+#include "gemm_stream.h"
+
+namespace dnn {
+
+constexpr int OS_SB = 512;  // A bytes per row per LDS step (bf16: 8 chunks of 32 k; W8: 4 chunks of 64 k)
+
+template <int MT, int STEPS>
+constexpr int os_lds_bytes() {
+  return 4 * STEPS * MT * 16 * OS_SB + 4 * MT * 2 * 16 * 4;  // 4 wave images + row statistics
+}
+
+template <int MT, int NTW, bool W8, int NORM, int ACT, bool SPLIT, int STEPS>
+__global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __restrict__ A, int lda_b,
+                                                              const uint8_t* __restrict__ Wsh,
+                                                              const float* __restrict__ sw, void* __restrict__ Cv,
+                                                              int ldc, const float* __restrict__ bias,
+                                                              const bf16_t* __restrict__ R, int ldr, int M, int N,
+                                                              int nch, int cps, const float* __restrict__ colsum,
+                                                              float eps, int kelems, float* __restrict__ slab,
+                                                              int ntiles, int mgroups) {
+  using Cfg = StrCfg<W8>;
+  constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
+  constexpr int MP = MT * 16;
+  constexpr int BN = 16 * NTW;
+  constexpr int CPW = STEPS * CS;                  // max chunks per wave
+  constexpr int IMG = STEPS * MP * OS_SB;          // one wave's A image
+  constexpr int GPS = MP * OS_SB / 1024;           // LDS-DMA instructions per step
+  extern __shared__ __attribute__((aligned(1024))) char os_lds[];
+  float* st_lds = reinterpret_cast<float*>(os_lds + 4 * IMG);  // [4 waves][MT][2][16]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = xcd_remap(blockIdx.x, gridDim.x);
+  // tile-major inside a slice, m-group fastest: one (tile, slice)'s m-groups
+  // are consecutive logical ids (one XCD: its weight slice is fetched once)
+  const int mg = lg % mgroups;
+  const int rest = lg / mgroups;
+  const int tile = rest % ntiles, slice = rest / ntiles;
+  const int m0 = mg * MP;
+  const int ntile16 = (N + 15) >> 4;
+
+  // this wave's chunk range [w0, w1) inside the slice
+  const int s0 = slice * cps, s1 = min(nch, s0 + cps);
+  const int cpw = (cps + 3) >> 2;
+  const int w0 = min(s1, s0 + wave * cpw), w1 = min(s1, w0 + cpw);
+  const int nvalid = w1 - w0;  // 0..CPW, wave-uniform
+
+  char* img = os_lds + wave * IMG;
+  // ---- issue: A rows by LDS-DMA (full lines), then every weight chunk
+  {
+    const int kb0 = w0 * ACH;                      // first A byte of the wave's range in a row
+    // last valid 16 B of the range (surplus slots clamp here; their weights are zeroed)
+    const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+#pragma unroll
+      for (int p = 0; p < GPS; ++p) {
+        const int r = 2 * p + (lane >> 5);         // row inside the step image
+        const int j = lane & 31;                   // LDS slot of this lane
+        const int g = j ^ (r & 15);                // global slot it holds
+        const int row = min(m0 + r, M - 1);
+        const int kb = min(kb0 + s * OS_SB + g * 16, kb_last);
+        glds16(A + (size_t)row * lda_b + kb, img + s * MP * OS_SB + p * 1024);
+      }
+    }
+  }
+  i32x4 wv[NTW][CPW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    int ct = tile * NTW + j;
+    ct = ct < ntile16 ? ct : ntile16 - 1;
+    const uint8_t* wp = Wsh + ((size_t)ct * nch) * 1024 + lane * 16;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int cc = min(min(w0 + c, max(w1, w0 + 1) - 1), nch - 1);
+      wv[j][c] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + (size_t)cc * 1024));
+    }
+  }
+  const int fr = lane & 15, fg = lane >> 4;
+  float shift[MT], s1s[MT], s2s[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    shift[t] = 0.f;
+    s1s[t] = s2s[t] = 0.f;
+    if constexpr (NORM == 2) {
+      const int row = min(m0 + 16 * t + fr, M - 1);
+      shift[t] = bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)row * lda_b));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[NTW][MT];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const int s = c / CS, cc = c % CS;
+    const bool valid = c < nvalid;  // wave-uniform
+    if (!valid) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) wv[j][c] = i32x4{0, 0, 0, 0};
+    }
+    bf16x8 af[MT][AU];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int h = 0; h < AU; ++h) {
+        const int row = 16 * t + fr;
+        const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
+        af[t][h] = *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
+      }
+    if constexpr (NORM != 0) {
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int h = 0; h < AU; ++h) str_stats<NORM>(af[t][h], shift[t], s1s[t], s2s[t]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      if constexpr (W8) {
+        bf16x8 wlo, whi;
+        bf16x2v o[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[2 * i] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)wv[j][c][i], 1.0f, false);
+          o[2 * i + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((uint32_t)wv[j][c][i], 1.0f, true);
+        }
+        __builtin_memcpy(&wlo, &o[0], 16);
+        __builtin_memcpy(&whi, &o[4], 16);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, af[t][0], acc[j][t], 0, 0, 0);
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi, af[t][AU - 1], acc[j][t], 0, 0, 0);
+        }
+      } else {
+        bf16x8 wf;
+        __builtin_memcpy(&wf, &wv[j][c], 16);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af[t][0], acc[j][t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- row statistics of this wave's K range: the 4 lane groups hold disjoint k
+  if constexpr (NORM != 0) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      float a = s1s[t], q = s2s[t];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        st_lds[((wave * MT + t) * 2 + 0) * 16 + lane] = a;
+        st_lds[((wave * MT + t) * 2 + 1) * 16 + lane] = q;
+      }
+    }
+  }
+  // ---- the 4 K-quarters meet in LDS: each wave parks its sums in its own
+  // image (its fragment reads are complete), then every wave reads all four
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  f32x4* red = reinterpret_cast<f32x4*>(img);
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) red[(j * MT + t) * 64 + lane] = acc[j][t];
+  __syncthreads();
+
+  const int Ns = ntiles * BN;
+  const int MPT = mgroups * MP;
+  for (int q = wave; q < NTW * MT; q += 4) {
+    const int j = q / MT, t = q % MT;
+    f32x4 v = reinterpret_cast<const f32x4*>(os_lds)[(j * MT + t) * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += reinterpret_cast<const f32x4*>(os_lds + w * IMG)[(j * MT + t) * 64 + lane];
+    const int ml = 16 * t + fr;       // row inside the m-group
+    const int m = m0 + ml;
+    const int nb = (tile * NTW + j) * 16;
+    const int n = nb + fg * 4;
+    float a = 0.f, q2 = 0.f;
+    if constexpr (NORM != 0) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        a += st_lds[((w * MT + t) * 2 + 0) * 16 + fr];
+        q2 += st_lds[((w * MT + t) * 2 + 1) * 16 + fr];
+      }
+    }
+    if constexpr (SPLIT) {
+      *reinterpret_cast<f32x4*>(slab + ((size_t)slice * MPT + m) * Ns + n) = v;
+      if constexpr (NORM != 0) {
+        if (tile == 0 && j == 0 && lane < 16) {  // statistics once per (slice, row): tile 0 (gemm_stream_reduce reads tile 0)
+          float* st = slab + (size_t)(cps > 0 ? (nch + cps - 1) / cps : 1) * MPT * Ns +
+                      ((size_t)slice * MPT + m) * 2;
+          st[0] = a;
+          st[1] = q2;
+        }
+      }
+      continue;
+    } else {
+      if constexpr (W8) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= n + r < N ? sw[n + r] : 0.f;
+      }
+      if constexpr (NORM != 0) {
+        const float invk = 1.f / (float)kelems, d = a * invk;
+        const float mean = NORM == 2 ? shift[t] + d : 0.f;
+        const float var = NORM == 2 ? fmaxf(q2 * invk - d * d, 0.f) : q2 * invk;
+        const float rstd = rsqrtf(var + eps);
+        if constexpr (NORM == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = rstd * (v[r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+        } else {
+          v *= rstd;
+        }
+      }
+      const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
+      if constexpr (ACT == ACT_SILU_MUL) {
+        epi_silu_t4<false>(v, m, nb / 2, M, N / 2, Cv, ldc, vec, lane);
+      } else {
+        epi_t4<ACT, false>(v, m, n, M, N, Cv, ldc, bias, R, ldr, vec);
+      }
+    }
+  }
+}
+
+}  // namespace dnn

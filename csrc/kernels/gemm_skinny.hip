@@ -29,6 +29,7 @@
 // and so the step time halve.  KS is chosen on the host so that N/16 x KS waves
 // cover the CUs.
 #include "gemm_epilogue.h"
+#include "gemm_oneshot.h"
 #include "gemm_stream.h"
 
 namespace dnn {
@@ -437,6 +438,144 @@ static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const flo
   return (int)hipGetLastError();
 }
 
+// ---- one-shot kernel dispatch (gemm_oneshot.h): 17..64 rows, fragment-order
+// weights.  A config is (MT rows/16 per workgroup, NTW column tiles, STEPS
+// LDS steps per wave, split-K); the plan below is fitted to
+// bench/oneshot_sweep.py, and dnn_gemm_set_oneshot can pin a config (A/B).
+static int g_os_on = 1;                             // 0 off, 1 planned shapes, 2 every eligible shape (tests)
+static int g_os_pin[4] = {0, 0, 0, 0};              // mt, ntw, steps, splitk (0 = planned)
+
+struct OsCfg {
+  int mt = 0, ntw = 0, steps = 0, splitk = 1;
+};
+
+static long long os_ws_need(const OsCfg& c, int M, int N) {
+  if (c.splitk <= 1) return 0;
+  const int MP = 16 * c.mt, mgroups = (M + MP - 1) / MP, BN = 16 * c.ntw;
+  const long long Ns = (long long)((N + BN - 1) / BN) * BN, MPT = (long long)mgroups * MP;
+  return (long long)c.splitk * MPT * Ns * 4 + (long long)c.splitk * MPT * 2 * 4;
+}
+
+// The plan (profiles/r4_oneshot_sweep*.jsonl): returns false where gemm_skinny /
+// gemm_stream stay.
+template <bool W8>
+static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, OsCfg& c) {
+  const int nch = kbytes / 64, CS = W8 ? 4 : 8;
+  if (g_os_pin[0] > 0) {
+    c.mt = g_os_pin[0];
+    c.ntw = g_os_pin[1];
+    c.steps = g_os_pin[2];
+    c.splitk = max(1, g_os_pin[3]);
+  } else {
+    if (g_os_on == 0) return false;
+    c.mt = M <= 32 ? 2 : 2;
+    const int ntile16 = (N + 15) / 16;
+    // chunks per workgroup slice: 4 waves x STEPS x CS
+    c.steps = nch <= 4 * CS ? 1 : 2;
+    c.splitk = (nch + 4 * c.steps * CS - 1) / (4 * c.steps * CS);
+    const int mgroups = (M + 16 * c.mt - 1) / (16 * c.mt);
+    c.ntw = 1;
+    for (int ntw : {4, 2}) {
+      if ((ntile16 + ntw - 1) / ntw * mgroups * c.splitk >= 256) {
+        c.ntw = ntw;
+        break;
+      }
+    }
+    if (g_os_on == 1) return false;  // planned shapes: filled in from the sweep
+  }
+  if (c.mt != 1 && c.mt != 2 && c.mt != 4) return false;
+  if (c.ntw != 1 && c.ntw != 2 && c.ntw != 4) return false;
+  if (c.steps != 1 && c.steps != 2) return false;
+  if (c.mt == 4 && c.steps == 2) return false;  // 256 KB of LDS
+  const int per = 4 * c.steps * CS;
+  const int cps = (nch + c.splitk - 1) / c.splitk;
+  if (cps > per) return false;
+  if (c.splitk > 1 && (!have_ws || os_ws_need(c, M, N) > ws_bytes || c.splitk > STR_MAX_SPLIT)) return false;
+  return true;
+}
+
+template <int MT, int NTW, int STEPS, int ACT, int NORM, bool W8>
+static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
+                         const float* bias, const void* R, int ldr, int M, int N, int kbytes, const float* colsum,
+                         float eps, hipStream_t st, void* ws, int splitk) {
+  constexpr int MP = MT * 16, BN = 16 * NTW;
+  const int nch = kbytes / 64;
+  const int cps = (nch + splitk - 1) / splitk;
+  splitk = (nch + cps - 1) / cps;
+  const int ntiles = (N + BN - 1) / BN, mgroups = (M + MP - 1) / MP;
+  const int kelems = W8 ? kbytes : kbytes / 2;
+  const dim3 grid(ntiles * mgroups * splitk), block(256);
+  const size_t smem = os_lds_bytes<MT, STEPS>();
+  if (splitk == 1) {
+    hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS>), grid, block, smem, st,
+                       (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N,
+                       nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, true, STEPS>), grid, block, smem, st,
+                     (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, nch,
+                     cps, colsum, eps, kelems, (float*)ws, ntiles, mgroups);
+  const int NO = ACT == ACT_SILU_MUL ? N / 2 : N;
+  const long long threads = (long long)M * ((NO + 3) / 4);
+  hipLaunchKernelGGL((gemm_stream_reduce<ACT, NORM, W8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                     (const float*)ws, splitk, mgroups * MP, ntiles * BN, (const uint8_t*)A, lda_b, sw, colsum, eps,
+                     kelems, C, ldc, bias, (const bf16_t*)R, ldr, M, N);
+  return (int)hipGetLastError();
+}
+
+template <int ACT, int NORM, bool W8>
+static int launch_os(const OsCfg& c, const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
+                     const float* bias, const void* R, int ldr, int M, int N, int kbytes, const float* colsum,
+                     float eps, hipStream_t st, void* ws) {
+#define OSC(MTV, NTV, SV)                                                                                        \
+  if (c.mt == MTV && c.ntw == NTV && c.steps == SV)                                                            \
+    return launch_os_cfg<MTV, NTV, SV, ACT, NORM, W8>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, \
+                                                      eps, st, ws, c.splitk);
+  OSC(1, 1, 1) OSC(1, 2, 1) OSC(1, 4, 1) OSC(1, 1, 2) OSC(1, 2, 2) OSC(1, 4, 2)
+  OSC(2, 1, 1) OSC(2, 2, 1) OSC(2, 4, 1) OSC(2, 1, 2) OSC(2, 2, 2) OSC(2, 4, 2)
+  OSC(4, 1, 1) OSC(4, 2, 1) OSC(4, 4, 1)
+#undef OSC
+  return -3;
+}
+
+template <int ACT, int NORM, bool W8>
+static bool os_eligible(const void* A, int lda_b, const void* Wsh, int M, int kbytes) {
+  if (Wsh == nullptr || M < 17 || M > 64 || kbytes % 64 != 0) return false;
+  return ((uintptr_t)A & 15) == 0 && (lda_b & 15) == 0;
+}
+
+extern "C" int dnn_gemm_set_oneshot(int on, int mt, int ntw, int steps, int splitk) {
+  g_os_on = on;
+  g_os_pin[0] = mt;
+  g_os_pin[1] = ntw;
+  g_os_pin[2] = steps;
+  g_os_pin[3] = splitk;
+  return 0;
+}
+
+// Sweep / A-B entry (bench/oneshot_sweep.py): plain product (no epilogue), an
+// explicit config; returns -1 when the config does not apply to the shape.
+extern "C" int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M,
+                                      int N, int K, int mt, int ntw, int steps, int splitk, int w8, void* ws,
+                                      long long ws_bytes, hipStream_t st) {
+  const int kbytes = w8 ? K : K * 2;
+  if (!os_eligible<ACT_NONE, 0, false>(A, lda * 2, Wsh, M, kbytes) || (w8 && sw == nullptr)) return -1;
+  const int saved[4] = {g_os_pin[0], g_os_pin[1], g_os_pin[2], g_os_pin[3]};
+  g_os_pin[0] = mt;
+  g_os_pin[1] = ntw;
+  g_os_pin[2] = steps;
+  g_os_pin[3] = splitk;
+  OsCfg c;
+  const bool ok = w8 ? os_plan<true>(M, N, kbytes, ws != nullptr, ws_bytes, c)
+                     : os_plan<false>(M, N, kbytes, ws != nullptr, ws_bytes, c);
+  for (int i = 0; i < 4; ++i) g_os_pin[i] = saved[i];
+  if (!ok) return -1;
+  return w8 ? launch_os<ACT_NONE, 0, true>(c, A, lda * 2, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N, kbytes, nullptr,
+                                           0.f, st, ws)
+            : launch_os<ACT_NONE, 0, false>(c, A, lda * 2, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N, kbytes, nullptr,
+                                            0.f, st, ws);
+}
+
 template <int ACT, int NORM, bool W8>
 static bool stream_eligible(const void* A, int lda_b, const void* Wsh, int M, int N, int kbytes) {
   if (!g_stream_on || Wsh == nullptr || M < 17 || M > 64 || kbytes % 64 != 0) return false;
@@ -483,6 +622,9 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
                          hipStream_t st, const float* colsum = nullptr, float eps = 0.f,
                          const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0) {
   if constexpr (!F32 && !FP8 && ACT != ACT_RELU) {
+    OsCfg oc;
+    if (os_eligible<ACT, NORM, W8>(A, lda_b, Wsh, M, kbytes) && os_plan<W8>(M, N, kbytes, ws != nullptr, ws_bytes, oc))
+      return launch_os<ACT, NORM, W8>(oc, A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps, st, ws);
     int splitk = 1, cps = 0;
     if (stream_eligible<ACT, NORM, W8>(A, lda_b, Wsh, M, N, kbytes) &&
         stream_plan<W8>(M <= 32 ? 32 : 64, N, kbytes, ws != nullptr, ws_bytes, splitk, cps)) {

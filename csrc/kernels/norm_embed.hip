@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict
 // still in registers) is scaled by its own amax/448 and written as OCP e4m3
 // with the K padding zeroed, plus the per-row scale — the layout
 // quant_fp8_rows produces — so the activation never round-trips through bf16.
-template <int NC, bool RMS>
+template <int NC, bool RMS, bool SPLIT = false>
 __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ w,
                                                       const float* __restrict__ b, uint8_t* __restrict__ q, int ldq,
                                                       float* __restrict__ sq, int M, int N, int kpad, float eps) {
@@ -200,6 +200,16 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__
   for (int i = 0; i < NC; ++i) {
     const int c = (lane + 64 * i) * 8;
     if (c < kpad) {
+      if constexpr (SPLIT) {  // hi plane + residual plane at +kpad (quant_fp8_rows' split layout)
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = c < N ? v[i][j] * inv : 0.f;
+        int h0, h1, l0, l1;
+        q8_split8(y, h0, h1, l0, l1);
+        *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)h0, (uint32_t)h1);
+        *reinterpret_cast<uint2*>(qr + kpad + c) = make_uint2((uint32_t)l0, (uint32_t)l1);
+        continue;
+      }
       int lo = 0, hi = 0;
       if (c < N) {
         lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
@@ -308,12 +318,19 @@ extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, 
 // Normalise (w, b; LayerNorm or RMSNorm) and quantise rows to e4m3 with per-row
 // scales: q [M][ldq bytes] (columns N..kpad-1 zeroed), sq [M].
 extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq,
-                                int M, int N, int kpad, float eps, int rms, hipStream_t st) {
-  if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad || sq == nullptr) return -1;
+                                int M, int N, int kpad, float eps, int rms, hipStream_t st, int split) {
+  if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad * (split ? 2 : 1) || sq == nullptr) return -1;
   const int nc = (kpad / 8 + 63) / 64;
   dim3 grid((M + 3) / 4), blk(256);
 #define LQ(NCV)                                                                                                   \
   if (nc <= NCV) {                                                                                                \
+    if (split) {                                                                                                  \
+      if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, \
+                                  b, (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                      \
+      else hipLaunchKernelGGL((norm_q8_kernel<NCV, false, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b, \
+                              (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                             \
+      return (int)hipGetLastError();                                                                              \
+    }                                                                                                             \
     if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,       \
                                 (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                           \
     else hipLaunchKernelGGL((norm_q8_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,          \

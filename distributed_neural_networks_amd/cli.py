@@ -205,7 +205,8 @@ def build_stage(ctx: NodeContext, part: int, ranges, device: torch.device, full_
             st = build_device_stage(pipe.model, sd, a, b, first, last, device, dtype=pipe.dtype,
                                     max_batch=n_seq, max_seq=n_pos, max_tokens=ntok,
                                     temperature=pipe.temperature, top_k=pipe.top_k, seed=pipe.seed,
-                                    kv_dtype=pipe.kv_cache_dtype, kv_scale=pipe.kv_cache_scale)
+                                    kv_dtype=pipe.kv_cache_dtype, kv_scale=pipe.kv_cache_scale,
+                                    fp8_prefill=pipe.fp8_prefill)
     else:
         st = TorchStage(pipe.model, sd, a, b, first, last, device,
                         sampling=(pipe.temperature, pipe.top_k, pipe.seed))

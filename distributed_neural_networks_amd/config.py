@@ -13,7 +13,7 @@ Behavioural contract (reference ``node.py:222-290``, ``config.json:1-18``):
   top level ``model``, ``dtype``, ``transport``, ``micro_batch_size``,
   ``num_microbatches``, ``seq_len``, ``decode_steps``, ``prompt_len``, ``temperature``, ``top_k``,
   ``seed``, ``heartbeat_timeout_s``, ``stall_timeout_s``, ``prefill_chunk``, ``replicas``,
-  ``kv_cache_dtype``, ``kv_cache_scale``; per node
+  ``kv_cache_dtype``, ``kv_cache_scale``, ``fp8_prefill``; per node
   ``layers: [start, end]`` (inclusive, as in
   ``partitions/gpt_model_parts.py:12``) and ``device``.
 
@@ -64,6 +64,7 @@ class PipelineConfig:
     dtype: Optional[str] = None
     kv_cache_dtype: str = "bf16"              # "fp8": OCP e4m3 KV cache (half the decode K/V bytes)
     kv_cache_scale: str = "calibrated"        # fp8 cache: per-layer scale from the first prefill's amax, or "unit"
+    fp8_prefill: str = "split"                # dtype fp8: prefill activations "split" (e4m3 hi + residual) or "e4m3"
     transport: str = "grpc"
     micro_batch_size: int = 1
     num_microbatches: int = 1
@@ -202,6 +203,9 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     kvd = cfg.get("kv_cache_dtype", "bf16")
     if kvd not in ("bf16", "fp8"):
         raise ConfigError(f"ERROR: 'kv_cache_dtype' must be 'bf16' or 'fp8', got {kvd!r}")
+    fpp = cfg.get("fp8_prefill", "split")
+    if fpp not in ("split", "e4m3"):
+        raise ConfigError(f"ERROR: 'fp8_prefill' must be 'split' or 'e4m3', got {fpp!r}")
     kvs = cfg.get("kv_cache_scale", "calibrated")
     if kvs not in ("calibrated", "unit"):
         raise ConfigError(f"ERROR: 'kv_cache_scale' must be 'calibrated' or 'unit', got {kvs!r}")
@@ -216,7 +220,7 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     return PipelineConfig(
         nodes=nodes, model_weights=str(weights), num_parts=num_parts,
         return_to_node_id=cfg.get("return_to_node_id"), model=model, dtype=cfg.get("dtype"), kv_cache_dtype=kvd,
-        kv_cache_scale=kvs,
+        kv_cache_scale=kvs, fp8_prefill=fpp,
         transport=transport, micro_batch_size=int(cfg.get("micro_batch_size", 1)),
         num_microbatches=int(cfg.get("num_microbatches", 1)), seq_len=int(cfg.get("seq_len", 64)),
         prompt_len=cfg.get("prompt_len"), decode_steps=int(cfg.get("decode_steps", 0)),

@@ -31,6 +31,7 @@ class Fp8Weight:
     scale: torch.Tensor  # (N,) fp32
     k: int = 0           # logical K
     shuf: Optional[torch.Tensor] = None  # decode copy in skinny fragment order (gemm.shuffle_weight), or None
+    q2: Optional[torch.Tensor] = None    # (N, 2 Kpad) [q | q / 16]: prefill with split activations (attach_split)
 
     @property
     def shape(self):
@@ -51,14 +52,30 @@ def quantize_weight(w: torch.Tensor, device) -> Fp8Weight:
     return Fp8Weight(q.contiguous(), s.to(dtype=torch.float32).contiguous(), K)
 
 
-def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: Optional[int] = None):
-    """Per-row e4m3 quantisation; q_out rows are zero-padded to kpad_of(K)."""
+def attach_split(w: Fp8Weight) -> Fp8Weight:
+    """Prefill weights for split activations: ``q2 = [q | q / 16]`` along K
+    (e4m3; q / 16 is exact down to e4m3's subnormals).  The W8A8 prefill then
+    feeds ``[hi | lo]`` activation planes (``quant_rows(split=True)``,
+    ``layernorm_q8(split=True)``: hi = e4m3(y), lo = e4m3((y - hi) * 16)) and
+    one fp8 GEMM over 2 Kpad sums hi.W + lo.W/16 — the activation keeps ~8
+    mantissa bits instead of e4m3's 4 (GPT-2 XL logits 5.7 % -> ~0.1 % from
+    the fp32 golden).  Twice the prefill weight bytes and MFMA work of plain
+    W8A8, i.e. the bf16 prefill's MFMA time with half its weight bytes."""
+    if w.q2 is None:
+        w.q2 = torch.cat([w.q, (w.q.float() / 16.0).to(torch.float8_e4m3fn)], dim=1).contiguous()
+    return w
+
+
+def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: Optional[int] = None,
+               split: bool = False):
+    """Per-row e4m3 quantisation; q_out rows are zero-padded to kpad_of(K)
+    (``split``: rows of 2 kpad bytes, the residual plane after the hi bytes)."""
     M = rows if rows is not None else x.shape[0]
     K = x.shape[-1]
     kp = kpad_of(K)
-    if q_out.dtype not in (torch.uint8, torch.float8_e4m3fn) or q_out.numel() < M * kp:
+    if q_out.dtype not in (torch.uint8, torch.float8_e4m3fn) or q_out.numel() < M * kp * (2 if split else 1):
         raise ValueError("quant_rows: bad output buffer")
-    check(lib().quant_fp8_rows(ptr(x), x.stride(0), ptr(q_out), ptr(s_out), M, K, kp, stream_ptr()),
+    check(lib().quant_fp8_rows(ptr(x), x.stride(0), ptr(q_out), ptr(s_out), M, K, kp, stream_ptr(), int(split)),
           "quant_fp8_rows")
 
 
@@ -67,19 +84,25 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
                qbuf: Optional[torch.Tensor] = None, sbuf: Optional[torch.Tensor] = None,
                prequantized: bool = False) -> torch.Tensor:
     """W8A8 GEMM.  ``prequantized``: ``qbuf``/``sbuf`` already hold the e4m3
-    rows and scales of x (``transformer_ops.layernorm_q8``); x only gives M, K."""
+    rows and scales of x (``transformer_ops.layernorm_q8``); x only gives M, K.
+    Prefill rows with ``w.q2`` (``attach_split``) run on split activations
+    (2 Kpad bytes per row; a prequantized buffer must be split too)."""
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
     N, kp = w.q.shape
     if kp != kpad_of(K) or (w.k and w.k != K):
         raise ValueError(f"linear_fp8: x K={K} vs weight K={w.k} (padded {kp})")
+    split = w.q2 is not None and M > 64
+    kq = 2 * kp if split else kp
     if prequantized:
         if qbuf is None or sbuf is None:
             raise ValueError("linear_fp8: prequantized needs qbuf and sbuf")
+        if qbuf.numel() * qbuf.element_size() < M * kq:
+            raise ValueError("linear_fp8: prequantized buffer too small for the activation layout")
     else:
-        qbuf = qbuf if qbuf is not None else torch.empty((M, kp), dtype=torch.uint8, device=x.device)
+        qbuf = qbuf if qbuf is not None else torch.empty((M, kq), dtype=torch.uint8, device=x.device)
         sbuf = sbuf if sbuf is not None else torch.empty((M,), dtype=torch.float32, device=x.device)
-        quant_rows(x2, qbuf, sbuf, M)
+        quant_rows(x2, qbuf, sbuf, M, split=split)
     if out is None:
         out = torch.empty((M, N // 2 if act == 3 else N), dtype=torch.bfloat16, device=x.device)
     o2 = out.reshape(-1, out.shape[-1])
@@ -89,8 +112,8 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = Non
                                 ptr(bias), ptr(r2), 0 if r2 is None else r2.stride(0), M, N, kp, act, 0, 1,
                                 stream_ptr()), "gemm_skinny_fp8")
         return out
-    check(lib().gemm_fp8(ptr(qbuf), ptr(sbuf), ptr(w.q), ptr(w.scale), ptr(o2), o2.stride(0), ptr(bias), ptr(r2),
-                         0 if r2 is None else r2.stride(0), M, N, kp, act, stream_ptr()), "gemm_fp8")
+    check(lib().gemm_fp8(ptr(qbuf), ptr(sbuf), ptr(w.q2 if split else w.q), ptr(w.scale), ptr(o2), o2.stride(0),
+                         ptr(bias), ptr(r2), 0 if r2 is None else r2.stride(0), M, N, kq, act, stream_ptr()), "gemm_fp8")
     return out
 
 

@@ -204,7 +204,8 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         if w8 and q8 is not None and s8 is not None:
             # standardise + quantise in one pass: the e4m3 rows feed the W8A8 GEMM directly
             kp = f.w.q.shape[1]
-            layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+            layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0),
+                         split=f.w.q2 is not None)
             return linear_fp8(x, f.w, f.bias, a, residual, out, q8, s8, prequantized=True)
         if w8:
             xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
@@ -268,9 +269,11 @@ def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q:
             return False
         from .transformer_ops import layernorm_q8
         kp = f.w.q.shape[1]
-        layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
-        check(lib().gemm_fp8_qkv_scatter(ptr(q8), ptr(s8), ptr(f.w.q), ptr(f.w.scale), ptr(f.bias), ptr(q), ptr(kc),
-                                         ptr(vc), ptr(pos), B, T, H, Hkv, hd, kc.shape[2], kp, stream_ptr()),
+        split = f.w.q2 is not None  # split activations: [hi | lo] planes against [W | W/16]
+        layernorm_q8(x, ones, None, q8, s8, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0), split=split)
+        check(lib().gemm_fp8_qkv_scatter(ptr(q8), ptr(s8), ptr(f.w.q2 if split else f.w.q), ptr(f.w.scale),
+                                         ptr(f.bias), ptr(q), ptr(kc), ptr(vc), ptr(pos), B, T, H, Hkv, hd,
+                                         kc.shape[2], 2 * kp if split else kp, stream_ptr()),
               "gemm_fp8_qkv_scatter")
         return True
     from .transformer_ops import row_stats

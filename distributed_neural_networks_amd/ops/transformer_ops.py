@@ -55,9 +55,10 @@ def row_stats(x: torch.Tensor, stats: torch.Tensor, eps: float = 1e-5, rms: bool
 
 def layernorm_q8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_out: torch.Tensor,
                  s_out: torch.Tensor, kpad: int, eps: float = 1e-5, rms: bool = False, rows: Optional[int] = None,
-                 ldx: Optional[int] = None) -> torch.Tensor:
+                 ldx: Optional[int] = None, split: bool = False) -> torch.Tensor:
     """Normalise rows and quantise them to e4m3 with per-row scales in one pass
-    (the ``quant_rows`` layout: q_out (M, kpad) bytes, K padding zeroed; s_out (M,))."""
+    (the ``quant_rows`` layout: q_out (M, kpad) bytes, K padding zeroed; s_out (M,);
+    ``split``: (M, 2 kpad), the residual plane after the hi bytes, ``fp8.attach_split``)."""
     _bf16_2d(x, "layernorm_q8")
     N = x.shape[-1]
     M = rows if rows is not None else x.numel() // N
@@ -66,10 +67,11 @@ def layernorm_q8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_
         raise TypeError("layernorm_q8: fp32 weight/bias expected")
     if N % 8 or N > 8192 or kpad < N or kpad % 8:
         raise ValueError(f"layernorm_q8: unsupported width {N} / kpad {kpad}")
-    if q_out.numel() * q_out.element_size() < M * kpad or s_out.numel() < M:
+    ldq = kpad * (2 if split else 1)
+    if q_out.numel() * q_out.element_size() < M * ldq or s_out.numel() < M:
         raise ValueError("layernorm_q8: output too small")
-    check(lib().layernorm_q8(ptr(x), ldx, ptr(w), ptr(b), ptr(q_out), kpad, ptr(s_out), M, N, kpad, eps,
-                             1 if rms else 0, stream_ptr()), "layernorm_q8")
+    check(lib().layernorm_q8(ptr(x), ldx, ptr(w), ptr(b), ptr(q_out), ldq, ptr(s_out), M, N, kpad, eps,
+                             1 if rms else 0, stream_ptr(), int(split)), "layernorm_q8")
     return q_out
 
 

@@ -70,8 +70,15 @@ class TransformerStage(StageCompute):
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
                  device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
                  fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0,
-                 kv_dtype: str = "bf16", kv_scale: str = "calibrated"):
+                 kv_dtype: str = "bf16", kv_scale: str = "calibrated", fp8_prefill: str = "split"):
         info = model_info(model)
+        # fp8 weights, prefill (W8A8) activations: "split" = e4m3 hi + e4m3
+        # residual planes against [W | W/16] (ops/fp8.py attach_split; ~0.1 %
+        # logits error), "e4m3" = one e4m3 byte per activation (2x faster
+        # GEMMs, ~6 % logits error on GPT-2 XL); decode is W8A16 either way
+        if fp8_prefill not in ("split", "e4m3"):
+            raise ValueError(f"fp8_prefill {fp8_prefill!r}: split or e4m3")
+        self.fp8_prefill = fp8_prefill
         # sampling (last stage): temperature 0 = greedy argmax; otherwise
         # Gumbel-max over the top_k logits (0 = all), seeded per (row, position)
         self.temperature, self.top_k, self.seed = float(temperature), int(top_k), int(seed)
@@ -117,6 +124,8 @@ class TransformerStage(StageCompute):
         # the weight bytes in HBM, -9..-19 % per decode projection at M = 32
         if os.environ.get("DNN_SHUF_WEIGHTS", "1") != "0":
             self._attach_decode_copies()
+        if self.fp8 and self.fp8_prefill == "split":
+            self._attach_split_prefill()
         # RoPE tables (Llama)
         self.cos = self.sin = None
         if self.family == "llama3":
@@ -160,6 +169,15 @@ class TransformerStage(StageCompute):
                     attach_shuffled(w)
         if self.last and not isinstance(self.w_head, torch.Tensor):
             attach_shuffled(self.w_head)
+
+    def _attach_split_prefill(self):
+        """[W | W/16] prefill copies of every block projection (split activations)."""
+        from ..ops.fp8 import Fp8Weight, attach_split
+        for L in self.layers:
+            for w in (L.w_qkv, L.w_o, L.w_up, L.w_down):
+                w = getattr(w, "w", w)  # FoldedLinear -> its Fp8Weight
+                if isinstance(w, Fp8Weight):
+                    attach_split(w)
 
     # ------------------------------------------------------------------ fp8 KV scale
     @property
@@ -311,7 +329,7 @@ class TransformerStage(StageCompute):
         self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
-            kmax = max(kpad_of(d), kpad_of(ffn))
+            kmax = max(kpad_of(d), kpad_of(ffn)) * (2 if self.fp8_prefill == "split" else 1)
             self.q8 = torch.empty((ntok * kmax,), dtype=torch.uint8, device=dev)
             self.s8 = torch.empty((ntok,), dtype=torch.float32, device=dev)
         if self.last:
@@ -499,12 +517,12 @@ def _e4m3_amax(t: torch.Tensor) -> float:
 def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
                        max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
                        temperature: float = 0.0, top_k: int = 0, seed: int = 0, kv_dtype: str = "bf16",
-                       kv_scale: str = "calibrated"):
+                       kv_scale: str = "calibrated", fp8_prefill: str = "split"):
     fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
     info = model_info(model)
     max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))
     return TransformerStage(model, sd, start, end, first, last, device, max_batch, max_seq, max_tokens, fp8,
-                            temperature, top_k, seed, kv_dtype=kv_dtype, kv_scale=kv_scale)
+                            temperature, top_k, seed, kv_dtype=kv_dtype, kv_scale=kv_scale, fp8_prefill=fp8_prefill)
 
 
 # ---------------------------------------------------------------------- smoke / golden check
