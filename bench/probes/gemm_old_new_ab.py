@@ -7,7 +7,7 @@ One JSON line per shape.  Build the comparison library from any commit:
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels /tmp/g.hip \
         csrc/kernels/gemm_skinny.hip -o bench/libgemm_old.so
 
-(profiles/r2_gemm_persist_vs_prior_ab.jsonl: the persistent-grid rewrite vs
+(profiles/archive/r2_gemm_persist_vs_prior_ab.jsonl: the persistent-grid rewrite vs
 the kernel before it — 8-21 % slower, reverted.)"""
 import ctypes
 import json

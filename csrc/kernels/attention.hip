@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       // are in, so skip the rescale when it moved for no query of the wave
       // (0.1120 -> 0.1104 ms on GPT-2 B=64 T=512); at hd 128 the branch costs
       // more than it saves (1.174 -> 1.202 ms at T=4096), the rescale stays
-      // unconditional there (profiles/r2_flash_packed_softmax_ab.jsonl)
+      // unconditional there (profiles/archive/r2_flash_packed_softmax_ab.jsonl)
       if (HD != 64 || !__all(alpha == 1.f)) {
         const f32x2 a2 = f32x2{alpha, alpha};
 #pragma unroll
@@ -482,7 +482,7 @@ __device__ __forceinline__ void kv8_unpack(const i32x4& w, uint32_t (&p)[8]) {
 // row reduction per key and head) costs ~20 VALU ops per 4 keys and head; with
 // one wave per SIMD (small grids: Llama-3 batch 1 has 8 workgroups) nothing
 // hides that and the score loop, not memory, set the kernel time (~1.2 us per
-// 128 keys, profiles/r2_attn_decode_phase_probe.jsonl).  With MF a wave
+// 128 keys, profiles/archive/r2_attn_decode_phase_probe.jsonl).  With MF a wave
 // computes S^T for a tile of 16 keys x 16 query-head columns (G used) as
 // HD/32 v_mfma_f32_16x16x32_bf16: lane l feeds key row l&15 (A, straight from
 // the cache) and head l&15 (B = q^T, RoPE'd once); C lands as 4 keys x 1 head
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   // so 10 rows keep the same bytes in flight and one batch covers 640 keys at
   // hd 64 (the 512-567-token benchmark contexts take one K and one V round
   // trip, not two).  bf16 MHA with 10 or 12 rows measured neutral (GPT-2 B=64
-  // 0.585 / 0.584 / 0.590 ms, profiles/r2_decode_rows_in_flight_bf16_ab.jsonl):
+  // 0.585 / 0.584 / 0.590 ms, profiles/archive/r2_decode_rows_in_flight_bf16_ab.jsonl):
   // that path is bound by the K/V bytes, not by its round trips
   constexpr int DEC_U = RU > 0 ? RU : (KV8 ? 10 : dnn::DEC_U);
   static_assert(DEC_U % 2 == 0, "P.V folds key pairs");
@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   // first batch of value rows: requested now, in flight across the barrier and
   // the softmax (they depend only on the key range).  Issuing it before the
   // score loop instead measured slower on the e4m3 path (GPT-2 B=64 0.523 ->
-  // 0.531 ms, B=256 1.053 -> 1.108: 142 VGPRs, profiles/r2_kv8_v_early_ab.jsonl)
+  // 0.531 ms, B=256 1.053 -> 1.108: 142 VGPRs, profiles/archive/r2_kv8_v_early_ab.jsonl)
   bf16x8 vr0[DEC_U];
 #pragma unroll
   for (int u = 0; u < DEC_U; ++u) {
@@ -1202,7 +1202,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
 // (Folding this pass into the attention kernel — the last-arriving split
 // combines, tickets behind an agent-scope release / acquire — measured 20 %
 // slower on Llama-3 8B B=32 decode, 4.49 -> 5.39 ms/step: every split pays the
-// release fence's L2 write-back.  profiles/r2_decode_fold_combine_ab.jsonl;
+// release fence's L2 write-back.  profiles/archive/r2_decode_fold_combine_ab.jsonl;
 // write-through sc1 stores + sc1 loads without the fences read stale partials.)
 __global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H, int Hkv,
                                       int HD, int NS) {

@@ -397,7 +397,7 @@ __device__ __forceinline__ void f1_tile_coords(int logical, int ntm, int ntn, in
 // DMA into a 32 KiB fp32 staging area two k-steps ahead (5 % slower), the
 // split+store between the two MFMA halves (flat), a second register set for A
 // two k-steps ahead once the loads were coalesced (flat, 6 spilled VGPRs).  Probes
-// (profiles/r2_cifar_fc1_probes.jsonl): without the A stream the kernel runs
+// (profiles/archive/r2_cifar_fc1_probes.jsonl): without the A stream the kernel runs
 // 0.51 ms, without any load 0.45 ms (1.8 PF/s), with both 0.80 ms.
 //
 // SPLIT_IN: A arrives pre-split in the blocked boundary encoding (see

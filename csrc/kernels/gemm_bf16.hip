@@ -416,7 +416,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   // the fragment registers the main loop no longer needs) is issued before the
   // first output is computed, so the tile pays one memory round trip for R
   // instead of one per output row group (-20..-25 % GEMM throughput otherwise,
-  // profiles/r2_gemm_epilogue_cost.jsonl).
+  // profiles/archive/r2_gemm_epilogue_cost.jsonl).
   if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N) {
     bf16x4 rr[2][2][4][2];
 #pragma unroll
@@ -665,9 +665,9 @@ static int g_gemm_tile = 0;
 // Rows up to which every bf16 GEMM streams its weights on the skinny kernels
 // (A/B switch).  At M = 64 a wide-N head with warm weights runs faster on the
 // 128^2 MFMA tiles (GPT-2 50304 x 768: 28.3 -> 22.5 us, x 1600: 52.7 -> 33.6,
-// profiles/r2_head_probe.jsonl), but inside the decode step (weights cold behind
+// profiles/archive/r2_head_probe.jsonl), but inside the decode step (weights cold behind
 // 1.27 GB of K/V) GPT-2 B=64 ran 0.588 -> 0.603 ms/step that way and GPT-2 XL
-// B=64 4.507 -> 4.493 (profiles/r2_decode_ab_skinny_max_m.jsonl): 64 stays.
+// B=64 4.507 -> 4.493 (profiles/archive/r2_decode_ab_skinny_max_m.jsonl): 64 stays.
 static int g_skinny_max_m = 64;
 
 extern "C" int dnn_gemm_set_skinny_max_m(int m) {
@@ -709,7 +709,7 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   // slots) and is ~1.3x the 128^2 kernel (2 blocks/CU, 512 slots) per slot
   // when both fill the chip; 1.4 also sends M=32768 N=768 (1.5 waves of 256^2
   // tiles) to the 256^2 kernel, 6 % faster at K=3072 and equal at K=768
-  // (profiles/r1_gemm_bench_v2_widened_epilogue.jsonl).
+  // (profiles/archive/r1_gemm_bench_v2_widened_epilogue.jsonl).
   const int tiles256 = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
   const int tiles128 = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
   auto fill = [](int tiles, int slots) {

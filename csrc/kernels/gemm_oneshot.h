@@ -9,7 +9,7 @@
 // trip (3-7 per wave, ~1-2 us each under load), with the activations loaded
 // fragment-shaped (16 rows x 64 B per instruction: twice the TA work of a
 // full-line load, guide §5 "x operand through LDS in full lines"); the sweep
-// (profiles/r1_skinny_sweep_shuf_fit.jsonl) puts every configuration at
+// (profiles/archive/r1_skinny_sweep_shuf_fit.jsonl) puts every configuration at
 // 0.4-0.9 TB/s on those shapes.  gemm_stream fixes the A path but pipelines
 // K-steps, which only pays for >= 8 MB weights with >= 6 steps per slice.
 //

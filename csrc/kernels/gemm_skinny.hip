@@ -139,7 +139,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   // consecutive along K — every wave load is a contiguous 1 KiB and a batch of U
   // chunks one U KiB stream (row-major W: 16 rows x 64 B, 16 DRAM pages per
   // load).  Llama-3 8B at M = 32: -9..-19 % per projection
-  // (profiles/r1_skinny_sweep_shuf.jsonl).
+  // (profiles/archive/r1_skinny_sweep_shuf.jsonl).
   const uint8_t* wp[NT];
   const int wstep = Wsh != nullptr ? 1024 : 64;  // bytes between consecutive chunks of one lane
 #pragma unroll
@@ -592,7 +592,7 @@ extern "C" int dnn_gemm_set_stream(int on, long long min_bytes, int fold) {
 
 // Per chunk a wave issues NT weight loads and MT activation loads (L2) for
 // NT x MT MFMAs.  The configuration table below is fitted to
-// bench/skinny_sweep.py on MI355X (profiles/r1_skinny_sweep.jsonl, weights
+// bench/skinny_sweep.py on MI355X (profiles/archive/r1_skinny_sweep.jsonl, weights
 // rotated past the 256 MB MALL):
 //   M <= 8     : 1 tile, 4 chunks in flight, 8 waves/WG (within 3% of the best
 //                row-major config on every Llama-3 / GPT-2 XL shape); with the
@@ -657,10 +657,10 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     // (Llama-3 8B fp8 decode graph 12.25 -> 10.33 us), the rest below
     if (!FP8 && Wsh != nullptr && N > 4096 && N < 16384 && kbytes <= 8192) CFG(1, 1, 4, false, 4);
     // fp8 vocabulary head (128K x 4K, fragment order): 2 column tiles per wave
-    // 83.3 -> 75.8 us, 6.9 TB/s (profiles/r2_skinny_sweep_w8_m1.jsonl)
+    // 83.3 -> 75.8 us, 6.9 TB/s (profiles/archive/r2_skinny_sweep_w8_m1.jsonl)
     if (W8 && Wsh != nullptr && N >= 65536) CFG(1, 2, 4, false, 8);
     // fp8 gate|up (28K x 4K) with the fused RMSNorm: 2 column tiles x 2 chunks
-    // on 2 waves 23.3 -> 21.3 us (profiles/r2_w8_decode_projections.jsonl)
+    // on 2 waves 23.3 -> 21.3 us (profiles/archive/r2_w8_decode_projections.jsonl)
     if (W8 && Wsh != nullptr && N >= 16384) CFG(1, 2, 2, false, 2);
     CFG(1, 1, 4, false, 8);
   }
@@ -668,16 +668,16 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     if (wide) CFG(1, 4, 2, false, 2);
     CFG(1, 2, 2, true, 4);
   }
-  // M in (16, 64]: profiles/r1_skinny_sweep.jsonl + r1_skinny_sweep_m32_m64.jsonl
+  // M in (16, 64]: profiles/archive/r1_skinny_sweep.jsonl + r1_skinny_sweep_m32_m64.jsonl
   // (bf16 and W8 on the GPT-2 / GPT-2 XL / Llama-3 shapes), checked in the decode
   // pipeline: wide N streams 4 column tiles on 2 waves, deep K (bf16 >= 8K) 1 tile
   // x 8 chunks on 2 waves, narrow N one column tile on 4 waves (more workgroups)
   // M split (one 16-row tile per workgroup) where the column tiles alone are
-  // too few for 256 CUs: graph-timed sweep profiles/r1_skinny_sweep_ms.jsonl —
+  // too few for 256 CUs: graph-timed sweep profiles/archive/r1_skinny_sweep_ms.jsonl —
   // GPT-2 N=768: 5.8 -> 3.8 us (K=768), 15.9 -> 8.3 us (K=3072) at M=64;
   // GPT-2 XL W8 N=1600: 9.8 -> 7.0 / 28.5 -> 16.0 us; Llama W8 N=4096 at M=32.
   if (!FP8 && Wsh != nullptr) {
-    // fragment-order weights (M 17..64): graph-timed sweep profiles/r1_skinny_sweep_shuf_fit.jsonl,
+    // fragment-order weights (M 17..64): graph-timed sweep profiles/archive/r1_skinny_sweep_shuf_fit.jsonl,
     // every rule within 1.0-1.1x of the best config of its shapes (Llama-3 8B at M = 32,
     // GPT-2 at M = 64, GPT-2 XL W8 at M = 64)
     if (wide) {

@@ -67,6 +67,14 @@ def set_stream_gemm(on: int = 1, min_bytes: int = 0, fold: int = -1) -> None:
     check(lib().gemm_set_stream(int(on), int(min_bytes), int(fold)), "gemm_set_stream")
 
 
+def set_oneshot_gemm(on: int = 1, mt: int = 0, ntw: int = 0, steps: int = 0, splitk: int = 0) -> None:
+    """One-shot decode GEMM (``csrc/kernels/gemm_oneshot.h``, 17..64 rows,
+    fragment-order weights): 0 off, 1 on the shapes its plan covers (default),
+    2 every eligible shape (tests); a non-zero ``mt``/``ntw``/``steps``/``splitk``
+    pins that configuration for every eligible call (A/B probes)."""
+    check(lib().gemm_set_oneshot(int(on), int(mt), int(ntw), int(steps), int(splitk)), "gemm_set_oneshot")
+
+
 def _ws_args(ws: Optional[torch.Tensor]):
     return (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
 
@@ -213,7 +221,7 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         if FOLD_NORM_PREFILL:
             # statistics only (8 B per row, carved from the front of std_buf), the
             # norm applied in the GEMM epilogue on the raw activations: no
-            # normalised copy written and re-read (profiles/r2_prefill_fold_norm_ab.jsonl)
+            # normalised copy written and re-read (profiles/archive/r2_prefill_fold_norm_ab.jsonl)
             from .transformer_ops import row_stats
             st = std_buf.reshape(-1)[:4 * M].view(torch.float32).view(M, 2)
             row_stats(x, st, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))

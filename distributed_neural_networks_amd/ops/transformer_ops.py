@@ -165,7 +165,7 @@ def decode_splits(S: int, B: int, Hkv: int, G: int = 1) -> int:
     if os.environ.get("DNN_DECODE_SPLITS"):  # A/B override
         return max(lds_min, int(os.environ["DNN_DECODE_SPLITS"]))
     if B * Hkv >= 512:  # >= 2 workgroups per CU already: the combine pass costs more than it hides
-        return lds_min    # (GPT-2 B=64: 0.754 -> 0.703 ms/step, profiles/r1_decode_benches_v6.jsonl)
+        return lds_min    # (GPT-2 B=64: 0.754 -> 0.703 ms/step, profiles/archive/r1_decode_benches_v6.jsonl)
     want = max(1, -(-1024 // max(1, B * Hkv)))
     return max(lds_min, min(want, -(-S // 256)))  # >= 256 keys per split: short contexts skip the combine
 

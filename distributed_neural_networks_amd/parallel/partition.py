@@ -106,8 +106,8 @@ def choose_cut(unit_ns: Sequence[float], boundary_bytes: Sequence[int], cuts: Se
 
 # Measured on 1x MI355X: per-image ns of the CIFAR units with the fused kernels
 # (conv stage = units 0-1 together) and the boundary bytes per image, per
-# precision (bf16: profiles/r1_*; fp32: profiles/r2_cifar_fc1_fused_ab.jsonl,
-# profiles/r2_bench_cifar_fp32_n1_kernels.md at B = 65536).
+# precision (bf16: profiles/archive/r1_*; fp32: profiles/archive/r2_cifar_fc1_fused_ab.jsonl,
+# profiles/archive/r2_bench_cifar_fp32_n1_kernels.md at B = 65536).
 CIFAR_UNIT_NS = {"bf16": (0.0, 10.8, 5.3, 0.3), "fp32": (0.0, 27.0, 11.7, 0.5)}
 CIFAR_BOUNDARY_BYTES = {"bf16": (32 * 16 * 16 * 2, 4096 * 2, 512 * 2, 10 * 4),
                         "fp32": (32 * 16 * 16 * 4, 4096 * 4, 512 * 4, 10 * 4)}

@@ -310,7 +310,7 @@ class DecodeRing:
         replay on this many HIP streams (0 = one stream, -1 = min(M, 4));
         scratch rows follow the KV rows (``TransformerStage.step``), so
         concurrent microbatches share no buffer.  Off by default: measured on
-        GPT-2 4-stage (profiles/r2_decode_lanes_gpt2.jsonl) concurrent small
+        GPT-2 4-stage (profiles/archive/r2_decode_lanes_gpt2.jsonl) concurrent small
         microbatches beat the same microbatches on one stream (16 x 4: 2.17 ->
         0.88 ms/round) but not one large batch (64 x 1: 0.60 ms)."""
         self.stages = list(stages)

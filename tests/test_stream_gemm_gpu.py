@@ -181,3 +181,89 @@ def test_stream_fold_matches_reduce_launch(norm):
         assert torch.equal(a, b)
     tickets = ws[-4096:].view(torch.int32)
     assert int(tickets.abs().sum()) == 0  # every ticket re-armed
+
+
+# ---------------------------------------------------------------- one-shot decode GEMM (gemm_oneshot.h)
+@pytest.mark.parametrize("M", [17, 32, 64])
+@pytest.mark.parametrize("N,K,w8", [(2304, 768, False), (768, 3072, False), (4800, 1600, True), (1600, 6400, True),
+                                    (6144, 4096, False), (200, 512, False)])
+@pytest.mark.parametrize("epi", ["none", "bias_res", "ln_gelu", "rms_silu", "rms"])
+def test_oneshot_matches_skinny(M, N, K, w8, epi):
+    """The one-shot kernel (forced on every eligible shape, its planned and
+    split-K configurations) against the existing decode path on the same
+    fragment-order weights, for every epilogue the decode layers use: bias +
+    residual, folded LayerNorm + GELU, folded RMSNorm + packed SwiGLU, folded
+    RMSNorm; bf16 and W8A16 weights; partial M and N tiles."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import (FoldedLinear, decode_workspace, fold_norm, linear,
+                                                          linear_norm, set_oneshot_gemm, shuffle_weight)
+    if epi == "rms_silu" and N % 16:
+        pytest.skip("packed gate|up needs N % 16 == 0")
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N)
+    x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
+    w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(N, device=dev, generator=g) if epi == "bias_res" else None
+    res = torch.randn(M, N, device=dev, generator=g).bfloat16() if epi == "bias_res" else None
+    ws = decode_workspace(dev)
+
+    def run():
+        if epi in ("ln_gelu", "rms_silu", "rms"):
+            gam = torch.rand(K, device=dev, generator=g) + 0.5
+            rms = epi != "ln_gelu"
+            beta = None if rms else torch.randn(K, device=dev, generator=g) * 0.1
+            f = fold_norm(w, gam, beta, None, rms, 1e-5, dev, w8)
+            from distributed_neural_networks_amd.ops.gemm import attach_shuffled
+            attach_shuffled(f)
+            act = {"ln_gelu": "gelu", "rms_silu": "silu_mul", "rms": None}[epi]
+            return linear_norm(x, f, act=act, ws=ws)
+        if w8:
+            q = quantize_weight(w, dev)
+            q.shuf = shuffle_weight(q.q[:, :K])
+            return linear_w8(x, q, bias, 0, res, ws=ws)
+        return linear(x, w.bfloat16(), bias, None, res, w_shuf=shuffle_weight(w.bfloat16()), ws=ws)
+
+    try:
+        set_oneshot_gemm(0)
+        g.manual_seed(M * 7 + N + 1)
+        ref = run().float()
+        set_oneshot_gemm(2)
+        g.manual_seed(M * 7 + N + 1)
+        got = run().float()
+        torch.cuda.synchronize()
+    finally:
+        set_oneshot_gemm(1)
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("cfg", [(1, 1, 1, 1), (1, 4, 2, 3), (2, 2, 1, 2), (2, 4, 2, 1), (4, 1, 1, 1), (4, 4, 1, 4)])
+def test_oneshot_pinned_configs(cfg):
+    """Every (rows/16, column tiles, LDS steps, split-K) configuration the
+    sweep explores computes the same product (W8A16 and bf16)."""
+    from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
+    from distributed_neural_networks_amd.ops.fp8 import quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import decode_workspace, shuffle_weight
+    dev = torch.device("cuda", 0)
+    mt, ntw, steps, sk = cfg
+    ws = decode_workspace(dev)
+    for w8, (N, K) in ((False, (1000, 2048)), (True, (4800, 1600))):
+        M = {1: 17, 2: 33, 4: 50}[mt]  # partial m-groups
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = torch.randn(N, K, device=dev)
+        if w8:
+            q = quantize_weight(w, dev)
+            wsh, sw = shuffle_weight(q.q[:, :K]), q.scale
+            wref = q.q[:, :K].float() * q.scale[:, None]
+        else:
+            wsh, sw = shuffle_weight(w.bfloat16()), None
+            wref = w.bfloat16().float()
+        out = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+        rc = lib().gemm_oneshot_sweep(ptr(x), K, ptr(wsh), ptr(sw), ptr(out), N, M, N, K, mt, ntw, steps, sk, int(w8),
+                                      ptr(ws), ws.numel(), stream_ptr())
+        if rc == -1:
+            continue  # the config does not cover this K in one slice
+        assert rc == 0
+        torch.cuda.synchronize()
+        ref = x.float() @ wref.T
+        assert ((out.float() - ref).norm() / ref.norm()).item() < 1e-2, (cfg, w8)

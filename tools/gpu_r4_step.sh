@@ -5,7 +5,8 @@ mkdir -p gpurun_out
 timeout -k 10 480 python -u bench/oneshot_sweep.py > gpurun_out/s1_oneshot.jsonl 2> gpurun_out/s1_oneshot.err || exit 1
 cut -c1-300 gpurun_out/s1_oneshot.jsonl
 timeout -k 10 900 python -u -m pytest tests/test_native_comm_gpu.py tests/test_kv8_gpu.py tests/test_gloo_gpu.py \
-  tests/test_transformer_gpu.py -k "native or kv8 or gloo or split or full_width" -m gpu -q \
+  tests/test_transformer_gpu.py tests/test_stream_gemm_gpu.py -k "native or kv8 or gloo or split or full_width or oneshot" \
+  -m gpu -q \
   --timeout 300 --timeout-method thread -rfs > gpurun_out/s1_tests.log 2>&1
 rc=$?; tail -6 gpurun_out/s1_tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
