@@ -21,6 +21,7 @@ int dnn_gemm_fp8_qkv_scatter(const void* A8, const float* sa, const void* W8, co
                              void* q, void* kc, void* vc, const int* pos, int B, int T, int H, int Hkv, int hd, int S,
                              int Kb, hipStream_t st);
 int dnn_gemm_set_res_prefetch(int on);
+int dnn_gemm_set_half_cost(float c);
 int dnn_gemm_set_skinny_max_m(int m);
 int dnn_gemm_fp8_set_tile(int tile);
 int dnn_gemm_fp8_256(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,

@@ -285,25 +285,37 @@ __device__ __forceinline__ void epi_pair_scatter(f32x4 a0, f32x4 a1, int m, int 
   }
 }
 
-template <int ACT, bool OUT_F32, bool SCATTER = false>
+// NQ = 2: 256x256 tiles (4 phases per K-tile, below).  NQ = 1: 256x128 tiles
+// for N where the 256^2 grid leaves its last round of 256 CUs half empty
+// (GPT-2's 768-wide projections at M = 32768: 384 tiles = 1.5 rounds; as
+// 256x128 768 tiles = 3 full rounds of half-size tiles).
+// Same waves (2 M x 4 N) and LDS images; a wave owns 2 x 1 quadrants of 64x32
+// and a K-tile is two phases:
+//     ph1: read B0 (4), A0 (8)  | stage A0, B0 [t+1] -> buf^1 | vmcnt(4) | C00
+//     ph2: read A1 (8)          | stage A1 [t+1]     -> buf^1 | vmcnt(2) | C10
+// (one tile ahead: every restage lands 2 phases after the last read of its
+// half-tile, every read 1 phase after the wait + barrier that retired it).
+template <int ACT, bool OUT_F32, bool SCATTER = false, int NQ = 2>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W, int ldw, void* __restrict__ Cv,
     int ldc, const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr, int M, int N, int K,
     int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum, QkvScatter scat = {}) {
+  static_assert(NQ == 1 || NQ == 2, "256x256 or 256x128 tiles");
+  constexpr int TN = 128 * NQ;
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
+  const int ntn = (N + TN - 1) / TN, ntm = (M + BG_M - 1) / BG_M;
   int tm, tn;
   tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
-  const int m0 = tm * BG_M, n0 = tn * BG_N;
+  const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / BG_K;
 
-  f32x4 acc[2][2][4][2];
+  f32x4 acc[2][NQ][4][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NQ; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -320,6 +332,43 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
   };
 
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 64, brow = wc * 32;
+  if constexpr (NQ == 1) {
+    // prologue: tile 0 complete
+    stA(0, 0, 0);
+    stB(0, 0, 0);
+    stA(0, 1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bg_barrier();
+    if (wr == 1) bg_barrier();
+    auto ktile1 = [&](const int t, auto ucst) {
+      constexpr int u = decltype(ucst)::value;
+      // ph1
+      bg_read<2>(b0, half(u, 2), brow, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      bg_read<4>(af, half(u, 0), arow, lane);
+      stA(u ^ 1, 0, t + 1);
+      stB(u ^ 1, 0, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A1 of tile t landed
+      bg_barrier();
+      bg_mfma<4, 2>(acc[0][0], af, b0);
+      bg_barrier();
+      // ph2
+      bg_read<4>(af, half(u, 1), arow, lane);
+      stA(u ^ 1, 1, t + 1);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A0 / B0 of tile t+1 landed
+      bg_barrier();
+      bg_mfma<4, 2>(acc[1][0], af, b0);
+      bg_barrier();
+    };
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      ktile1(t, std::integral_constant<int, 0>{});
+      ktile1(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nk) ktile1(t, std::integral_constant<int, 0>{});
+  } else {
   // prologue: tile 0 complete, A0/B1 of tile 1 in flight
   stA(0, 0, 0);
   stB(0, 1, 0);
@@ -331,8 +380,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   bg_barrier();
   if (wr == 1) bg_barrier();
 
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  const int arow = wr * 64, brow = wc * 32;
   // One K-tile; the loop runs two per iteration so the buffer index u is a
   // compile-time constant and every LDS address an immediate offset.
   auto ktile = [&](const int t, auto ucst) {
@@ -371,6 +418,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     ktile(t + 1, std::integral_constant<int, 1>{});
   }
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
 
@@ -380,13 +428,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   if (rowstat != nullptr) {  // folded pre-norm (prefill QKV / up projections)
     // 8 row statistics and 4 column-sum vectors per lane, loaded once
     float2 rs[2][4];
-    f32x4 cs[2][2];
+    f32x4 cs[NQ][2];
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) rs[mq][i] = rowstat[min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1)];
 #pragma unroll
-    for (int nq = 0; nq < 2; ++nq)
+    for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
@@ -403,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-      for (int nq = 0; nq < 2; ++nq)
+      for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -417,12 +465,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   // first output is computed, so the tile pays one memory round trip for R
   // instead of one per output row group (-20..-25 % GEMM throughput otherwise,
   // profiles/archive/r2_gemm_epilogue_cost.jsonl).
-  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N) {
-    bf16x4 rr[2][2][4][2];
+  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + TN - 1 < N) {
+    bf16x4 rr[2][NQ][4][2];
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-      for (int nq = 0; nq < 2; ++nq)
+      for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           epi_pair_res_load(m0 + mq * 128 + arow + i * 16 + (lane & 15), n0 + nq * 128 + wc * 32, M, R, ldr, lane,
@@ -430,7 +478,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-      for (int nq = 0; nq < 2; ++nq)
+      for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], m0 + mq * 128 + arow + i * 16 + (lane & 15),
@@ -441,7 +489,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-    for (int nq = 0; nq < 2; ++nq)
+    for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
@@ -685,8 +733,17 @@ extern "C" int dnn_gemm_set_res_prefetch(int on) {
 }
 
 extern "C" int dnn_gemm_set_tile(int tile) {
-  if (tile != 0 && tile != 128 && tile != 256) return -1;
+  if (tile != 0 && tile != 128 && tile != 256 && tile != 255) return -1;  // 255: force 256x128
   g_gemm_tile = tile;
+  return 0;
+}
+
+// Relative time of one 256x128 tile against one 256x256 tile (the auto rule
+// picks 256x128 when ceil(tiles/256) x this beats the 256^2 rounds).
+static float g_half_cost = 0.56f;
+extern "C" int dnn_gemm_set_half_cost(float c) {
+  if (!(c > 0.f)) return -1;
+  g_half_cost = c;
   return 0;
 }
 
@@ -716,8 +773,17 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
     const int waves = (tiles + slots - 1) / slots;
     return (double)tiles / ((double)waves * slots);
   };
-  const bool big = g_gemm_tile == 256 ||
+  const bool big = g_gemm_tile == 256 || g_gemm_tile == 255 ||
                    (g_gemm_tile == 0 && M >= 256 && N >= 256 && 1.4 * fill(tiles256, 256) > fill(tiles128, 512));
+  const int tilesH = ((M + BG_M - 1) / BG_M) * ((N + 127) / 128);
+  const bool half = g_gemm_tile == 255 ||
+                    (big && g_gemm_tile == 0 && (float)((tilesH + 255) / 256) * g_half_cost < (float)((tiles256 + 255) / 256));
+  if (half) {
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32, false, 1>), dim3(tilesH), dim3(512), 0, st, (const bf16_t*)A,
+                       lda, (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch,
+                       rowstat, colsum);
+    return;
+  }
   if (big) {
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(tiles256), dim3(512), 0, st, (const bf16_t*)A, lda,
                        (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch, rowstat,

@@ -126,8 +126,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def set_gemm_tile(tile: int = 0) -> None:
-    """Force the large-GEMM tile (128 or 256) or restore the auto choice (0)."""
+    """Force the large-GEMM tile (128, 256, or 255 = 256x128) or restore the auto choice (0)."""
     check(lib().gemm_set_tile(int(tile)), "gemm_set_tile")
+
+
+def set_gemm_half_cost(c: float = 0.56) -> None:
+    """Auto tile rule: the time of a 256x128 tile relative to a 256x256 tile
+    (256x128 is picked when its rounds x ``c`` beat the 256^2 rounds)."""
+    check(lib().gemm_set_half_cost(float(c)), "gemm_set_half_cost")
 
 
 def pack_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
