@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--residual", action="store_true", help="residual epilogue (R = a separate (M,N) bf16 tensor)")
     ap.add_argument("--inplace", action="store_true", help="residual epilogue in place (R = C, the decoder's h += ...)")
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
+    ap.add_argument("--tiles", default="128,256", help="tile arms: 128, 256, 255 (= 256x128), 0 (auto)")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved repetitions of the arms")
     args = ap.parse_args()
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     dev = torch.device("cuda", 0)
@@ -56,10 +58,10 @@ def main():
         flop = 2.0 * M * N * K
         row = {"M": M, "N": N, "K": K}
         ref = None
-        for tile in (128, 256):
+        for tile in [int(t) for t in args.tiles.split(",")] * args.rounds:
             set_gemm_tile(tile)
             ms = timeit(lambda: linear(x, w, bias, act=args.act, residual=res, out=out), args.iters)
-            row[f"tile{tile}_tflops"] = round(flop / ms / 1e9, 1)
+            row[f"tile{tile}_tflops"] = max(row.get(f"tile{tile}_tflops", 0.0), round(flop / ms / 1e9, 1))
             if not args.inplace:
                 if ref is None:
                     ref = out.clone()

@@ -449,6 +449,11 @@ struct OsCfg {
   int mt = 0, ntw = 0, steps = 0, splitk = 1;
 };
 
+template <bool W8>
+constexpr bool os_fits(int ntw, int steps) {
+  return ntw * steps * (W8 ? 4 : 8) <= 32;
+}
+
 static long long os_ws_need(const OsCfg& c, int M, int N) {
   if (c.splitk <= 1) return 0;
   const int MP = 16 * c.mt, mgroups = (M + MP - 1) / MP, BN = 16 * c.ntw;
@@ -476,7 +481,7 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
     const int mgroups = (M + 16 * c.mt - 1) / (16 * c.mt);
     c.ntw = 1;
     for (int ntw : {4, 2}) {
-      if ((ntile16 + ntw - 1) / ntw * mgroups * c.splitk >= 256) {
+      if (os_fits<W8>(ntw, c.steps) && (ntile16 + ntw - 1) / ntw * mgroups * c.splitk >= 256) {
         c.ntw = ntw;
         break;
       }
@@ -487,6 +492,7 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
   if (c.ntw != 1 && c.ntw != 2 && c.ntw != 4) return false;
   if (c.steps != 1 && c.steps != 2) return false;
   if (c.mt == 4 && c.steps == 2) return false;  // 256 KB of LDS
+  if (!os_fits<W8>(c.ntw, c.steps)) return false;  // weight registers would spill
   const int per = 4 * c.steps * CS;
   const int cps = (nch + c.splitk - 1) / c.splitk;
   if (cps > per) return false;
@@ -527,10 +533,15 @@ template <int ACT, int NORM, bool W8>
 static int launch_os(const OsCfg& c, const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
                      const float* bias, const void* R, int ldr, int M, int N, int kbytes, const float* colsum,
                      float eps, hipStream_t st, void* ws) {
+  // configs whose weight registers (NTW x STEPS x CS x 4 VGPRs) pass 128 spill
+  // at the 256-VGPR cap of 2 workgroups per CU: not instantiated
 #define OSC(MTV, NTV, SV)                                                                                        \
-  if (c.mt == MTV && c.ntw == NTV && c.steps == SV)                                                            \
-    return launch_os_cfg<MTV, NTV, SV, ACT, NORM, W8>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, \
-                                                      eps, st, ws, c.splitk);
+  if (c.mt == MTV && c.ntw == NTV && c.steps == SV) {                                                          \
+    if constexpr (os_fits<W8>(NTV, SV))                                                                         \
+      return launch_os_cfg<MTV, NTV, SV, ACT, NORM, W8>(A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes,   \
+                                                        colsum, eps, st, ws, c.splitk);                         \
+    return -3;                                                                                                  \
+  }
   OSC(1, 1, 1) OSC(1, 2, 1) OSC(1, 4, 1) OSC(1, 1, 2) OSC(1, 2, 2) OSC(1, 4, 2)
   OSC(2, 1, 1) OSC(2, 2, 1) OSC(2, 4, 1) OSC(2, 1, 2) OSC(2, 2, 2) OSC(2, 4, 2)
   OSC(4, 1, 1) OSC(4, 2, 1) OSC(4, 4, 1)

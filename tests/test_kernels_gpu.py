@@ -36,8 +36,10 @@ def test_gemm_bf16(M, N, K, act):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 4096), (300, 2304, 768), (1000, 520, 192),
                                    (2048, 768, 3072), (65, 300, 128)])
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
-def test_gemm_bf16_256_tile(M, N, K, act):
-    """The 256x256 4-phase GEMM (forced), including edge tiles and odd K-tile counts."""
+@pytest.mark.parametrize("tile", [256, 255])
+def test_gemm_bf16_256_tile(M, N, K, act, tile):
+    """The 256x256 4-phase GEMM and its 256x128 2-phase variant (tile 255),
+    forced, including edge tiles and odd K-tile counts."""
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     if act == 3 and N % 16:
         pytest.skip("packed gate|up needs N % 16 == 0")
@@ -45,7 +47,7 @@ def test_gemm_bf16_256_tile(M, N, K, act):
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
     b = torch.randn(N, device=DEV)
-    set_gemm_tile(256)
+    set_gemm_tile(tile)
     try:
         if act == 3:
             y = linear(x, w, act="silu_mul")
@@ -68,7 +70,8 @@ def test_gemm_bf16_256_tile(M, N, K, act):
 
 @pytest.mark.parametrize("M,N,K", [(4400, 4208, 192), (4352, 4352, 768), (8192, 768, 768)])
 @pytest.mark.parametrize("epi", ["res", "gelu", "silu_mul", "norm"])
-def test_gemm_bf16_256_many_tiles(M, N, K, epi):
+@pytest.mark.parametrize("tile", [256, 255])
+def test_gemm_bf16_256_many_tiles(M, N, K, epi, tile):
     """More 256^2 tiles than CUs (several waves of workgroups, edge tiles, odd
     K-tile counts) with every prefill epilogue, incl. the folded pre-norm, vs fp32."""
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
@@ -82,7 +85,7 @@ def test_gemm_bf16_256_many_tiles(M, N, K, epi):
         mean, rstd = torch.randn(M, device=DEV), torch.rand(M, device=DEV) + 0.5
         rowstat = torch.stack([rstd, -mean * rstd], 1).contiguous()
         colsum = torch.randn(N, device=DEV)
-    set_gemm_tile(256)
+    set_gemm_tile(tile)
     try:
         if epi == "silu_mul":
             y = linear(x, w, act="silu_mul")
@@ -108,12 +111,13 @@ def test_gemm_bf16_256_many_tiles(M, N, K, epi):
     assert _rel(y, ref) < 1e-2
 
 
-def test_gemm_256_asymmetric_layout():
+@pytest.mark.parametrize("tile", [256, 255])
+def test_gemm_256_asymmetric_layout(tile):
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     n = 512
     x = torch.eye(n, device=DEV).bfloat16()
     w = torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n).remainder(97).bfloat16()
-    set_gemm_tile(256)
+    set_gemm_tile(tile)
     try:
         y = linear(x, w, out_dtype=torch.float32)
         torch.cuda.synchronize()
