@@ -46,6 +46,12 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_FLASH_DB"] = str(v)
     elif switch == "rowstats_r":  # prefill row statistics rows per wave (norm_embed.hip dnn_row_stats)
         os.environ["DNN_ROWSTATS_R"] = str(v)
+    elif switch == "oneshot":  # one-shot decode GEMM: 0 off, 1 planned shapes, 2 every eligible shape
+        gemm.set_oneshot_gemm(v)
+    elif switch == "gemm_tile":  # prefill GEMM tile: 0 auto, 256, 255 (= 256x128), 128
+        gemm.set_gemm_tile(v)
+    elif switch == "half_cost":  # auto 256x128 rule: relative tile cost x 100
+        gemm.set_gemm_half_cost(v / 100.0)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

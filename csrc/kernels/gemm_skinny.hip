@@ -473,7 +473,23 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
     c.splitk = max(1, g_os_pin[3]);
   } else {
     if (g_os_on == 0) return false;
-    c.mt = M <= 32 ? 2 : 2;
+    if (g_os_on == 1) {
+      // measured wins (profiles/r4_oneshot_sweep.jsonl, isolated graph-timed
+      // launches, weights rotated past the MALL): 33..64 rows, the whole K in
+      // one slice — GPT-2 (bf16, K 768): QKV 5.39 -> 4.76, O 3.66 -> 3.10,
+      // c_fc 5.46 -> 4.80 us; GPT-2 XL (W8, K 1600): QKV 9.69 -> 8.35, O
+      // 5.79 -> 5.00, c_fc 9.70 -> 8.71 us.  Split-K shapes (c_proj K 3072 /
+      // 6400, every Llama-3 8B projection at 32 rows) measured slower: they
+      // keep gemm_skinny / gemm_stream.
+      if (M <= 32 || nch > 4 * (W8 ? 2 : 1) * CS) return false;
+      c.splitk = 1;
+      c.steps = W8 ? 2 : 1;
+      const bool narrow = N <= (W8 ? 2048 : 1024);
+      c.mt = narrow ? 1 : 2;
+      c.ntw = narrow ? (W8 ? 2 : 1) : (W8 ? 4 : 2);
+      return os_fits<W8>(c.ntw, c.steps);
+    }
+    c.mt = 2;
     const int ntile16 = (N + 15) / 16;
     // chunks per workgroup slice: 4 waves x STEPS x CS
     c.steps = nch <= 4 * CS ? 1 : 2;
@@ -486,7 +502,6 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
         break;
       }
     }
-    if (g_os_on == 1) return false;  // planned shapes: filled in from the sweep
   }
   if (c.mt != 1 && c.mt != 2 && c.mt != 4) return false;
   if (c.ntw != 1 && c.ntw != 2 && c.ntw != 4) return false;

@@ -135,21 +135,50 @@ class HostStagedLink(P2PLink):
     def __init__(self, peer: int, device: torch.device, group=None):
         super().__init__(peer, device, group)
         self._side = torch.cuda.Stream(device)
+        self._sendq = None  # sender thread's queue (started on the first isend)
 
     @staticmethod
     def _host_like(t: torch.Tensor) -> torch.Tensor:
         return torch.empty(t.numel() * t.element_size(), dtype=torch.uint8, pin_memory=True)
 
+    def _sender(self):
+        """One thread per link posts the gloo sends in order, each once its
+        device->host copy has landed, so ``isend`` never blocks the host on
+        the compute queued before it (as an RCCL send does not)."""
+        import queue
+        import threading
+        self._sendq = queue.Queue()
+
+        def run():
+            while True:
+                item = self._sendq.get()
+                if item is None:
+                    return
+                ev, host, box, done = item
+                try:
+                    ev.synchronize()
+                    box.append(dist.isend(host, self.peer, group=self.group))
+                except BaseException as e:  # noqa: BLE001 — re-raised by the work's wait()
+                    box.append(e)
+                done.set()
+        threading.Thread(target=run, name=f"hostlink-send-{self.peer}", daemon=True).start()
+
     def isend(self, t: torch.Tensor):
         if not t.is_contiguous():
             raise ValueError("HostStagedLink.isend needs a contiguous tensor")
+        import threading
         self._count_send(t)
         host = self._host_like(t)
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             host.view(t.dtype).view(t.shape).copy_(t, non_blocking=True)
-        self._side.synchronize()
-        return _HostWork(dist.isend(host, self.peer, group=self.group), host)
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        if self._sendq is None:
+            self._sender()
+        box, done = [], threading.Event()
+        self._sendq.put((ev, host, box, done))
+        return _HostSendWork(box, done, host)
 
     def irecv(self, out: torch.Tensor):
         if not out.is_contiguous():
@@ -159,6 +188,27 @@ class HostStagedLink(P2PLink):
         posted.record(torch.cuda.current_stream(self.device))
         host = self._host_like(out)
         return _HostWork(dist.irecv(host, self.peer, group=self.group), host, out, posted, self._side)
+
+
+class _HostSendWork:
+    """A ``HostStagedLink`` send posted by the link's sender thread: ``wait``
+    returns once the gloo send has been posted and has completed (the source
+    tensor was already copied out, so no device ordering is needed)."""
+
+    def __init__(self, box, done, host):
+        self.box, self.done_ev, self.host = box, done, host
+        self.done = False
+
+    def wait(self):
+        if self.done:
+            return True
+        self.done_ev.wait()
+        w = self.box[0]
+        if isinstance(w, BaseException):
+            raise w
+        w.wait()
+        self.done = True
+        return True
 
 
 class _HostWork:

@@ -272,7 +272,7 @@ def test_kv8_calibration_recovers_from_saturation():
         res[kv] = st.logits[:B, :V].float().cpu().clone()
         if kv == "fp8":
             assert st.kv_calibrated and st.kv_saturated_layers == [], st.kv_saturated_layers
-            assert all(min(sc) >= 64.0 for sc in st.kv_scales), st.kv_scales
+            assert all(min(sc) >= 8.0 for sc in st.kv_scales), st.kv_scales  # unit would leave them clamped
             amax = max(float(st.kc[:, :B].float().abs().max()), float(st.vc[:, :B].float().abs().max()))
             assert amax < 448.0, amax  # nothing clamped in the real prefill
         del st, ring
