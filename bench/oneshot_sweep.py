@@ -29,6 +29,7 @@ SHAPES = {  # (N, K, M, w8)
     "gpt2": [(2304, 768, 64, 0), (768, 768, 64, 0), (3072, 768, 64, 0), (768, 3072, 64, 0)],
     "gpt2xl": [(4800, 1600, 64, 1), (1600, 1600, 64, 1), (6400, 1600, 64, 1), (1600, 6400, 64, 1)],
     "llama": [(6144, 4096, 32, 0), (4096, 4096, 32, 0), (28672, 4096, 32, 0), (4096, 14336, 32, 0)],
+    "heads": [(50304, 768, 64, 0), (50304, 1600, 64, 1)],  # the tied GPT-2 / GPT-2 XL heads at B = 64
 }
 
 

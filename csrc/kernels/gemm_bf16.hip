@@ -739,8 +739,13 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 }
 
 // Relative time of one 256x128 tile against one 256x256 tile (the auto rule
-// picks 256x128 when ceil(tiles/256) x this beats the 256^2 rounds).
-static float g_half_cost = 0.56f;
+// picks 256x128 when ceil(tiles/256) x this beats the 256^2 rounds).  Off by
+// default (measured, profiles/r4_gemm_tiles*.jsonl): at M = 32768 the 256x128
+// tiles ran N=768 K=768 752 -> 672 TF/s, K=3072 1052 -> 1070, N=2304 885 ->
+// 768, and the GPT-2 4-stage prefill 3.85 -> 3.76 M tok/s — the 2-phase
+// schedule, one K-tile ahead, loses more per tile than the full last round
+// saves; tile 255 keeps it selectable.
+static float g_half_cost = 1e9f;
 extern "C" int dnn_gemm_set_half_cost(float c) {
   if (!(c > 0.f)) return -1;
   g_half_cost = c;

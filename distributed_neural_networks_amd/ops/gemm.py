@@ -130,9 +130,10 @@ def set_gemm_tile(tile: int = 0) -> None:
     check(lib().gemm_set_tile(int(tile)), "gemm_set_tile")
 
 
-def set_gemm_half_cost(c: float = 0.56) -> None:
+def set_gemm_half_cost(c: float = 1e9) -> None:
     """Auto tile rule: the time of a 256x128 tile relative to a 256x256 tile
-    (256x128 is picked when its rounds x ``c`` beat the 256^2 rounds)."""
+    (256x128 is picked when its rounds x ``c`` beat the 256^2 rounds; the
+    default never picks it: measured slower, csrc/kernels/gemm_bf16.hip)."""
     check(lib().gemm_set_half_cost(float(c)), "gemm_set_half_cost")
 
 
