@@ -25,7 +25,9 @@
 //     (LDS-DMA writes lane-linear);
 //   * each wave loads its quarter of the NTW weight tiles straight to VGPRs,
 //     non-temporally (read once), all chunks in flight;
-//   * one vmcnt(0), then MFMAs from LDS fragments x register weights; the 4
+//   * loads are issued step-major (step s's A rows, then its weights); with
+//     two steps a counted vmcnt lets step 0 compute while step 1 lands;
+//   * MFMAs from LDS fragments x register weights; the 4
 //     partial sums meet in LDS (each wave reuses its own image region), and
 //     the epilogue runs in the workgroup (bias / GELU / residual / packed
 //     SwiGLU / fp8 channel scale / folded pre-norm from row statistics
@@ -85,36 +87,6 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   const int nvalid = w1 - w0;  // 0..CPW, wave-uniform
 
   char* img = os_lds + wave * IMG;
-  // ---- issue: A rows by LDS-DMA (full lines), then every weight chunk
-  {
-    const int kb0 = w0 * ACH;                      // first A byte of the wave's range in a row
-    // last valid 16 B of the range (surplus slots clamp here; their weights are zeroed)
-    const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-#pragma unroll
-      for (int p = 0; p < GPS; ++p) {
-        const int r = 2 * p + (lane >> 5);         // row inside the step image
-        const int j = lane & 31;                   // LDS slot of this lane
-        const int g = j ^ (r & 15);                // global slot it holds
-        const int row = min(m0 + r, M - 1);
-        const int kb = min(kb0 + s * OS_SB + g * 16, kb_last);
-        glds16(A + (size_t)row * lda_b + kb, img + s * MP * OS_SB + p * 1024);
-      }
-    }
-  }
-  i32x4 wv[NTW][CPW];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    int ct = tile * NTW + j;
-    ct = ct < ntile16 ? ct : ntile16 - 1;
-    const uint8_t* wp = Wsh + ((size_t)ct * nch) * 1024 + lane * 16;
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) {
-      const int cc = min(min(w0 + c, max(w1, w0 + 1) - 1), nch - 1);
-      wv[j][c] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + (size_t)cc * 1024));
-    }
-  }
   const int fr = lane & 15, fg = lane >> 4;
   float shift[MT], s1s[MT], s2s[MT];
 #pragma unroll
@@ -126,7 +98,35 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       shift[t] = bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)row * lda_b));
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- issue, step-major: the A rows of step s by LDS-DMA (full lines),
+  // then the step's weight chunks; step 0 computes while step 1 lands
+  const int kb0 = w0 * ACH;  // first A byte of the wave's range in a row
+  // last valid 16 B of the range (surplus slots clamp here; their weights are zeroed)
+  const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
+  i32x4 wv[NTW][CPW];
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
+#pragma unroll
+    for (int p = 0; p < GPS; ++p) {
+      const int r = 2 * p + (lane >> 5);  // row inside the step image
+      const int j = lane & 31;            // LDS slot of this lane
+      const int g = j ^ (r & 15);         // global slot it holds
+      const int row = min(m0 + r, M - 1);
+      const int kb = min(kb0 + s * OS_SB + g * 16, kb_last);
+      glds16(A + (size_t)row * lda_b + kb, img + s * MP * OS_SB + p * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      int ct = tile * NTW + j;
+      ct = ct < ntile16 ? ct : ntile16 - 1;
+      const uint8_t* wp = Wsh + ((size_t)ct * nch) * 1024 + lane * 16;
+#pragma unroll
+      for (int c = s * CS; c < (s + 1) * CS; ++c) {
+        const int cc = min(min(w0 + c, max(w1, w0 + 1) - 1), nch - 1);
+        wv[j][c] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + (size_t)cc * 1024));
+      }
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
 
   f32x4 acc[NTW][MT];
@@ -135,9 +135,22 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // every load of step 0 retired, step 1's (GPS LDS-DMA + NTW x CS weight
+  // loads, issued after them) may still be in flight
+  if constexpr (STEPS == 2) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPS + NTW * CS) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
     const int s = c / CS, cc = c % CS;
+    if (STEPS == 2 && c == CS) {  // step 1's A image and weights
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const bool valid = c < nvalid;  // wave-uniform
     if (!valid) {
 #pragma unroll

@@ -481,7 +481,9 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
       // 5.79 -> 5.00, c_fc 9.70 -> 8.71 us.  Split-K shapes (c_proj K 3072 /
       // 6400, every Llama-3 8B projection at 32 rows) measured slower: they
       // keep gemm_skinny / gemm_stream.
-      if (M <= 32 || nch > 4 * (W8 ? 2 : 1) * CS) return false;
+      // the 50304-wide heads measured slower (GPT-2 26.2 -> 36.3 us, XL W8
+      // 38.3 -> 47.2 us, profiles/r4_oneshot_heads.jsonl): wide N stays skinny
+      if (M <= 32 || N >= 16384 || nch > 4 * (W8 ? 2 : 1) * CS) return false;
       c.splitk = 1;
       c.steps = W8 ? 2 : 1;
       const bool narrow = N <= (W8 ? 2048 : 1024);

@@ -26,15 +26,18 @@ def main():
     ap.add_argument("--min_grid", type=int, default=65536, help="only dispatches with at least this many threads")
     ap.add_argument("--top", type=int, default=4)
     a = ap.parse_args()
-    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    # per pass: a counter collected in several passes (GRBM_GUI_ACTIVE usually rides along in
+    # each) is averaged over them, not summed
+    per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     wall = collections.defaultdict(dict)
     for f in sorted(glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             if int(r["Grid_Size"]) < a.min_grid:
                 continue
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            per[k][r["Counter_Name"]][f] += float(r["Counter_Value"])
             wall[k][(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    sums = {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in per.items()}
     kern = sorted(sums, key=lambda k: -sum(wall[k].values()))[: a.top]
     counters = sorted({c for k in kern for c in sums[k]})
     print("| counter | " + " | ".join(f"`{k}`" for k in kern) + " |")
