@@ -300,13 +300,46 @@ def make_link(peer: int, device: torch.device, group=None) -> P2PLink:
 _PREFLIGHT_SEQ = [0]
 
 
+# bulk part of the preflight: PREFLIGHT_MSGS back-to-back messages of this many
+# bytes each way per ring pair, every byte checked (the stage hops move MBs per
+# microbatch; a 16-byte exchange alone would not exercise chunked transfers)
+PREFLIGHT_BYTES = int(os.environ.get("DNN_PREFLIGHT_BYTES", str(4 << 20)))
+PREFLIGHT_MSGS = 3
+
+
+def preflight_pattern(src: int, k: int, numel: int, device) -> torch.Tensor:
+    """Message ``k`` of rank ``src``'s bulk preflight: int32 values unique per
+    (src, k, position), so a dropped, duplicated, reordered or truncated
+    message fails the receiver's comparison."""
+    i = torch.arange(numel, dtype=torch.int64, device=device)
+    return ((i * 2654435761 + src * 40503 + k * 7919) & 0x7FFFFFFF).to(torch.int32)
+
+
+def _preflight_bulk(nxt, prv, r: int, n: int, device, timeout_s: float) -> None:
+    numel = max(1, PREFLIGHT_BYTES // 4)
+    src = (r - 1) % n
+    outs = [preflight_pattern(r, k, numel, device) for k in range(PREFLIGHT_MSGS)]
+    ins = [torch.full((numel,), -1, dtype=torch.int32, device=device) for _ in range(PREFLIGHT_MSGS)]
+    sends = lambda: [nxt.isend(t) for t in outs]  # noqa: E731
+    recvs = lambda: [prv.irecv(t) for t in ins]  # noqa: E731
+    works = sends() + recvs() if r % 2 == 0 else recvs() + sends()
+    for w in works:
+        w.synchronize(timeout_s)
+    for k, t in enumerate(ins):
+        bad = int((t != preflight_pattern(src, k, numel, device)).sum().item())
+        if bad:
+            raise RuntimeError(f"bulk preflight message {k} from rank {src}: {bad} of {numel} words differ")
+
+
 def native_preflight(device: torch.device, timeout_s: float = 90.0, store=None) -> str:
     """Check the native RCCL channels before a multi-GPU run and fall back to
     ProcessGroupNCCL P2P when they do not work, so a run still produces its
     numbers: every rank exchanges 16 bytes with both ring neighbours over its
     own pair channels (even ranks send first, odd ranks receive first, so the
     two ops of a 2-rank ring on one channel match), each op bounded by
-    ``timeout_s``.  The verdict is agreed through the process group's TCP
+    ``timeout_s``; on the forward ring it then sends ``PREFLIGHT_MSGS``
+    back-to-back messages of ``PREFLIGHT_BYTES`` (4 MiB; ``DNN_PREFLIGHT_BYTES``)
+    and the receiver compares every word against the sender's pattern.  The verdict is agreed through the process group's TCP
     store (no collective: it must work when RCCL itself is what failed).  Any
     failure on any rank aborts the native channels and sets
     ``DNN_P2P=torch`` on every rank.  Returns the mode in effect:
@@ -338,6 +371,8 @@ def native_preflight(device: torch.device, timeout_s: float = 90.0, store=None) 
                 got = int(b[0].item())
                 if got != (r - 1) % n:
                     raise RuntimeError(f"{tag} ring payload {got}, expected {(r - 1) % n}")
+                if tag == "world" and PREFLIGHT_BYTES > 0:
+                    _preflight_bulk(nxt, prv, r, n, device, timeout_s)
     except Exception as e:  # noqa: BLE001 — any failure means: fall back
         err = f"rank {r}: {type(e).__name__}: {e}"[:200]
     st = store or rccl._store()

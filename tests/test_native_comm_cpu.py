@@ -125,3 +125,58 @@ def test_channel_scope_aborts_on_error(fake_rccl):
             c = rccl.pair_channel(2, 5, dev, "world", store=st)
             raise RuntimeError("peer died")
     assert c.aborted and c.closed and rccl.live_channels() == 0
+
+
+class _FakeWork:
+    def __init__(self, fn=None):
+        self.fn = fn
+
+    def synchronize(self, timeout_s=None):
+        if self.fn is not None:
+            self.fn()
+            self.fn = None
+
+
+class _FakeRing:
+    """One in-order wire per rank pair: isend enqueues a copy, the matching
+    irecv dequeues it at synchronize (``corrupt`` flips one word of message k)."""
+
+    def __init__(self, corrupt=None, drop=None):
+        self.q, self.corrupt, self.drop, self.n = [], corrupt, drop, 0
+
+    def isend(self, t):
+        k, self.n = self.n, self.n + 1
+        if k != self.drop:
+            c = t.clone()
+            if k == self.corrupt:
+                c[c.numel() // 2] ^= 1
+            self.q.append(c)
+        return _FakeWork()
+
+    def irecv(self, t):
+        return _FakeWork(lambda: t.copy_(self.q.pop(0)))
+
+
+@pytest.mark.parametrize("corrupt,drop", [(None, None), (1, None), (None, 0)])
+def test_preflight_bulk_checks_every_word(monkeypatch, corrupt, drop):
+    """The bulk part of native_preflight: three back-to-back multi-word
+    messages per ring pair; a flipped word or a lost message fails the check
+    (one rank looping to itself, the pattern of its own rank)."""
+    from distributed_neural_networks_amd.parallel import links
+    monkeypatch.setattr(links, "PREFLIGHT_BYTES", 1 << 16)
+    ring = _FakeRing(corrupt, drop)
+    if corrupt is None and drop is None:
+        links._preflight_bulk(ring, ring, 0, 1, torch.device("cpu"), 5.0)
+        assert ring.n == links.PREFLIGHT_MSGS and not ring.q
+        return
+    with pytest.raises((RuntimeError, IndexError)):
+        links._preflight_bulk(ring, ring, 0, 1, torch.device("cpu"), 5.0)
+
+
+def test_preflight_pattern_distinguishes_messages():
+    from distributed_neural_networks_amd.parallel.links import preflight_pattern
+    pats = [preflight_pattern(s, k, 4096, "cpu") for s in range(3) for k in range(3)]
+    for i in range(len(pats)):
+        for j in range(i + 1, len(pats)):
+            assert not torch.equal(pats[i], pats[j])
+    assert int(pats[0].min()) >= 0
