@@ -287,6 +287,33 @@ def bench_pp2(args, info):
     return t1 - t0, n * mb * M / N, p50, f"pp2-rccl-{n}x{n}" + ("-bipartite" if n > 1 else "")
 
 
+def hop_bandwidth(info, nbytes: int, reps: int = 4) -> float:
+    """GB/s of one stage hop, measured on its own: rank 2p sends ``nbytes``
+    ``reps`` times to rank 2p+1 over the same link type as the pp2 hop (native
+    RCCL channel, or ProcessGroupNCCL / gloo), every pair at once; the slowest
+    pair's rate.  Reported next to the pp2 headline: the reference cut moves
+    16 KiB per image, so at N >= 2 the headline is bounded by pairs x this
+    rate / 16 KiB, whatever the stage kernels do."""
+    from distributed_neural_networks_amd.parallel.links import make_link
+    from distributed_neural_networks_amd.parallel import rccl
+    r, N, dev = info.rank, info.world, info.device
+    peer = r ^ 1
+    el = 0.0
+    with rccl.scope(dev):
+        if peer < N:
+            link = make_link(peer, dev)
+            buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            op = link.send if r % 2 == 0 else link.recv
+            op(buf)  # warm: channel / communicator setup outside the timing
+        t0 = sync_time(info)
+        if peer < N:
+            for _ in range(reps):
+                op(buf)
+        el = sync_time(info) - t0
+    el = max_over_ranks(info, el)
+    return nbytes * reps / el / 1e9 if el > 0 else float("nan")
+
+
 def pp2_latency(args, info, s0, s1, back) -> float:
     """p50 of one image through the pipeline as the reference serves a
     request (``node.py:137-200``): rank 0 runs stage 0, the 16 KiB boundary
@@ -606,6 +633,16 @@ def main():
         if info.device.type == "cuda" and args.precision == "fp32":
             out.update(precision_check(info.device, args.precision, 16384))
         out.update(extra)
+    if N > 1 and args.placement == "pp2":
+        try:
+            bw = hop_bandwidth(info, (4 << 20) if info.device.type != "cuda" else (256 << 20))
+            if out is not None:
+                pairs = N // 2
+                out["hop_GBps_per_pair"] = round(bw, 2)
+                out["hop_bound_images_per_s"] = round(pairs * bw * 1e9 / (hop_kib * 1024), 1)
+        except Exception as e:  # noqa: BLE001 — a diagnostic: never costs the headline
+            if out is not None:
+                out["hop_GBps_error"] = f"{type(e).__name__}: {e}"[:200]
     if N > 1 and not args.no_extra:
         multi_gpu_extras(args, info, out)
     if info.rank == 0:

@@ -278,6 +278,9 @@ def test_bench_pp2_schedule_cpu(n, launcher):
     assert d["config"]["global_batch"] == (n // 2) * 16
     assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
     assert d["p50_latency_ms"] is not None and d["p50_latency_ms"] > 0
+    # the hop on its own (what bounds the reference cut at N >= 2)
+    assert "hop_GBps_error" not in d and d["hop_GBps_per_pair"] > 0
+    assert d["hop_bound_images_per_s"] == pytest.approx((n // 2) * d["hop_GBps_per_pair"] * 1e9 / 16384, rel=0.02)
     assert "extras_error" not in d and d["fc1cut_images_per_s"] > 0
     for key, groups in (("gpt2_4stage", min(n, 4)), ("llama3_8b_8stage_b32", min(n, 4)),
                         ("gpt2xl_fp8_8stage_b64", min(n, 4))):
