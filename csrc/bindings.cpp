@@ -65,6 +65,15 @@ PYBIND11_MODULE(_dnn_hip, m) {
   m.def("gemm_set_oneshot", [](int on, int mt, int ntw, int steps, int splitk) {
     return dnn_gemm_set_oneshot(on, mt, ntw, steps, splitk);
   }, py::arg("on"), py::arg("mt") = 0, py::arg("ntw") = 0, py::arg("steps") = 0, py::arg("splitk") = 0);
+  m.def("gemm_set_head", [](int on) { return dnn_gemm_set_head(on); });
+  m.def("gemm_head", [](u64 A, int lda, u64 Wsh, u64 sw, u64 colsum, u64 bias, float eps, int norm, u64 C, int ldc,
+                        int M, int N, int K, int w8, u64 part, int part_cap, u64 st) {
+    return dnn_gemm_head(CP(A), lda, CP(Wsh), CFP(sw), CFP(colsum), CFP(bias), eps, norm, P(C), ldc, M, N, K, w8,
+                         P(part), part_cap, ST(st));
+  });
+  m.def("argmax_final", [](u64 part, int S, int M, u64 out, u64 out2, u64 pos_inc, u64 st) {
+    return dnn_argmax_final(CP(part), S, M, IP(out), IP(out2), IP(pos_inc), ST(st));
+  });
   m.def("gemm_oneshot_sweep", [](u64 A, int lda, u64 Wsh, u64 sw, u64 C, int ldc, int M, int N, int K, int mt, int ntw,
                                  int steps, int splitk, int w8, u64 ws, long long ws_bytes, u64 st) {
     return dnn_gemm_oneshot_sweep(CP(A), lda, CP(Wsh), CFP(sw), P(C), ldc, M, N, K, mt, ntw, steps, splitk, w8, P(ws),

@@ -47,6 +47,12 @@ int dnn_gemm_set_oneshot(int on, int mt, int ntw, int steps, int splitk);
 int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
                            int K, int mt, int ntw, int steps, int splitk, int w8, void* ws, long long ws_bytes,
                            hipStream_t st);
+// decode vocabulary head + argmax partials (gemm_head.h): returns partials per row (> 0) or < 0 (not covered)
+int dnn_gemm_set_head(int on);
+int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, const float* colsum, const float* bias,
+                  float eps, int norm, void* C, int ldc, int M, int N, int K, int w8, void* part, int part_cap,
+                  hipStream_t st);
+int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);

@@ -29,6 +29,7 @@
 // and so the step time halve.  KS is chosen on the host so that N/16 x KS waves
 // cover the CUs.
 #include "gemm_epilogue.h"
+#include "gemm_head.h"
 #include "gemm_oneshot.h"
 #include "gemm_stream.h"
 
@@ -893,3 +894,91 @@ extern "C" int dnn_gemm_skinny_sweep(const void* A, int lda, const void* W, int 
   SWM(4)
 #undef SWM
 }
+
+namespace dnn {
+
+// ---- decode vocabulary head (gemm_head.h): logits + per-workgroup argmax partials
+static int g_head_on = 1;
+
+extern "C" int dnn_gemm_set_head(int on) {
+  g_head_on = on;
+  return 0;
+}
+
+static int head_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
+template <bool W8, int NORM, int NCH, int CPP, int GS>
+static int launch_head_cfg(const void* A, int lda_b, const void* Wsh, const float* sw, const float* colsum,
+                           const float* bias, float eps, void* C, int ldc, int M, int N, int K, int grid, void* part,
+                           hipStream_t st) {
+  constexpr size_t smem = head_lds_bytes<W8, NCH, CPP, GS>();
+  hipLaunchKernelGGL((gemm_head_kernel<W8, NORM, NCH, CPP, GS>), dim3(grid), dim3(512), smem, st, (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, colsum,
+                     bias, eps, (bf16_t*)C, ldc, M, N, K, (int2*)part);
+  return (int)hipGetLastError();
+}
+
+template <int NORM>
+static int launch_head(bool w8, int nch, const void* A, int lda_b, const void* Wsh, const float* sw,
+                       const float* colsum, const float* bias, float eps, void* C, int ldc, int M, int N, int K,
+                       int grid, void* part, hipStream_t st) {
+  // (weight chunks, chunks per K pass, chunks per load group): the LDS image is
+  // 64 rows x CPP chunks of activations (<= 128 KiB); GPT-2 family widths
+#define HEADC(W8V, NCHV, CPPV, GSV)                                                                             \
+  if (w8 == W8V && nch == NCHV)                                                                                 \
+    return launch_head_cfg<W8V, NORM, NCHV, CPPV, GSV>(A, lda_b, Wsh, sw, colsum, bias, eps, C, ldc, M, N, K, grid, \
+                                                      part, st);
+  HEADC(false, 8, 8, 8)     // gpt2-tiny (d 256)
+  HEADC(false, 24, 24, 12)  // gpt2 (d 768)
+  HEADC(false, 32, 32, 8)   // gpt2-medium (d 1024)
+  HEADC(false, 40, 20, 10)  // gpt2-large (d 1280), 2 K passes
+  HEADC(false, 50, 28, 7)   // gpt2-xl bf16 (d 1600), 2 K passes
+  HEADC(true, 4, 4, 4)      // gpt2-tiny fp8
+  HEADC(true, 12, 12, 4)    // gpt2 fp8
+  HEADC(true, 16, 16, 4)    // gpt2-medium fp8
+  HEADC(true, 20, 10, 5)    // gpt2-large fp8, 2 K passes
+  HEADC(true, 25, 14, 5)    // gpt2-xl fp8 (d 1600), 2 K passes
+#undef HEADC
+  return -3;
+}
+
+// Returns the number of partials per row (the grid, > 0), or < 0 when the
+// shape is not covered (the caller runs the GEMM + argmax_rows instead).
+// part: >= M x part_cap int2; C: bf16 [M, ldc], ldc % 4 == 0.
+extern "C" int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, const float* colsum,
+                             const float* bias, float eps, int norm, void* C, int ldc, int M, int N, int K, int w8,
+                             void* part, int part_cap, hipStream_t st) {
+  if (!g_head_on || M < 1 || M > 64 || N < 16 || Wsh == nullptr || part == nullptr || C == nullptr) return -1;
+  if ((w8 && sw == nullptr) || (norm == NORM_LN && colsum == nullptr) || norm < 0 || norm > 2) return -1;
+  if (((uintptr_t)A & 15) != 0 || ((lda * 2) & 15) != 0 || ((uintptr_t)C & 7) != 0 || (ldc & 3) != 0 || ldc < N)
+    return -1;
+  if (K <= 0 || K % (w8 ? 64 : 32) != 0) return -1;
+  const int nch = w8 ? K / 64 : K / 32;
+  const int ntile16 = (N + 15) / 16;
+  const int cus = head_cus();
+  if (cus <= 0) return -1;
+  int grid = (ntile16 + 7) / 8;
+  grid = grid < cus ? grid : cus;
+  if ((long long)grid * 16 < ntile16 || grid > part_cap) return -1;  // at most two column tiles per wave
+  int rc;
+  if (norm == NORM_LN)
+    rc = launch_head<NORM_LN>(w8 != 0, nch, A, lda * 2, Wsh, sw, colsum, bias, eps, C, ldc, M, N, K, grid, part, st);
+  else if (norm == NORM_RMS)
+    rc = launch_head<NORM_RMS>(w8 != 0, nch, A, lda * 2, Wsh, sw, colsum, bias, eps, C, ldc, M, N, K, grid, part, st);
+  else
+    rc = launch_head<NORM_NONE>(w8 != 0, nch, A, lda * 2, Wsh, sw, colsum, bias, eps, C, ldc, M, N, K, grid, part,
+                                st);
+  if (rc == -3) return -1;
+  return rc != 0 ? -2 : grid;
+}
+
+}  // namespace dnn

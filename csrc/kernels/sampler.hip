@@ -285,6 +285,17 @@ extern "C" int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, fl
   return -2;  // vocabulary > 128K entries
 }
 
+// The second pass of a row-split argmax whose partials another kernel wrote
+// (part[row * S + s]; gemm_head.h writes one per workgroup), with the decode
+// step tail.
+extern "C" int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (S <= 0 || part == nullptr) return -1;
+  hipLaunchKernelGGL(argmax_final_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const int2*)part, S, M, out, out2,
+                     pos_inc);
+  return (int)hipGetLastError();
+}
+
 // part (optional, >= M * 64 int2): workspace of the row-split path (bf16 rows,
 // fewer than 512 rows x segments otherwise); nullptr = one workgroup per row.
 extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st,

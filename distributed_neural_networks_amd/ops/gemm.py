@@ -302,6 +302,54 @@ def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q:
     return True
 
 
+FUSED_HEAD = True  # decode head + argmax partials in one launch (A/B switch: set_fused_head)
+HEAD_PART_PER_ROW = 256  # int2 partials per row the fused head may write (one per workgroup, <= CUs)
+
+
+def set_fused_head(on: bool = True) -> None:
+    """A/B switch of the fused decode head (``head_argmax``)."""
+    global FUSED_HEAD
+    FUSED_HEAD = bool(on)
+    check(lib().gemm_set_head(1 if on else 0), "gemm_set_head")
+
+
+def head_argmax(x: torch.Tensor, f: FoldedLinear, logits: torch.Tensor, part: torch.Tensor, out: torch.Tensor,
+                also: Optional[torch.Tensor] = None, advance: Optional[torch.Tensor] = None) -> bool:
+    """Greedy decode head (gemm_head.h): ``logits = linear(norm(x), W)`` for a
+    folded-norm head with a fragment-order copy (bf16 or W8A16), and the
+    argmax of every row in the same pass — each workgroup writes its winner
+    per row to ``part``, a merge launch (``argmax_final``) writes ``out`` and
+    the decode step tail (``also`` = copy of the ids, ``advance += 1``).
+    Returns False with nothing launched where it does not apply (more than 64
+    rows, a width without an instantiated config, a vocabulary over two
+    column tiles per wave): the caller then runs the GEMM and argmax_rows."""
+    from .fp8 import Fp8Weight
+    if not FUSED_HEAD or not isinstance(f, FoldedLinear):
+        return False
+    M, K = x.shape
+    w8 = isinstance(f.w, Fp8Weight)
+    wsh = f.w.shuf if w8 else f.ws
+    if wsh is None or M > 64 or x.dtype != torch.bfloat16 or x.stride(1) != 1:
+        return False
+    N = f.w.shape[0]
+    if logits.dtype != torch.bfloat16 or logits.stride(1) != 1 or logits.shape[0] < M or logits.shape[1] < N:
+        raise ValueError("head_argmax: bad logits buffer")
+    if part.dtype != torch.int32 or not part.is_contiguous() or part.numel() < 2 * HEAD_PART_PER_ROW * M:
+        raise ValueError(f"head_argmax: part must be contiguous int32 with >= {2 * HEAD_PART_PER_ROW * M} entries")
+    for t, nm in ((out, "out"), (also, "also"), (advance, "advance")):
+        if t is not None and (t.dtype != torch.int32 or t.numel() < M or not t.is_contiguous()):
+            raise ValueError(f"head_argmax: {nm} must be contiguous int32 with >= {M} entries")
+    S = lib().gemm_head(ptr(x), x.stride(0), ptr(wsh), ptr(f.w.scale) if w8 else 0, ptr(f.colsum), ptr(f.bias),
+                        f.eps, f.norm, ptr(logits), logits.stride(0), M, N, K, 1 if w8 else 0, ptr(part),
+                        HEAD_PART_PER_ROW, stream_ptr())
+    if S == -1:
+        return False
+    if S <= 0:
+        raise RuntimeError(f"gemm_head failed ({S})")
+    check(lib().argmax_final(ptr(part), S, M, ptr(out), ptr(also), ptr(advance), stream_ptr()), "argmax_final")
+    return True
+
+
 def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
     """Pre-shuffle a decode weight [N, K] (bf16, or e4m3 bytes) into the skinny
     GEMM's MFMA fragment order: for column tile t (16 rows) and 64-B chunk c,

@@ -35,7 +35,8 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import transformer_ops as T_
-from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, decode_workspace, fold_norm, linear, linear_norm,
+from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, HEAD_PART_PER_ROW, decode_workspace, fold_norm, head_argmax,
+                        linear, linear_norm,
                         pack_gate_up, qkv_scatter_norm, skinny_rows)
 from .stages import StageCompute, StageOutput
 
@@ -326,6 +327,9 @@ class TransformerStage(StageCompute):
         # row-split argmax partials (last stage; rows offset by the microbatch like the logits)
         self.amx_part = torch.empty((self.max_batch * 2 * T_.ARGMAX_PART_PER_ROW,),
                                     dtype=torch.int32, device=dev)
+        # fused decode head's per-workgroup argmax partials (ops/gemm.py head_argmax)
+        self.head_part = (torch.empty((self.max_batch * 2 * HEAD_PART_PER_ROW,), dtype=torch.int32, device=dev)
+                          if self.last else None)
         self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
@@ -449,6 +453,15 @@ class TransformerStage(StageCompute):
         else:
             rows, src, ldx = ntok, h, d
         logits = self.logits[r0:r0 + rows]
+        if self.fuse_norm and last_only and not self.temperature > 0:
+            # greedy: the head writes the logits and each workgroup's argmax
+            # partials; one merge launch takes the ids and the step tail
+            x_last = torch.as_strided(src, (rows, d), (ldx, 1))
+            dst = out if out is not None else self.next_ids[r0:r0 + rows]
+            also, adv = advance if advance is not None else (None, None)
+            if head_argmax(x_last, self.w_head, logits[:, :self.V], self.head_part[r0 * 2 * HEAD_PART_PER_ROW:], dst,
+                           also, adv):
+                return StageOutput(logits[:, :self.V], dst)
         if self.fuse_norm:
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
             linear_norm(x_last, self.w_head, out=logits[:, :self.V], std_buf=self.buf_lnf[r0:], ones=self.ones,
