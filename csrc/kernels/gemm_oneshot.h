@@ -25,8 +25,13 @@
 //     (LDS-DMA writes lane-linear);
 //   * each wave loads its quarter of the NTW weight tiles straight to VGPRs,
 //     non-temporally (read once), all chunks in flight;
-//   * loads are issued step-major (step s's A rows, then its weights); with
-//     two steps a counted vmcnt lets step 0 compute while step 1 lands;
+//   * the A rows are issued first, then the weights step-major: the folded
+//     norm's row statistics are taken from the image while the weights are
+//     still in flight (measured neutral against taking them from the MFMA
+//     fragments: the statistics' VALU, ~200 elements per lane at 32 rows and
+//     K = 1600, outlasts the weight flight either way,
+//     profiles/r4_oneshot_norm_ab*.jsonl), and with two steps a counted vmcnt
+//     lets step 0 compute while step 1 lands;
 //   * MFMAs from LDS fragments x register weights; the 4
 //     partial sums meet in LDS (each wave reuses its own image region), and
 //     the epilogue runs in the workgroup (bias / GELU / residual / packed
@@ -98,8 +103,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       shift[t] = bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)row * lda_b));
     }
   }
-  // ---- issue, step-major: the A rows of step s by LDS-DMA (full lines),
-  // then the step's weight chunks; step 0 computes while step 1 lands
+  // ---- issue: every A row segment of the wave's range by LDS-DMA (full
+  // lines), then every weight chunk, step-major.  The activations come from
+  // L2 and land first: the row statistics are taken from the image while the
+  // weights are still in flight, and step 0 computes while step 1 lands
   const int kb0 = w0 * ACH;  // first A byte of the wave's range in a row
   // last valid 16 B of the range (surplus slots clamp here; their weights are zeroed)
   const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
@@ -115,6 +122,9 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       const int kb = min(kb0 + s * OS_SB + g * 16, kb_last);
       glds16(A + (size_t)row * lda_b + kb, img + s * MP * OS_SB + p * 1024);
     }
+  }
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       int ct = tile * NTW + j;
@@ -129,16 +139,40 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   }
   __builtin_amdgcn_sched_barrier(0);
 
+  // ---- row statistics of this wave's K range from its image (the 4 lane
+  // groups hold disjoint k), while the weight loads are outstanding
+  if constexpr (NORM != 0) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");  // the image (issued first)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int s = c / CS, cc = c % CS;
+      if (c < nvalid) {  // wave-uniform
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int h = 0; h < AU; ++h) {
+            const int row = 16 * t + fr;
+            const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
+            const bf16x8 a8 =
+                *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
+            str_stats<NORM>(a8, shift[t], s1s[t], s2s[t]);
+          }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
   f32x4 acc[NTW][MT];
 #pragma unroll
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // every load of step 0 retired, step 1's (GPS LDS-DMA + NTW x CS weight
-  // loads, issued after them) may still be in flight
+  // the image and step 0's weights retired; step 1's weights (NTW x CS loads,
+  // issued last) may still be in flight
   if constexpr (STEPS == 2) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPS + NTW * CS) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NTW * CS) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -147,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
     const int s = c / CS, cc = c % CS;
-    if (STEPS == 2 && c == CS) {  // step 1's A image and weights
+    if (STEPS == 2 && c == CS) {  // step 1's weights
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -165,14 +199,6 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
         const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
         af[t][h] = *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
       }
-    if constexpr (NORM != 0) {
-      if (valid) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-          for (int h = 0; h < AU; ++h) str_stats<NORM>(af[t][h], shift[t], s1s[t], s2s[t]);
-      }
-    }
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       if constexpr (W8) {
