@@ -1204,6 +1204,43 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
 // slower on Llama-3 8B B=32 decode, 4.49 -> 5.39 ms/step: every split pays the
 // release fence's L2 write-back.  profiles/archive/r2_decode_fold_combine_ab.jsonl;
 // write-through sc1 stores + sc1 loads without the fences read stale partials.)
+// Up to NSMAX splits: every partial of the thread's head dim is requested
+// before the first use (one memory round trip instead of the loop below's
+// three dependent ones); the same arithmetic in the same order, so the output
+// is bit-identical.
+template <int NSMAX>
+__global__ void decode_combine_fast_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H,
+                                           int Hkv, int HD, int NS) {
+  const int bh = blockIdx.x;  // b*H + h
+  const int b = bh / H, hh = bh % H;
+  const int G = H / Hkv, kvh = hh / G, g = hh % G;
+  const float* base = ws + ((size_t)(b * Hkv + kvh) * NS) * G * (HD + 2) + g * (HD + 2);
+  const size_t step = (size_t)G * (HD + 2);
+  float ms[NSMAX], ls[NSMAX], os[NSMAX];
+#pragma unroll
+  for (int s = 0; s < NSMAX; ++s) {
+    const bool ok = s < NS;
+    const float* p = base + (ok ? s : 0) * step;
+    ms[s] = ok ? p[HD] : -INFINITY;
+    ls[s] = ok ? p[HD + 1] : 0.f;
+    os[s] = (ok && (int)threadIdx.x < HD) ? p[threadIdx.x] : 0.f;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < NSMAX; ++s) m = fmaxf(m, ms[s]);
+  float l = 0.f, acc = 0.f;
+#pragma unroll
+  for (int s = 0; s < NSMAX; ++s) {
+    if (ms[s] != -INFINITY) {
+      const float e = exp2f(ms[s] - m);
+      l += ls[s] * e;
+      acc += os[s] * e;
+    }
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if ((int)threadIdx.x < HD) o[(size_t)b * H * HD + hh * HD + threadIdx.x] = f2bf(acc * inv);
+}
+
 __global__ void decode_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ o, int B, int H, int Hkv,
                                       int HD, int NS) {
   const int bh = blockIdx.x;  // b*H + h
@@ -1307,6 +1344,21 @@ extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc
   return (int)hipGetLastError();
 }
 
+// the split merge: the one-round-trip kernel for up to 8 splits (head dim <= 256)
+static void launch_decode_combine(const float* ws, bf16_t* o, int B, int H, int Hkv, int hd, int ns, hipStream_t st) {
+  if (ns <= 8 && hd <= 256) {
+    const int th = hd <= 64 ? 64 : (hd <= 128 ? 128 : 256);
+    if (ns <= 2)
+      hipLaunchKernelGGL(decode_combine_fast_kernel<2>, dim3(B * H), dim3(th), 0, st, ws, o, B, H, Hkv, hd, ns);
+    else if (ns <= 4)
+      hipLaunchKernelGGL(decode_combine_fast_kernel<4>, dim3(B * H), dim3(th), 0, st, ws, o, B, H, Hkv, hd, ns);
+    else
+      hipLaunchKernelGGL(decode_combine_fast_kernel<8>, dim3(B * H), dim3(th), 0, st, ws, o, B, H, Hkv, hd, ns);
+    return;
+  }
+  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, o, B, H, Hkv, hd, ns);
+}
+
 struct Dec1pArgs {
   const bf16_t* q;
   int ldq;
@@ -1359,14 +1411,18 @@ static int attn_decode_1p_launch(const void* q, int ldq, void* kc, void* vc, voi
                                  int S, const int* lens, const float* cosT, const float* sinT, float sl2, int splits,
                                  float* ws, int fm, bool nt, bool force, hipStream_t st) {
   const int G = H / Hkv;
-  const int ns = (S + DEC1P_CAP - 1) / DEC1P_CAP;
+  int ns = (S + DEC1P_CAP - 1) / DEC1P_CAP;
+  // DNN_DECODE_1P_NS=n: at least n key splits (A/B; needs the caller's workspace)
+  const char* ns_e = getenv("DNN_DECODE_1P_NS");
+  const int ns_min = ns_e != nullptr ? atoi(ns_e) : 0;
+  if (ns_min > ns) ns = ns_min;
   if (ns > 1 && ns > splits) return 1;
   if (!force && (long)B * Hkv * ns < 128) return 1;
   // GQA past one workgroup per CU: the 86 KiB of LDS per workgroup keeps one
   // resident per CU, so a second round of workgroups runs serially and the
   // batched kernel wins (Llama-3 B=64: 36.5 vs 30.9 us,
   // profiles/r3_attn_1p_shapes.jsonl); MHA's 4-wave workgroups are small
-  if (!force && G > 1 && (long)B * Hkv * ns > 256) return 1;
+  if (!force && ns_min <= 1 && G > 1 && (long)B * Hkv * ns > 256) return 1;
   dim3 grid(B * Hkv, ns);
   // row-layout scores for MHA, MFMA key tiles for GQA: at MHA hd 64 an MFMA tile
   // uses 1 of 16 head columns and its half-row key loads ran 10 % slower than
@@ -1395,7 +1451,7 @@ static int attn_decode_1p_launch(const void* q, int ldq, void* kc, void* vc, voi
   else
     return 1;
   if (ns > 1)
-    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, ns);
+    launch_decode_combine(ws, (bf16_t*)o, B, H, Hkv, hd, ns, st);
   return (int)hipGetLastError();
 }
 
@@ -1461,7 +1517,7 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
     DEC8(128, true, 0) DEC8(128, false, 0) { return -2; }
 #undef DEC8
     if (splits > 1)
-      hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
+      launch_decode_combine(ws, (bf16_t*)o, B, H, Hkv, hd, splits, st);
     return (int)hipGetLastError();
   }
 #define DEC_FM(HDV, GV, NTV, MFV)                                                                                     \
@@ -1493,7 +1549,7 @@ static int attn_decode_launch(const void* q, int ldq, void* kc, void* vc, void* 
 #undef DEC_NT
 #undef DEC_FM
   if (splits > 1)
-    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, ws, (bf16_t*)o, B, H, Hkv, hd, splits);
+    launch_decode_combine(ws, (bf16_t*)o, B, H, Hkv, hd, splits, st);
   return (int)hipGetLastError();
 }
 

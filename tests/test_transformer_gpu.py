@@ -234,12 +234,15 @@ def test_attn_decode(B, H, Hkv, hd, S, lens, mfma, monkeypatch):
         assert _rel(out[b], ref) < 2e-2, b
 
 
-@pytest.mark.parametrize("B,H,Hkv,hd,S,rope", [(32, 32, 8, 128, 600, True), (64, 12, 12, 64, 560, False),
-                                               (64, 25, 25, 64, 1300, False)])
-def test_attn_decode_one_pass_bench_shapes(B, H, Hkv, hd, S, rope, monkeypatch):
+@pytest.mark.parametrize("B,H,Hkv,hd,S,rope,ns", [(32, 32, 8, 128, 600, True, 0), (64, 12, 12, 64, 560, False, 0),
+                                                  (64, 25, 25, 64, 1300, False, 0), (32, 32, 8, 128, 600, True, 2),
+                                                  (32, 32, 8, 128, 600, True, 3), (64, 12, 12, 64, 560, False, 3)])
+def test_attn_decode_one_pass_bench_shapes(B, H, Hkv, hd, S, rope, ns, monkeypatch):
     """The benchmark decode shapes (Llama-3 8B B=32, GPT-2 B=64, GPT-2 XL with a
     cache past one 640-key split) take the one-pass kernel by default: fused
-    step vs the batched kernel and vs the fp32 softmax on ragged positions."""
+    step vs the batched kernel and vs the fp32 softmax on ragged positions.
+    ``ns``: the one-pass kernel forced to that many key splits
+    (DNN_DECODE_1P_NS), merged by the one-round-trip combine."""
     from distributed_neural_networks_amd.models.llama3 import LLAMA_CONFIGS, rope_tables
     from distributed_neural_networks_amd.ops import transformer_ops as T
     torch.manual_seed(11)
@@ -260,7 +263,12 @@ def test_attn_decode_one_pass_bench_shapes(B, H, Hkv, hd, S, rope, monkeypatch):
     ws = torch.empty(B * Hkv * splits * G * (hd + 2), device=DEV)
     out = torch.empty(B, H * hd, device=DEV, dtype=torch.bfloat16)
     monkeypatch.delenv("DNN_DECODE_1P", raising=False)
+    if ns:
+        splits = max(splits, ns)
+        ws = torch.empty(B * Hkv * splits * G * (hd + 2), device=DEV)
+        monkeypatch.setenv("DNN_DECODE_1P_NS", str(ns))
     T.attn_decode_qkv(qkv, kc, vc, out, B, H, Hkv, hd, p, ws, splits, cos, sin)
+    monkeypatch.delenv("DNN_DECODE_1P_NS", raising=False)
     monkeypatch.setenv("DNN_DECODE_1P", "0")
     out2 = torch.empty_like(out)
     T.attn_decode_qkv(qkv, kc2, vc2, out2, B, H, Hkv, hd, p, ws, splits, cos, sin)
