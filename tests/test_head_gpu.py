@@ -36,6 +36,10 @@ def _setup(M, K, N, w8, rms=False, seed=0):
     (8, 256, 512, True, False),
     (64, 1280, 5000, False, False),   # two K passes, bf16
     (48, 1280, 4000, True, False),
+    (16, 1024, 3000, False, False),   # every instantiated width: gpt2-medium / gpt2-xl bf16 / gpt2 fp8 / medium fp8
+    (40, 1600, 3000, False, False),
+    (24, 768, 3000, True, False),
+    (64, 1024, 3000, True, True),
 ])
 def test_head_matches_golden_and_unfused(M, K, N, w8, rms):
     from distributed_neural_networks_amd.ops import transformer_ops as T_
