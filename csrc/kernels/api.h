@@ -53,6 +53,7 @@ int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, cons
                   float eps, int norm, void* C, int ldc, int M, int N, int K, int w8, void* part, int part_cap,
                   hipStream_t st);
 int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st);
+int dnn_gemm_set_split_tail(int on);  // prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);

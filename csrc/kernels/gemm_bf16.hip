@@ -745,6 +745,16 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 // 768, and the GPT-2 4-stage prefill 3.85 -> 3.76 M tok/s — the 2-phase
 // schedule, one K-tile ahead, loses more per tile than the full last round
 // saves; tile 255 keeps it selectable.
+// the 256^2 + 256x128 tail split in launch_gemm (A/B switch; DNN_SPLIT_TAIL=0 starts with it off)
+static int g_split_tail = [] {
+  const char* e = getenv("DNN_SPLIT_TAIL");
+  return e != nullptr ? atoi(e) : 1;
+}();
+extern "C" int dnn_gemm_set_split_tail(int on) {
+  g_split_tail = on;
+  return 0;
+}
+
 static float g_half_cost = 1e9f;
 extern "C" int dnn_gemm_set_half_cost(float c) {
   if (!(c > 0.f)) return -1;
@@ -787,6 +797,27 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32, false, 1>), dim3(tilesH), dim3(512), 0, st, (const bf16_t*)A,
                        lda, (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, K, g_res_prefetch,
                        rowstat, colsum);
+    return;
+  }
+  // Tail split (round 4): when the 256^2 grid is full rounds plus a last
+  // column of tiles that fills at most one more round as 256x128 tiles (GPT-2's
+  // 768-wide O / c_proj at M = 32768: 256 tiles + a 128-tile column), the
+  // first N - 256 columns run as 256^2 tiles and the last 256 as 256x128 tiles
+  // in a second launch — 1 + 1/2 rounds instead of 2 full ones, no workspace
+  // and no reduction (the two launches write disjoint columns).
+  const int ntm256 = (M + BG_M - 1) / BG_M;
+  if (big && g_split_tail && g_gemm_tile == 0 && ACT != ACT_SILU_MUL && N % 256 == 0 && N >= 512 &&
+      (ntm256 * (N / 256 - 1)) % 256 == 0 && 2 * ntm256 <= 256) {
+    const int Na = N - 256;
+    const size_t cb = F32 ? sizeof(float) : sizeof(bf16_t);
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, Na, K,
+                       g_res_prefetch, rowstat, colsum);
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32, false, 1>), dim3(ntm256 * 2), dim3(512), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw,
+                       (void*)((char*)C + (size_t)Na * cb), ldc, bias != nullptr ? bias + Na : nullptr,
+                       R != nullptr ? (const bf16_t*)R + Na : nullptr, ldr, M, 256, K, g_res_prefetch, rowstat,
+                       colsum != nullptr ? colsum + Na : nullptr);
     return;
   }
   if (big) {

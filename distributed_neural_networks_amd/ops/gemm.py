@@ -130,6 +130,13 @@ def set_gemm_tile(tile: int = 0) -> None:
     check(lib().gemm_set_tile(int(tile)), "gemm_set_tile")
 
 
+def set_gemm_split_tail(on: bool = True) -> None:
+    """A/B switch of the prefill tail split (gemm_bf16.hip launch_gemm): a
+    256^2 grid of full rounds plus one column of tiles runs that column as
+    256x128 tiles in a second launch (GPT-2 O / c_proj at M = 32768)."""
+    check(lib().gemm_set_split_tail(1 if on else 0), "gemm_set_split_tail")
+
+
 def set_gemm_half_cost(c: float = 1e9) -> None:
     """Auto tile rule: the time of a 256x128 tile relative to a 256x256 tile
     (256x128 is picked when its rounds x ``c`` beat the 256^2 rounds; the

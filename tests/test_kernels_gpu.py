@@ -366,3 +366,47 @@ def test_cifar_split_boundary_bit_identical(B):
     torch.cuda.synchronize()
     assert torch.equal(outs["fp32"][0], outs["split"][0])
     assert torch.equal(outs["fp32"][1], outs["split"][1])
+
+
+@pytest.mark.parametrize("K,act,res,fold", [(768, None, True, False), (3072, None, True, False),
+                                            (768, "gelu", False, False), (768, None, False, True)])
+def test_gemm_tail_split_matches_single_grid(K, act, res, fold):
+    """GPT-2's 768-wide prefill projections at M = 32768 run as 256^2 tiles on
+    the first 512 columns plus 256x128 tiles on the last 256 (two launches,
+    disjoint columns): identical to the single 256^2 grid (same per-output
+    MFMA order), with bias, residual, activation and the folded-norm epilogue,
+    and close to fp32."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_split_tail, set_gemm_tile
+    M, N = 32768, 768
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=DEV, generator=g) * 0.1
+    r = torch.randn(M, N, device=DEV, generator=g).bfloat16() if res else None
+    kw = {}
+    if fold:
+        st = torch.empty((M, 2), device=DEV, dtype=torch.float32)
+        T.row_stats(x, st, 1e-5, False, rows=M, ldx=K)
+        kw = dict(rowstat=st, colsum=w.float().sum(1).contiguous())
+    outs = []
+    try:
+        for tile, split in ((0, True), (256, False)):
+            set_gemm_tile(tile)
+            set_gemm_split_tail(split)
+            outs.append(linear(x, w, b, act, r, **kw))
+            torch.cuda.synchronize()
+    finally:
+        set_gemm_tile(0)
+        set_gemm_split_tail(True)
+    assert torch.equal(outs[0], outs[1])
+    xf = x.float()
+    if fold:
+        xf = torch.nn.functional.layer_norm(xf, (K,), eps=1e-5)
+    ref = xf @ w.float().t() + b
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    if res:
+        ref = ref + r.float()
+    err = ((outs[0].float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
