@@ -245,6 +245,7 @@ struct QkvScatter {
   const int* pos;
   int T, H, Hkv, hd_shift, S;  // head dim = 1 << hd_shift
   float invT;                  // 1 / T (row -> sequence without an integer division)
+  int c_off = 0;               // first qkv column of this launch (the tail-split launch covers the last 256)
 };
 
 // 8 consecutive output columns c..c+7 (one head) of row m -> destination.  The
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
           // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
           // residual, N % 32 == 0, hd % 8 == 0 -> a 32-column pair is whole or
           // past N, wave-uniformly)
-          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, bias, lane, scat);
+          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias, lane, scat);
         } else if (!OUT_F32 && pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
                              bias, R, ldr, lane);
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
           v[j] = acc[mq][nq][i][j] * (cs * rs);
         }
         if (SCATTER) {
-          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb, M, bias, lane, scat);
+          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias, lane, scat);
         } else if (ACT == ACT_SILU_MUL) {
           epi_silu_pair<false>(v[0], v[1], m, nb / 2, M, N / 2, C, ldc, vec, lane);
         } else if (rpre) {
@@ -876,6 +877,23 @@ extern "C" int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, 
   const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
   if ((hd & (hd - 1)) != 0 || M >= (1 << 24)) return -3;
   QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, __builtin_ctz(hd), S, 1.0f / (float)T};
+  // tail split as launch_gemm's (GPT-2 c_attn at M = 32768: 1024 + 128 tiles
+  // -> 4 rounds of 256^2 + 1 round of 256x128); the bias is indexed by the
+  // global column (c_off), the folded norm's colsum by the launch's own
+  const int ntm256 = (M + BG_M - 1) / BG_M;
+  if (g_split_tail && N % 256 == 0 && N >= 512 && (ntm256 * (N / 256 - 1)) % 256 == 0 && 2 * ntm256 <= 256) {
+    const int Na = N - 256;
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, Na, K,
+                       0, reinterpret_cast<const float2*>(rowstat), colsum, sc);
+    QkvScatter tail = sc;
+    tail.c_off = Na;
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true, 1>), dim3(ntm256 * 2), dim3(512), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw, q, hd, bias,
+                       (const bf16_t*)nullptr, 0, M, 256, K, 0, reinterpret_cast<const float2*>(rowstat),
+                       colsum != nullptr ? colsum + Na : nullptr, tail);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(tiles), dim3(512), 0, st, (const bf16_t*)A,
                      lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, N, K, 0,
                      reinterpret_cast<const float2*>(rowstat), colsum, sc);

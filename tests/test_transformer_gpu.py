@@ -979,12 +979,14 @@ def test_linear_norm_prefill_fold_vs_normalised_copy(M, N, K, rms, act):
 
 @pytest.mark.parametrize("B,T,H,Hkv,hd,pos0,S", [(4, 256, 12, 12, 64, 0, 300), (2, 200, 8, 2, 64, 30, 240),
                                                  (3, 100, 4, 4, 128, 7, 400), (2, 160, 12, 12, 64, 100, 200),
-                                                 (2, 192, 25, 25, 64, 0, 256)])
+                                                 (2, 192, 25, 25, 64, 0, 256),
+                                                 (64, 512, 12, 12, 64, 0, 520)])  # GPT-2 bench: tail-split launches
 def test_qkv_scatter_prefill(B, T, H, Hkv, hd, pos0, S):
     """Prefill c_attn with the QKV scatter epilogue (q head-major, K/V straight
     into the caches at pos[b] + t, rows past S dropped) == the qkv-row GEMM +
     qkv_split, bit for bit, with the folded LayerNorm; H = 25 (GPT-2 XL) has a
-    partial last column tile (N = 4800)."""
+    partial last column tile (N = 4800); B x T = 32768 at N = 2304 runs the
+    scatter as 256^2 + 256x128 launches (tail split)."""
     from distributed_neural_networks_amd.ops import gemm as G
     from distributed_neural_networks_amd.ops import transformer_ops as T_
     torch.manual_seed(12)
