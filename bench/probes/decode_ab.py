@@ -54,8 +54,8 @@ def apply(switch: str, v: int) -> None:
         gemm.set_gemm_half_cost(v / 100.0)
     elif switch == "decode_1p_ns":  # one-pass decode attention: at least v key splits (attention.hip)
         os.environ["DNN_DECODE_1P_NS"] = str(v)
-    elif switch == "split_tail":  # prefill 256^2 + 256x128 tail split (gemm_bf16.hip)
-        gemm.set_gemm_split_tail(bool(v))
+    elif switch == "split_tail":  # prefill 256^2 + 256x128 tail split (gemm_bf16.hip): mask 1 bf16, 2 fp8
+        gemm.set_gemm_split_tail(int(v))
     elif switch == "fused_head":  # decode head + argmax partials in one launch (gemm_head.h)
         gemm.set_fused_head(bool(v))
     elif switch == "argmax_split":

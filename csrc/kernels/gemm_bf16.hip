@@ -550,17 +550,19 @@ __device__ __forceinline__ void bg_mfma_f8(f32x4 (&acc)[MI][NJ], const bf16x8 (&
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int ACT, bool SCATTER = false>
+template <int ACT, bool SCATTER = false, int NQ = 2>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     const uint8_t* __restrict__ A8, const float* __restrict__ sa, const uint8_t* __restrict__ W8,
     const float* __restrict__ sw, bf16_t* __restrict__ C, int ldc, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb, QkvScatter scat = {}) {
+  static_assert(NQ == 1 || NQ == 2, "256x256 or 256x128 tiles");
+  constexpr int TN = 128 * NQ;  // NQ = 1: the 256x128 variant (tail-split launches), as the bf16 kernel's
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = (N + BG_N - 1) / BG_N, ntm = (M + BG_M - 1) / BG_M;
+  const int ntn = (N + TN - 1) / TN, ntm = (M + BG_M - 1) / BG_M;
   int tm, tn;
   tile_coords(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, tm, tn);
-  const int m0 = tm * BG_M, n0 = tn * BG_N;
+  const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = Kb / 128;
   // byte-identical staging: view the e4m3 rows as bf16 rows of half the length
@@ -568,11 +570,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
   const int lda = Kb / 2, ldw = Kb / 2;
 
-  f32x4 acc[2][2][4][2];
+  f32x4 acc[2][NQ][4][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NQ; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -588,6 +590,41 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     stage_half(W, ldw, n0 + h * 128, N, t * BG_K, half(u, 2 + h), wave, lane);
   };
 
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 64, brow = wc * 32;
+  if constexpr (NQ == 1) {
+    // the bf16 kernel's 2-phase K-tile (256x128), one scaled MFMA per tile pair
+    stA(0, 0, 0);
+    stB(0, 0, 0);
+    stA(0, 1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bg_barrier();
+    if (wr == 1) bg_barrier();
+    auto ktile1 = [&](const int t, auto ucst) {
+      constexpr int u = decltype(ucst)::value;
+      bg_read<2>(b0, half(u, 2), brow, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      bg_read<4>(af, half(u, 0), arow, lane);
+      stA(u ^ 1, 0, t + 1);
+      stB(u ^ 1, 0, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A1 of tile t landed
+      bg_barrier();
+      bg_mfma_f8<4, 2>(acc[0][0], af, b0);
+      bg_barrier();
+      bg_read<4>(af, half(u, 1), arow, lane);
+      stA(u ^ 1, 1, t + 1);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A0 / B0 of tile t+1 landed
+      bg_barrier();
+      bg_mfma_f8<4, 2>(acc[1][0], af, b0);
+      bg_barrier();
+    };
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      ktile1(t, std::integral_constant<int, 0>{});
+      ktile1(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nk) ktile1(t, std::integral_constant<int, 0>{});
+  } else {
   stA(0, 0, 0);
   stB(0, 1, 0);
   stA(0, 1, 0);
@@ -598,8 +635,6 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   bg_barrier();
   if (wr == 1) bg_barrier();
 
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  const int arow = wr * 64, brow = wc * 32;
   auto ktile = [&](const int t, auto ucst) {
     constexpr int u = decltype(ucst)::value;
     bg_read<2>(b0, half(u, 2), brow, lane);
@@ -632,19 +667,20 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     ktile(t + 1, std::integral_constant<int, 1>{});
   }
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
 
   const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
   // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
-  const bool rpre = ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + 255 < N;
-  bf16x4 rr[2][2][4][2];
+  const bool rpre = ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + TN - 1 < N;
+  bf16x4 rr[2][NQ][4][2];
   if (rpre) {
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-      for (int nq = 0; nq < 2; ++nq)
+      for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           epi_pair_res_load(m0 + mq * 128 + arow + i * 16 + (lane & 15), n0 + nq * 128 + wc * 32, M, R, ldr, lane,
@@ -653,7 +689,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-    for (int nq = 0; nq < 2; ++nq)
+    for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
@@ -746,7 +782,9 @@ extern "C" int dnn_gemm_set_tile(int tile) {
 // 768, and the GPT-2 4-stage prefill 3.85 -> 3.76 M tok/s — the 2-phase
 // schedule, one K-tile ahead, loses more per tile than the full last round
 // saves; tile 255 keeps it selectable.
-// the 256^2 + 256x128 tail split in launch_gemm (A/B switch; DNN_SPLIT_TAIL=0 starts with it off)
+// the 256^2 + 256x128 tail split (A/B switch, a bit mask: 1 the bf16 kernel, 2 the fp8 one; DNN_SPLIT_TAIL
+// sets the start value).  fp8 is off by default: GPT-2 XL prefill 259.5 -> 257.4 k tok/s with it
+// (profiles/r4_prefill_ab_tail_split_gpt2xl.jsonl), bf16 GPT-2 +1.6 %
 static int g_split_tail = [] {
   const char* e = getenv("DNN_SPLIT_TAIL");
   return e != nullptr ? atoi(e) : 1;
@@ -754,6 +792,19 @@ static int g_split_tail = [] {
 extern "C" int dnn_gemm_set_split_tail(int on) {
   g_split_tail = on;
   return 0;
+}
+
+// Tail split rule: the columns of the 256^2 part (a multiple of 256), or 0.
+// Applies when the 256^2 grid is whole rounds of 256 tiles plus one last
+// column of tiles (1..256 columns wide) that fits one more round as 256x128
+// tiles: GPT-2 (N 768 / 2304) and GPT-2 XL (N 1600 / 4800 / 6400) at M = 32768.
+static int tail_split_cols(int M, int N, bool fp8 = false) {
+  if (!(g_split_tail & (fp8 ? 2 : 1)) || g_gemm_tile != 0) return 0;
+  const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
+  if (ntn < 2 || (ntm * (ntn - 1)) % 256 != 0) return 0;
+  const int Na = (ntn - 1) * 256;
+  if (ntm * ((N - Na + 127) / 128) > 256) return 0;
+  return Na;
 }
 
 static float g_half_cost = 1e9f;
@@ -807,17 +858,17 @@ static void launch_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   // in a second launch — 1 + 1/2 rounds instead of 2 full ones, no workspace
   // and no reduction (the two launches write disjoint columns).
   const int ntm256 = (M + BG_M - 1) / BG_M;
-  if (big && g_split_tail && g_gemm_tile == 0 && ACT != ACT_SILU_MUL && N % 256 == 0 && N >= 512 &&
-      (ntm256 * (N / 256 - 1)) % 256 == 0 && 2 * ntm256 <= 256) {
-    const int Na = N - 256;
+  const int Na = (big && ACT != ACT_SILU_MUL) ? tail_split_cols(M, N) : 0;
+  if (Na > 0) {
+    const int Nt = N - Na;
     const size_t cb = F32 ? sizeof(float) : sizeof(bf16_t);
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,
                        (const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, bias, (const bf16_t*)R, ldr, M, Na, K,
                        g_res_prefetch, rowstat, colsum);
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32, false, 1>), dim3(ntm256 * 2), dim3(512), 0, st,
-                       (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw,
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT, F32, false, 1>), dim3(ntm256 * ((Nt + 127) / 128)), dim3(512), 0,
+                       st, (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw,
                        (void*)((char*)C + (size_t)Na * cb), ldc, bias != nullptr ? bias + Na : nullptr,
-                       R != nullptr ? (const bf16_t*)R + Na : nullptr, ldr, M, 256, K, g_res_prefetch, rowstat,
+                       R != nullptr ? (const bf16_t*)R + Na : nullptr, ldr, M, Nt, K, g_res_prefetch, rowstat,
                        colsum != nullptr ? colsum + Na : nullptr);
     return;
   }
@@ -881,16 +932,17 @@ extern "C" int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, 
   // -> 4 rounds of 256^2 + 1 round of 256x128); the bias is indexed by the
   // global column (c_off), the folded norm's colsum by the launch's own
   const int ntm256 = (M + BG_M - 1) / BG_M;
-  if (g_split_tail && N % 256 == 0 && N >= 512 && (ntm256 * (N / 256 - 1)) % 256 == 0 && 2 * ntm256 <= 256) {
-    const int Na = N - 256;
+  const int Na = tail_split_cols(M, N);
+  if (Na > 0) {
+    const int Nt = N - Na;
     hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,
                        (const bf16_t*)A, lda, (const bf16_t*)W, ldw, q, hd, bias, (const bf16_t*)nullptr, 0, M, Na, K,
                        0, reinterpret_cast<const float2*>(rowstat), colsum, sc);
     QkvScatter tail = sc;
     tail.c_off = Na;
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true, 1>), dim3(ntm256 * 2), dim3(512), 0, st,
-                       (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw, q, hd, bias,
-                       (const bf16_t*)nullptr, 0, M, 256, K, 0, reinterpret_cast<const float2*>(rowstat),
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<ACT_NONE, false, true, 1>), dim3(ntm256 * ((Nt + 127) / 128)),
+                       dim3(512), 0, st, (const bf16_t*)A, lda, (const bf16_t*)W + (size_t)Na * ldw, ldw, q, hd, bias,
+                       (const bf16_t*)nullptr, 0, M, Nt, K, 0, reinterpret_cast<const float2*>(rowstat),
                        colsum != nullptr ? colsum + Na : nullptr, tail);
     return (int)hipGetLastError();
   }
@@ -911,6 +963,19 @@ extern "C" int dnn_gemm_fp8_qkv_scatter(const void* A8, const float* sa, const v
   const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
   if ((hd & (hd - 1)) != 0 || M >= (1 << 24)) return -3;
   QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, __builtin_ctz(hd), S, 1.0f / (float)T};
+  const int Na = tail_split_cols(M, N, true);  // GPT-2 XL c_attn (N = 4800): 2304 + 256 half tiles
+  if (Na > 0) {
+    const int ntm256 = (M + BG_M - 1) / BG_M, Nt = N - Na;
+    hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,
+                       (const uint8_t*)A8, sa, (const uint8_t*)W8, sw, (bf16_t*)q, hd, bias, (const bf16_t*)nullptr, 0,
+                       M, Na, Kb, sc);
+    QkvScatter tail = sc;
+    tail.c_off = Na;
+    hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true, 1>), dim3(ntm256 * ((Nt + 127) / 128)), dim3(512), 0,
+                       st, (const uint8_t*)A8, sa, (const uint8_t*)W8 + (size_t)Na * Kb, sw + Na, (bf16_t*)q, hd, bias,
+                       (const bf16_t*)nullptr, 0, M, Nt, Kb, tail);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A8, sa,
                      (const uint8_t*)W8, sw, (bf16_t*)q, hd, bias, (const bf16_t*)nullptr, 0, M, N, Kb, sc);
   return (int)hipGetLastError();
@@ -925,8 +990,21 @@ extern "C" int dnn_gemm_fp8_256(const void* A, const float* sa, const void* W, c
   if (Kb % 128 != 0 || M <= 0 || N <= 0 || sa == nullptr || sw == nullptr) return -1;
   if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
   const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+  // tail split (as launch_gemm's): GPT-2 XL O / c_proj (N = 1600) and c_fc (N = 6400) at M = 32768
+  const int Na = act != ACT_SILU_MUL ? tail_split_cols(M, N, true) : 0;
+  const int ntm256 = (M + BG_M - 1) / BG_M, Nt = N - Na;
 #define F8L(a)                                                                                                    \
   if (act == a) {                                                                                                 \
+    if (Na > 0) {                                                                                                 \
+      hipLaunchKernelGGL((gemm_fp8_256_kernel<a>), dim3(ntm256 * (Na / 256)), dim3(512), 0, st,                   \
+                         (const uint8_t*)A, sa, (const uint8_t*)W, sw, (bf16_t*)C, ldc, bias, (const bf16_t*)R,    \
+                         ldr, M, Na, Kb);                                                                         \
+      hipLaunchKernelGGL((gemm_fp8_256_kernel<a, false, 1>), dim3(ntm256 * ((Nt + 127) / 128)), dim3(512), 0, st, \
+                         (const uint8_t*)A, sa, (const uint8_t*)W + (size_t)Na * Kb, sw + Na, (bf16_t*)C + Na,    \
+                         ldc, bias != nullptr ? bias + Na : nullptr,                                              \
+                         R != nullptr ? (const bf16_t*)R + Na : nullptr, ldr, M, Nt, Kb);                         \
+      return (int)hipGetLastError();                                                                              \
+    }                                                                                                             \
     hipLaunchKernelGGL((gemm_fp8_256_kernel<a>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A, sa,            \
                        (const uint8_t*)W, sw, (bf16_t*)C, ldc, bias, (const bf16_t*)R, ldr, M, N, Kb);            \
     return (int)hipGetLastError();                                                                                \

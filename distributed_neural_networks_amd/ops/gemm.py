@@ -130,11 +130,14 @@ def set_gemm_tile(tile: int = 0) -> None:
     check(lib().gemm_set_tile(int(tile)), "gemm_set_tile")
 
 
-def set_gemm_split_tail(on: bool = True) -> None:
-    """A/B switch of the prefill tail split (gemm_bf16.hip launch_gemm): a
+def set_gemm_split_tail(on=True) -> None:
+    """A/B switch of the prefill tail split (gemm_bf16.hip tail_split_cols): a
     256^2 grid of full rounds plus one column of tiles runs that column as
-    256x128 tiles in a second launch (GPT-2 O / c_proj at M = 32768)."""
-    check(lib().gemm_set_split_tail(1 if on else 0), "gemm_set_split_tail")
+    256x128 tiles in a second launch (GPT-2 O / c_proj / c_attn at M = 32768).
+    ``on``: True = the default (bf16 kernel only), False = off, or an int
+    bit mask (1 bf16, 2 fp8)."""
+    mask = (1 if on else 0) if isinstance(on, bool) else int(on)
+    check(lib().gemm_set_split_tail(mask), "gemm_set_split_tail")
 
 
 def set_gemm_half_cost(c: float = 1e9) -> None:

@@ -410,3 +410,38 @@ def test_gemm_tail_split_matches_single_grid(K, act, res, fold):
         ref = ref + r.float()
     err = ((outs[0].float() - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("N,K,split,act,res", [(1600, 1600, True, 0, True), (6400, 1600, True, 2, False),
+                                               (1600, 6400, False, 0, True), (4800, 1600, True, 0, False)])
+def test_fp8_gemm_tail_split_matches_single_grid(N, K, split, act, res):
+    """GPT-2 XL prefill shapes on the fp8 256^2 kernel at M = 32768: the grid's
+    last column of tiles (64 / 256 / 192 wide) as 256x128 tiles in a second
+    launch gives the single grid's bits (split activations or not, GELU,
+    residual)."""
+    from distributed_neural_networks_amd.ops.fp8 import attach_split, linear_fp8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import set_gemm_split_tail
+    M = 32768
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = quantize_weight(torch.randn(N, K, device=DEV, generator=g) / K ** 0.5, DEV)
+    if split:
+        attach_split(w)
+    b = torch.randn(N, device=DEV, generator=g) * 0.1
+    r = torch.randn(M, N, device=DEV, generator=g).bfloat16() if res else None
+    outs = []
+    try:
+        for mask in (3, 0):  # fp8 split on (off by default) / off
+            set_gemm_split_tail(mask)
+            outs.append(linear_fp8(x, w, b, act, r))
+            torch.cuda.synchronize()
+    finally:
+        set_gemm_split_tail(True)
+    assert torch.equal(outs[0], outs[1])
+    ref = x.float() @ (w.q[:, :K].float() * w.scale[:, None]).t() + b
+    if act == 2:
+        ref = torch.nn.functional.gelu(ref)
+    if res:
+        ref = ref + r.float()
+    err = ((outs[0].float() - ref).norm() / ref.norm()).item()
+    assert err < (3e-2 if split else 8e-2), err
