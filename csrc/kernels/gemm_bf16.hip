@@ -799,10 +799,13 @@ extern "C" int dnn_gemm_set_split_tail(int on) {
 // column of tiles (1..256 columns wide) that fits one more round as 256x128
 // tiles: GPT-2 (N 768 / 2304) and GPT-2 XL (N 1600 / 4800 / 6400) at M = 32768.
 static int tail_split_cols(int M, int N, bool fp8 = false) {
-  if (!(g_split_tail & (fp8 ? 2 : 1)) || g_gemm_tile != 0) return 0;
+  // fp8: bit 2 every tail, bit 4 only tails of >= 128 columns (GPT-2 XL c_attn / c_fc, not the 64-column
+  // tail of the 1600-wide O / c_proj)
+  if (!(g_split_tail & (fp8 ? 6 : 1)) || g_gemm_tile != 0) return 0;
   const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
   if (ntn < 2 || (ntm * (ntn - 1)) % 256 != 0) return 0;
   const int Na = (ntn - 1) * 256;
+  if (fp8 && !(g_split_tail & 2) && N - Na < 128) return 0;
   if (ntm * ((N - Na + 127) / 128) > 256) return 0;
   return Na;
 }
