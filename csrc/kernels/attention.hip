@@ -294,9 +294,9 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int g = 0; g < 16; g += 2) mx = fmaxf(mx, fmaxf(sacc[kt][g], sacc[kt][g + 1]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx * scale_log2);
+        for (int g = 0; g < 16; g += 2) mx = fmax_nan(mx, fmax_nan(sacc[kt][g], sacc[kt][g + 1]));
+      mx = fmax_nan(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmax_nan(m_i, mx * scale_log2);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
       // exponent arguments, row sums and the O rescale on packed fp32 math

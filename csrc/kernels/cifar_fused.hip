@@ -259,7 +259,7 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
 #pragma unroll
       for (int qx = 0; qx < 2; ++qx) {
         const int g0 = (2 * qy) * 4 + 2 * qx;
-        v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
+        v[qy * 2 + qx] = fmaxf(fmax_nan(fmax_nan(acc[g0], acc[g0 + 1]), fmax_nan(acc[g0 + 4], acc[g0 + 5])) + bias1, 0.f);
       }
     const bool odd = r32 & 1;
     const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_v4_kernel(
 #pragma unroll
             for (int qx = 0; qx < 2; ++qx) {
               const int g0 = (2 * qy) * 4 + 2 * qx;
-              pv[qx] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias,
+              pv[qx] = fmaxf(fmax_nan(fmax_nan(acc[i][g0], acc[i][g0 + 1]), fmax_nan(acc[i][g0 + 4], acc[i][g0 + 5])) + bias,
                              0.f);
             }
             const int PY = 2 * ty2 + qy, PX = 4 * tx2 + 2 * h;

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
 #pragma unroll
         for (int qx = 0; qx < 2; ++qx) {
           const int g0 = (2 * qy) * 4 + 2 * qx;
-          v[qy * 2 + qx] = fmaxf(fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g0 + 4], acc[g0 + 5])) + bias, 0.f);
+          v[qy * 2 + qx] = fmaxf(fmax_nan(fmax_nan(acc[g0], acc[g0 + 1]), fmax_nan(acc[g0 + 4], acc[g0 + 5])) + bias, 0.f);
         }
       const bool odd = r32 & 1;
       const int s0 = __float_as_int(odd ? v[0] : v[2]), s1 = __float_as_int(odd ? v[1] : v[3]);
@@ -308,8 +308,8 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
             float v[2][2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-              v[i][0] = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
-              v[i][1] = fmaxf(fmaxf(fmaxf(acc[i][g0 + 2], acc[i][g0 + 3]), fmaxf(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
+              v[i][0] = fmaxf(fmax_nan(fmax_nan(acc[i][g0], acc[i][g0 + 1]), fmax_nan(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
+              v[i][1] = fmaxf(fmax_nan(fmax_nan(acc[i][g0 + 2], acc[i][g0 + 3]), fmax_nan(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
                               0.f);
             }
             const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][0]), __float_as_uint(v[1][0]), false,
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(512, 1) void cifar_stage0_x3_kernel(
           for (int qy = 0; qy < 2; ++qy) {
             float2 pv;
             const int g0 = (2 * qy) * 4;
-            pv.x = fmaxf(fmaxf(fmaxf(acc[i][g0], acc[i][g0 + 1]), fmaxf(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
-            pv.y = fmaxf(fmaxf(fmaxf(acc[i][g0 + 2], acc[i][g0 + 3]), fmaxf(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
+            pv.x = fmaxf(fmax_nan(fmax_nan(acc[i][g0], acc[i][g0 + 1]), fmax_nan(acc[i][g0 + 4], acc[i][g0 + 5])) + bias, 0.f);
+            pv.y = fmaxf(fmax_nan(fmax_nan(acc[i][g0 + 2], acc[i][g0 + 3]), fmax_nan(acc[i][g0 + 6], acc[i][g0 + 7])) + bias,
                          0.f);
             const int PY = 2 * ty2 + qy, PX = 4 * i + 2 * h;
             if constexpr (SPLIT_OUT) {
