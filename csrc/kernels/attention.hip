@@ -149,6 +149,12 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // (positions >= pos[b]) are read straight from it, older keys from the cache,
 // and the first query head of each kv group copies its 128-row slice of new
 // K/V into the cache — the qkv_split launch and its round trip disappear.
+// grid (H, B, query blocks), dispatched x fastest: every (b, h) of the last
+// query block (the causal diagonal's longest key range) goes first, the
+// one-block workgroups fill the tail (longest-processing-time-first).  With
+// blockIdx.x = query block the heavy workgroups were spread over the whole
+// dispatch and the last ones ran alone: GPT-2 B=64 T=512 0.1050 -> 0.0931 ms,
+// T=2048 0.140 -> 0.089, hd 128 T=4096 1.092 -> 0.781 (profiles/r4_flash_lpt_ab.jsonl)
 template <int HD, bool QKV = false, bool KV8 = false, bool DB = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   constexpr int CH = HD / 8;    // 16-B chunks per row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
-  const int qb = blockIdx.x, hh = blockIdx.y, b = blockIdx.z;
+  const int qb = (int)(gridDim.z - 1 - blockIdx.z), hh = blockIdx.x, b = blockIdx.y;
   const int kvh = hh / (H / Hkv);
   const int p0 = pos != nullptr ? pos[b] : 0;
   const int kv_len = p0 + T;
@@ -1298,7 +1304,7 @@ static void launch_flash(dim3 grid, hipStream_t st, const bf16_t* q, const bf16_
 extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, void* o, int B, int T, int H, int Hkv,
                               int hd, int S, const int* pos, float scale, hipStream_t st, int kv8) {
   if (H % Hkv != 0) return -1;
-  dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
+  dim3 grid(H, B, (T + FA_QB - 1) / FA_QB);
   const float sl2 = scale * 1.4426950408889634f;
   const bf16_t *q_ = (const bf16_t*)q, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
   bf16_t* o_ = (bf16_t*)o;
@@ -1323,7 +1329,7 @@ extern "C" int dnn_flash_attn(const void* q, const void* kc, const void* vc, voi
 extern "C" int dnn_flash_attn_qkv(const void* qkv, int ldqkv, void* kc, void* vc, void* o, int B, int T, int H,
                                   int Hkv, int hd, int S, const int* pos, float scale, hipStream_t st, int kv8) {
   if (H % Hkv != 0 || ldqkv < (H + 2 * Hkv) * hd || (ldqkv % 8) != 0) return -1;
-  dim3 grid((T + FA_QB - 1) / FA_QB, H, B);
+  dim3 grid(H, B, (T + FA_QB - 1) / FA_QB);
   const float sl2 = scale * 1.4426950408889634f;
   const bf16_t *q_ = (const bf16_t*)qkv, *k_ = (const bf16_t*)kc, *v_ = (const bf16_t*)vc;
   bf16_t *o_ = (bf16_t*)o, *ko = (bf16_t*)kc, *vo = (bf16_t*)vc;
