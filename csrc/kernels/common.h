@@ -29,10 +29,11 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-// NaN-propagating max (llvm.maximum -> v_maximum3_f32 on gfx950).  fmaxf in
-// the kernels' IEEE mode first quiets every operand the compiler cannot prove
-// canonical (MFMA results, selects) with a v_max_f32 x, x of its own, which
-// doubled the max work of the flash softmax; this form needs none.
+// NaN-propagating max (llvm.maximum -> v_maximum3_f32 on gfx950).  In IEEE
+// mode fmaxf first quiets every operand the compiler cannot prove canonical
+// (MFMA results, selects) with a v_max_f32 x, x of its own unless the file is
+// built with -fno-honor-nans (ops/build.py PER_FILE_FLAGS); this form needs no
+// quieting under any flags.
 __device__ __forceinline__ float fmax_nan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 
 // Exact-erf GELU (nanoGPT's nn.GELU()) without the branchy libm erff: with
