@@ -41,18 +41,22 @@ Scaling is weak: each stage-0 GPU sources ``--batch`` images per step.
 """
 from __future__ import annotations
 
+import time
+
+_T0 = time.perf_counter()  # process start, before torch loads: the --time_budget_s clock
+
 import argparse
 import json
 import os
 import statistics
 import sys
-import time
 
 import torch
 
 BASELINE_IMG_S = 4150.0  # reference CIFAR-10 2-stage, best batch (255), CPU gRPC
 METRIC = "images/sec CIFAR-10 2-stage"
 DTYPE_LABEL = {"fp32": "fp32 (bf16x3 split emulation, ~2^-16 per product)", "bf16": "bf16"}
+CPU_DTYPE_LABEL = "fp32 (torch CPU golden stages over gloo: schedule test, not a measurement)"
 
 
 def parse():
@@ -84,10 +88,24 @@ def parse():
     ap.add_argument("--cut", default="auto", choices=["auto", "1", "2"],
                     help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = per placement")
     ap.add_argument("--extra_budget_s", type=float, default=420.0,
-                    help="N>1: wall-clock budget of the extra keys (a hang only drops keys)")
-    ap.add_argument("--launch_timeout", type=float, default=1800.0,
-                    help="N>1 without a launcher: wall-clock limit of the self-launched job")
-    return ap.parse_args()
+                    help="N>1: wall-clock cap of the extra keys (a hang only drops keys)")
+    ap.add_argument("--time_budget_s", type=float, default=480.0,
+                    help="whole-run wall-clock budget per rank, from process start: the N>1 extras get what "
+                         "the headline left (minus a margin) and are skipped or cut when it runs out")
+    ap.add_argument("--launch_timeout", type=float, default=-1.0,
+                    help="N>1 without a launcher: wall-clock limit of the self-launched job "
+                         "(-1 = --time_budget_s + 240 s)")
+    a = ap.parse_args()
+    if a.launch_timeout < 0:
+        a.launch_timeout = a.time_budget_s + 240.0
+    return a
+
+
+EXTRAS_MARGIN_S = 20.0  # kept back from the budget for the line itself and shutdown
+
+
+def elapsed_s() -> float:
+    return time.perf_counter() - _T0
 
 
 def dist_setup(n, cpu=False):
@@ -284,27 +302,75 @@ def bench_pp2(args, info):
     stream(args.steps)
     t1 = sync_time(info)
     p50 = pp2_latency(args, info, s0, s1, back)
-    return t1 - t0, n * mb * M / N, p50, f"pp2-rccl-{n}x{n}" + ("-bipartite" if n > 1 else "")
+    fabric = "rccl" if dev.type == "cuda" else "gloo-cpu"
+    return t1 - t0, n * mb * M / N, p50, f"pp2-{fabric}-{n}x{n}" + ("-bipartite" if n > 1 else "")
 
 
-def hop_bandwidth(info, nbytes: int, reps: int = 4) -> float:
+def _settle(work, timeout_s: float) -> None:
+    """Complete one link op on the host, bounded where the link allows it."""
+    if hasattr(work, "ch"):  # native RCCL work: a bounded host wait
+        work.synchronize(timeout_s)
+    else:
+        work.wait()
+
+
+def agree(info, tag: str, err: str, store=None) -> str:
+    """Every rank publishes its local verdict (``err``: "" = ok) through the
+    process group's TCP store and reads everyone's: returns the first failure
+    of any rank, or "".  No collective, so it holds when the failure is in the
+    communicator itself — the ranks then skip the same section together
+    instead of some of them blocking in a barrier the others never reach."""
+    if info.world == 1:
+        return err
+    import torch.distributed as dist
+    st = store or dist.distributed_c10d._get_default_store()
+    seq = _AGREE_SEQ[0]
+    _AGREE_SEQ[0] += 1
+    st.set(f"dnn/agree/{tag}/{seq}/{info.rank}", err or "ok")
+    for q in range(info.world):
+        v = st.get(f"dnn/agree/{tag}/{seq}/{q}").decode(errors="replace")
+        if v != "ok":
+            return v
+    return ""
+
+
+_AGREE_SEQ = [0]
+
+
+def hop_bandwidth(info, nbytes: int, reps: int = 4, timeout_s: float = 60.0) -> float:
     """GB/s of one stage hop, measured on its own: rank 2p sends ``nbytes``
     ``reps`` times to rank 2p+1 over the same link type as the pp2 hop (native
     RCCL channel, or ProcessGroupNCCL / gloo), every pair at once; the slowest
     pair's rate.  Reported next to the pp2 headline: the reference cut moves
     16 KiB per image, so at N >= 2 the headline is bounded by pairs x this
-    rate / 16 KiB, whatever the stage kernels do."""
+    rate / 16 KiB, whatever the stage kernels do.
+
+    The link setup and a warm transfer (bounded by ``timeout_s``) run first
+    and the ranks agree on their outcome through the store before any
+    collective: one rank's failure skips the measurement on every rank
+    (raising the same error everywhere) instead of leaving the others in the
+    timing barrier."""
     from distributed_neural_networks_amd.parallel.links import make_link
     from distributed_neural_networks_amd.parallel import rccl
     r, N, dev = info.rank, info.world, info.device
     peer = r ^ 1
     el = 0.0
     with rccl.scope(dev):
-        if peer < N:
-            link = make_link(peer, dev)
-            buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            op = link.send if r % 2 == 0 else link.recv
-            op(buf)  # warm: channel / communicator setup outside the timing
+        err = ""
+        try:
+            if peer < N:
+                link = make_link(peer, dev)
+                if hasattr(link, "ch"):
+                    link.ch.ready(timeout_s)
+                buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                post = link.isend if r % 2 == 0 else link.irecv
+                _settle(post(buf), timeout_s)  # warm: channel / communicator setup outside the timing
+                op = link.send if r % 2 == 0 else link.recv
+        except Exception as e:  # noqa: BLE001 — agreed below, raised on every rank
+            err = f"rank {r}: {type(e).__name__}: {e}"[:200]
+        bad = agree(info, "hop", err)
+        if bad:
+            raise RuntimeError(f"hop setup failed: {bad}")
         t0 = sync_time(info)
         if peer < N:
             for _ in range(reps):
@@ -312,6 +378,33 @@ def hop_bandwidth(info, nbytes: int, reps: int = 4) -> float:
         el = sync_time(info) - t0
     el = max_over_ranks(info, el)
     return nbytes * reps / el / 1e9 if el > 0 else float("nan")
+
+
+class Deadline:
+    """A wall-clock backstop for a multi-rank section: if the block is still
+    running after ``seconds``, rank 0 prints the line it has (noting what was
+    cut) and every rank exits 0, so a hang only drops keys and never the
+    headline."""
+
+    def __init__(self, seconds: float, line, what: str):
+        import threading
+        self.what = what
+
+        def bail():
+            if line is not None:
+                line["extras_error"] = f"{self.what} exceeded its {seconds:.0f} s budget; skipped"
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        self.timer = threading.Timer(max(1.0, seconds), bail)
+        self.timer.daemon = True
+
+    def __enter__(self):
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.cancel()
+        return False
 
 
 def pp2_latency(args, info, s0, s1, back) -> float:
@@ -574,6 +667,8 @@ def main():
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
         import gpt_bench
         return gpt_bench.main(args)
+    phases = {"startup_s": round(elapsed_s(), 2)}
+    tp = time.perf_counter()
     info = dist_setup(args.gpus, args.cpu)
     selflaunch.check_world(args.gpus, info.world)
     N = info.world
@@ -596,6 +691,8 @@ def main():
         n_cu = torch.cuda.get_device_properties(info.device).multi_processor_count
         cops.set_stage0_grid(max(1, n_cu - spare))
     fill = 0.0
+    phases["init_s"] = round(time.perf_counter() - tp, 2)
+    tp = time.perf_counter()
     from distributed_neural_networks_amd.parallel import rccl
     with rccl.scope(info.device):  # this placement's native channels close when it is measured
         if N == 1:
@@ -611,8 +708,11 @@ def main():
     total = imgs_per_gpu * N * args.steps
     value = total / el
     extra = {}
+    phases["headline_s"] = round(time.perf_counter() - tp, 2)
     if N == 1 and not args.no_extra and info.device.type == "cuda":
+        tp = time.perf_counter()
         extra = extra_keys(args, info)
+        phases["extras_s"] = round(time.perf_counter() - tp, 2)
     hop_kib = 4 * (4 if args.precision == "fp32" else 2)
     out = None
     if info.rank == 0:
@@ -620,7 +720,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_S, 2),
-            "dtype": DTYPE_LABEL[args.precision], "data": "synthetic (random fp32 images, random-init weights)",
+            "dtype": DTYPE_LABEL[args.precision] if info.device.type == "cuda" else CPU_DTYPE_LABEL,
+            "data": "synthetic (random fp32 images, random-init weights)",
             "p50_latency_ms": None if p50 != p50 else round(p50, 4),
             "config": {"model": "cifar10-convnet (cifar_model_parts.py NeuralNetwork)",
                        "global_batch": int(round(imgs_per_gpu * N)), "seq_len": None, "parallelism": par,
@@ -631,11 +732,15 @@ def main():
                                      2: f"conv+fc1|fc2 ({hop_kib // 8} KiB/img hop)"}[args._cut]},
         }
         if info.device.type == "cuda" and args.precision == "fp32":
+            tp = time.perf_counter()
             out.update(precision_check(info.device, args.precision, 16384))
+            phases["precision_check_s"] = round(time.perf_counter() - tp, 2)
         out.update(extra)
     if N > 1 and args.placement == "pp2":
+        tp = time.perf_counter()
         try:
-            bw = hop_bandwidth(info, (4 << 20) if info.device.type != "cuda" else (256 << 20))
+            with Deadline(min(120.0, max(10.0, args.time_budget_s - elapsed_s() - EXTRAS_MARGIN_S)), out, "hop"):
+                bw = hop_bandwidth(info, (4 << 20) if info.device.type != "cuda" else (256 << 20))
             if out is not None:
                 pairs = N // 2
                 out["hop_GBps_per_pair"] = round(bw, 2)
@@ -643,8 +748,13 @@ def main():
         except Exception as e:  # noqa: BLE001 — a diagnostic: never costs the headline
             if out is not None:
                 out["hop_GBps_error"] = f"{type(e).__name__}: {e}"[:200]
+        phases["hop_s"] = round(time.perf_counter() - tp, 2)
     if N > 1 and not args.no_extra:
-        multi_gpu_extras(args, info, out)
+        multi_gpu_extras(args, info, out, phases)
+    if out is not None:
+        phases["total_s"] = round(elapsed_s(), 2)
+        out["phase_s"] = phases
+        out["time_budget_s"] = args.time_budget_s
     if info.rank == 0:
         print(json.dumps(out), flush=True)
     if N > 1:
@@ -668,30 +778,37 @@ RINGS = (
 )
 
 
-def multi_gpu_extras(args, info, line):
-    """Extra keys at N > 1, on every rank, under one wall-clock budget: the
+def multi_gpu_extras(args, info, line, phases):
+    """Extra keys at N > 1, on every rank, inside the run's time budget: the
     fc1-cut CIFAR plan, then the GPT-2 4-stage, Llama-3 8B 8-stage and GPT-2 XL
     fp8 8-stage decode rings across min(N, stages) GPU groups (tokens back to
-    group 0 over RCCL) with per-token p50.  A failure drops that key; a hang
+    group 0 over RCCL) with per-token p50.  The extras get what the headline
+    left of ``--time_budget_s`` (at most ``--extra_budget_s``); the ranks agree
+    on the remaining time (the slowest rank's clock) before each section and
+    skip the rest together when it is short.  A failure drops that key; a hang
     past the budget makes every rank exit 0 (rank 0 first prints the line it
-    has), so the headline is never lost."""
+    has), so the headline is never lost.  Each section's seconds go into
+    ``phase_s``."""
     import copy
-    import threading
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
     import gpt_bench
     from distributed_neural_networks_amd.parallel import comm, rccl
-    current = ["fc1cut"]
 
-    def bail():
+    def remaining() -> float:  # agreed: every rank runs the same collective here
+        return args.time_budget_s - EXTRAS_MARGIN_S - max_over_ranks(info, elapsed_s())
+
+    budget = min(args.extra_budget_s, remaining())
+    if budget < 15.0:
         if line is not None:
-            line["extras_error"] = f"{current[0]} exceeded the {args.extra_budget_s:.0f} s extras budget; skipped"
-            print(json.dumps(line), flush=True)
-        os._exit(0)
-    timer = threading.Timer(args.extra_budget_s, bail)
-    timer.daemon = True
-    timer.start()
+            line["extras_skipped"] = f"time budget: {budget:.0f} s left of {args.time_budget_s:.0f} s"
+        return
+    t_end = time.perf_counter() + budget
     cuda = info.device.type == "cuda"
-    try:
+    # minimum seconds a section needs to be worth starting (setup + a few steps)
+    need = {"fc1cut": 10.0, "gpt2_4stage": 20.0, "llama3_8b_8stage_b32": 45.0, "gpt2xl_fp8_8stage_b64": 45.0}
+    with Deadline(budget, line, "extras") as dl:
+        tp = time.perf_counter()
+        dl.what = "fc1cut"
         try:
             a = copy.copy(args)
             a.latency_iters = 3
@@ -706,11 +823,18 @@ def multi_gpu_extras(args, info, line):
         except Exception as e:  # noqa: BLE001
             if line is not None:
                 line["fc1cut_error"] = f"{type(e).__name__}: {e}"[:200]
+        phases["fc1cut_s"] = round(time.perf_counter() - tp, 2)
         for key, argv_gpu, argv_cpu, label in RINGS:
-            current[0] = key
+            dl.what = key
             if cuda:
                 torch.cuda.empty_cache()
             comm.barrier(info)
+            left = max_over_ranks(info, t_end - time.perf_counter())
+            if cuda and left < need[key]:
+                if line is not None:
+                    line[key + "_skipped"] = f"time budget: {left:.0f} s left"
+                continue
+            tp = time.perf_counter()
             argv = ["--gpus", str(info.world)] + (argv_gpu if cuda else
                                                   ["--cpu", "--steps", "3", "--warmup", "1", "--batch", "2",
                                                    "--prompt", "8", "--prefill_iters", "1"] + argv_cpu)
@@ -720,7 +844,8 @@ def multi_gpu_extras(args, info, line):
             except Exception as e:  # noqa: BLE001
                 if line is not None:
                     line[key + "_error"] = f"{type(e).__name__}: {e}"[:200]
-                continue
+                g = None
+            phases[key + "_s"] = round(time.perf_counter() - tp, 2)
             if line is not None and g is not None:
                 c = g["config"]
                 line[key + "_decode_tok_s"] = g["value"]
@@ -729,9 +854,8 @@ def multi_gpu_extras(args, info, line):
                 line[key + "_p50_token_ms"] = g["decode_p50_token_latency_ms"]
                 line[key + "_config"] = dict(
                     c, model=label if cuda else f"{c['model']} (gloo schedule test)",
-                    placement=f"{c['gpu_groups']} GPU groups x {c['replicas']} replicas, decode ring over RCCL")
-    finally:
-        timer.cancel()
+                    placement=f"{c['gpu_groups']} GPU groups x {c['replicas']} replicas, decode ring over "
+                              + ("RCCL" if cuda else "gloo (CPU)"))
 
 
 if __name__ == "__main__":

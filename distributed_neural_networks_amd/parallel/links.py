@@ -144,24 +144,38 @@ class HostStagedLink(P2PLink):
     def _sender(self):
         """One thread per link posts the gloo sends in order, each once its
         device->host copy has landed, so ``isend`` never blocks the host on
-        the compute queued before it (as an RCCL send does not)."""
+        the compute queued before it (as an RCCL send does not).  The thread
+        holds the queue, not the link: ``close()`` — or the link being
+        garbage-collected — puts the stop sentinel, so rings and links built
+        and dropped by a long process do not leave idle threads behind."""
         import queue
         import threading
-        self._sendq = queue.Queue()
+        import weakref
+        q = self._sendq = queue.Queue()
+        peer, group = self.peer, self.group
 
         def run():
             while True:
-                item = self._sendq.get()
+                item = q.get()
                 if item is None:
                     return
                 ev, host, box, done = item
                 try:
                     ev.synchronize()
-                    box.append(dist.isend(host, self.peer, group=self.group))
+                    box.append(dist.isend(host, peer, group=group))
                 except BaseException as e:  # noqa: BLE001 — re-raised by the work's wait()
                     box.append(e)
                 done.set()
-        threading.Thread(target=run, name=f"hostlink-send-{self.peer}", daemon=True).start()
+        self._thread = threading.Thread(target=run, name=f"hostlink-send-{peer}", daemon=True)
+        self._thread.start()
+        self._stop = weakref.finalize(self, q.put, None)
+
+    def close(self, timeout_s: float = 30.0) -> None:
+        """Stop the sender thread after the sends already queued are posted."""
+        if self._sendq is not None:
+            self._stop()
+            self._thread.join(timeout_s)
+            self._sendq = None
 
     def isend(self, t: torch.Tensor):
         if not t.is_contiguous():

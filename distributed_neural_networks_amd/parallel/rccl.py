@@ -46,6 +46,11 @@ INIT_TIMEOUT_S = float(os.environ.get("DNN_RCCL_INIT_TIMEOUT_S", "300"))
 _CHANNELS: Dict[Tuple[str, Tuple[int, ...]], "Channel"] = {}
 _LOCK = threading.Lock()
 _SCOPES: list = []  # open scope() frames, innermost last: keys of the channels each one opened
+# opens per (tag, rank pair) in this process.  Both ranks of a pair open (and
+# scope-close) its channel the same number of times in the same order, so the
+# count names one generation of the pair's unique id in the store: a reopen
+# never reads the id of a communicator that has already been destroyed.
+_OPENS: Dict[Tuple[str, Tuple[int, ...]], int] = {}
 
 
 def _lib():
@@ -231,16 +236,32 @@ def pair_channel(my_rank: int, peer: int, device: torch.device, tag: str = "worl
         if ch is not None and not ch.closed:
             return ch
         st = store or _store()
-        skey = f"dnn/rccl/{tag}/{ranks[0]}-{ranks[1]}"
+        gen = _OPENS.get(key, 0) + 1
+        _OPENS[key] = gen
+        skey = store_key(tag, ranks, gen)
         if my_rank == ranks[0]:
             uid = _lib().comm_unique_id()
             st.set(skey, uid)
+            if gen > 1:  # the previous generation's id is never read again
+                _delete_key(st, store_key(tag, ranks, gen - 1))
             ch = Channel(uid, 2, 0, device, key=key)
         else:  # the id is read on the init thread: opening a channel never blocks
             ch = Channel(None, 2, 1, device, key=key, uid_fn=lambda: st.get(skey))
         _CHANNELS[key] = ch
         _note_opened(key)
         return ch
+
+
+def store_key(tag: str, ranks: Tuple[int, ...], gen: int) -> str:
+    """Store key of generation ``gen`` (1 = first open) of a pair's unique id."""
+    return f"dnn/rccl/{tag}/{ranks[0]}-{ranks[1]}/{gen}"
+
+
+def _delete_key(st, k: str) -> None:
+    try:
+        st.delete_key(k)
+    except Exception:  # noqa: BLE001 — hygiene only (a store without delete keeps it)
+        pass
 
 
 def _note_opened(key) -> None:
@@ -267,7 +288,10 @@ def scope(device: Optional[torch.device] = None):
         yield frame
         ok = True
     finally:
-        _SCOPES.remove(frame)
+        # by identity: two frames that opened nothing are equal lists, and
+        # list.remove would drop the outer one and orphan this one
+        popped = _SCOPES.pop()
+        assert popped is frame, "rccl.scope frames closed out of order"
         with _LOCK:
             chans = [_CHANNELS.pop(k) for k in frame if k in _CHANNELS]
         if chans and ok:

@@ -270,11 +270,15 @@ def test_bench_pp2_schedule_cpu(n, launcher):
     launcher: bench.py must spawn the 4 ranks itself."""
     d = _bench_cpu(n, launcher=launcher)
     assert d["n_gpus"] == n and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
-    assert d["dtype"].startswith("fp32") and "bf16x3" in d["dtype"] and d["scaling"] == "weak"
+    assert d["dtype"].startswith("fp32") and "schedule test" in d["dtype"] and d["scaling"] == "weak"
     assert d["config"]["stage_cut"] == "conv|fc (reference split, 16 KiB/img hop)"
     assert d["config"]["receiver_fill_images_per_step"] == 0
     assert d["config"]["p2p"] == "gloo"  # native RCCL preflight applies to nccl runs only
-    assert d["config"]["parallelism"].startswith(f"pp2-rccl-{n // 2}x{n // 2}")
+    assert d["config"]["parallelism"].startswith(f"pp2-gloo-cpu-{n // 2}x{n // 2}")
+    # every phase's seconds, inside the run's budget
+    ph = d["phase_s"]
+    assert {"startup_s", "init_s", "headline_s", "hop_s", "fc1cut_s", "gpt2_4stage_s", "total_s"} <= set(ph), ph
+    assert ph["total_s"] < d["time_budget_s"]
     assert d["config"]["global_batch"] == (n // 2) * 16
     assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
     assert d["p50_latency_ms"] is not None and d["p50_latency_ms"] > 0

@@ -75,6 +75,7 @@ def fake_rccl(monkeypatch):
     monkeypatch.setattr(rccl, "Channel", _FakeChannel)
     monkeypatch.setattr(rccl, "_lib", lambda: _Lib)
     monkeypatch.setattr(rccl, "_CHANNELS", {})
+    monkeypatch.setattr(rccl, "_OPENS", {})
     _FakeChannel.destroyed = []
     return rccl
 
@@ -180,3 +181,57 @@ def test_preflight_pattern_distinguishes_messages():
         for j in range(i + 1, len(pats)):
             assert not torch.equal(pats[i], pats[j])
     assert int(pats[0].min()) >= 0
+
+
+def test_nested_empty_scopes_close_their_own_frames(fake_rccl):
+    """Two nested scopes that both open nothing new (equal, empty frames):
+    the inner one's exit must pop the inner frame, so a channel the outer
+    block opens afterwards is still closed by the outer scope."""
+    rccl = fake_rccl
+    dev = torch.device("cpu")
+    st = _FakeStore()
+    rccl.pair_channel(0, 1, dev, "world", store=st)  # exists before both scopes
+    base = rccl.live_channels()
+    with rccl.scope(dev):
+        with rccl.scope(dev):
+            rccl.pair_channel(0, 1, dev, "world", store=st)  # already open: nothing new
+        c = rccl.pair_channel(0, 2, dev, "world", store=st)
+    assert c.closed and rccl.live_channels() == base
+    assert rccl._SCOPES == []
+
+
+def test_reopen_uses_a_fresh_store_key(fake_rccl):
+    """Every open of a (tag, pair) publishes its id under its own generation
+    key, so a reopen never reads the id of a destroyed communicator."""
+    rccl = fake_rccl
+    dev = torch.device("cpu")
+    st = _FakeStore()
+    for _ in range(3):
+        with rccl.scope(dev):
+            rccl.pair_channel(0, 1, dev, "world", store=st)
+    gens = sorted(k for k in st.kv if k.startswith("dnn/rccl/world/0-1/"))
+    assert gens == [f"dnn/rccl/world/0-1/{g}" for g in (1, 2, 3)], gens
+
+
+def test_pair_channel_reopen_two_processes(tmp_path):
+    """Two processes on a real TCPStore open and scope-close the same pair
+    channel 5 times, the lower rank lagging before each reopen: both ends
+    must see the same unique id at every generation (before the fix the
+    higher rank read the previous, destroyed communicator's id)."""
+    import os
+    import subprocess
+    import sys
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = [tmp_path / f"r{r}.txt" for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "rccl_reopen_worker.py"), str(r), str(port),
+                               str(outs[r]), "5"]) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=120) == 0
+    u0, u1 = (o.read_text().split() for o in outs)
+    assert len(u0) == 5 and u0 == u1
+    assert len(set(u0)) == 5
