@@ -58,6 +58,10 @@ def apply(switch: str, v: int) -> None:
         gemm.set_gemm_split_tail(int(v))
     elif switch == "fused_head":  # decode head + argmax partials in one launch (gemm_head.h)
         gemm.set_fused_head(bool(v))
+    elif switch == "rowstats":  # producer-side decode row statistics (ops/gemm.py ROWSTATS)
+        gemm.ROWSTATS = bool(v)
+    elif switch == "multistep":  # K decode rounds per HIP graph (runtime/scheduler.py DecodeRing multi_step)
+        os.environ["DNN_DECODE_MULTISTEP"] = str(v)
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
         transformer_ops.ARGMAX_SPLIT = bool(v)

@@ -72,8 +72,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_head(CP(A), lda, CP(Wsh), CFP(sw), CFP(colsum), CFP(bias), eps, norm, P(C), ldc, M, N, K, w8,
                          P(part), part_cap, ST(st));
   });
-  m.def("argmax_final", [](u64 part, int S, int M, u64 out, u64 out2, u64 pos_inc, u64 st) {
-    return dnn_argmax_final(CP(part), S, M, IP(out), IP(out2), IP(pos_inc), ST(st));
+  m.def("gemm_rowstats", [](u64 out, int out_ld, u64 in, int in_ld) {
+    return dnn_gemm_rowstats(reinterpret_cast<void*>(static_cast<uintptr_t>(out)), out_ld, CP(in), in_ld);
+  });
+  m.def("gemm_rowstats_written", []() { return dnn_gemm_rowstats_written(); });
+  m.def("argmax_final", [](u64 part, int S, int M, u64 out, u64 out2, u64 pos_inc, u64 st, u64 hist, int hist_ld) {
+    return dnn_argmax_final(CP(part), S, M, IP(out), IP(out2), IP(pos_inc), ST(st), IP(hist), hist_ld);
   });
   m.def("gemm_oneshot_sweep", [](u64 A, int lda, u64 Wsh, u64 sw, u64 C, int ldc, int M, int N, int K, int mt, int ntw,
                                  int steps, int splitk, int w8, u64 ws, long long ws_bytes, u64 st) {
@@ -183,10 +187,12 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_sample_topk(CP(x), ld, M, N, reinterpret_cast<int*>(out), temperature, topk, seed,
                            reinterpret_cast<const int*>(step), ST(st));
   });
-  m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st, u64 out2, u64 pos_inc, u64 part) {
-    return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st), IP(out2), IP(pos_inc), reinterpret_cast<void*>(static_cast<uintptr_t>(part)));
+  m.def("argmax_rows", [](u64 x, int ld, int M, int N, u64 out, int f32in, u64 st, u64 out2, u64 pos_inc, u64 part,
+                          u64 hist, int hist_ld) {
+    return dnn_argmax_rows(CP(x), ld, M, N, IP(out), f32in, ST(st), IP(out2), IP(pos_inc),
+                           reinterpret_cast<void*>(static_cast<uintptr_t>(part)), IP(hist), hist_ld);
   }, py::arg("x"), py::arg("ld"), py::arg("M"), py::arg("N"), py::arg("out"), py::arg("f32in"), py::arg("st"),
-     py::arg("out2") = 0, py::arg("pos_inc") = 0, py::arg("part") = 0);
+     py::arg("out2") = 0, py::arg("pos_inc") = 0, py::arg("part") = 0, py::arg("hist") = 0, py::arg("hist_ld") = 0);
   m.def("quant_fp8_rows", [](u64 x, int ldx, u64 q, u64 scale, int M, int K, int kpad, u64 st, int split) {
     return dnn_quant_fp8_rows(CP(x), ldx, P(q), FP(scale), M, K, kpad, ST(st), split);
   }, py::arg("x"), py::arg("ldx"), py::arg("q"), py::arg("scale"), py::arg("M"), py::arg("K"), py::arg("kpad"),

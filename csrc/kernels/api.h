@@ -52,8 +52,13 @@ int dnn_gemm_set_head(int on);
 int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, const float* colsum, const float* bias,
                   float eps, int norm, void* C, int ldc, int M, int N, int K, int w8, void* part, int part_cap,
                   hipStream_t st);
-int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st);
-int dnn_gemm_set_split_tail(int on);  // prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
+// hist (optional, with pos_inc): hist[row * hist_ld + pos_inc[row]] = id before the advance (token history)
+int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st,
+                     int* hist = nullptr, int hist_ld = 0);
+int dnn_gemm_set_split_tail(int on);
+// producer-side row statistics for the next decode GEMM call of this thread (gemm_skinny.hip)
+int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld);
+int dnn_gemm_rowstats_written();  // prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);
@@ -90,7 +95,7 @@ int dnn_attn_decode(const void* q, const void* kc, const void* vc, void* o, int 
 int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, float temperature, int topk, unsigned seed,
                     const int* step, hipStream_t st);
 int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st, int* out2 = nullptr,
-                    int* pos_inc = nullptr, void* part = nullptr);
+                    int* pos_inc = nullptr, void* part = nullptr, int* hist = nullptr, int hist_ld = 0);
 int dnn_quant_fp8_rows(const void* x, int ldx, void* q, float* scale, int M, int K, int kpad, hipStream_t st,
                        int split = 0);
 int dnn_gemm_fp8(const void* A, const float* sa, const void* W, const float* sw, void* C, int ldc, const float* bias,

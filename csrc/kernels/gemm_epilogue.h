@@ -37,11 +37,14 @@ __device__ __forceinline__ f32x4 epi_norm4(f32x4 v, int m, int n, int M, int N, 
 
 //
 // Optional dequant scales (fp8 kernels): v *= rowscale * colscale[n..n+3].
+// ``stored`` (bf16 output only): receives the values as stored (bf16-rounded;
+// 0 for columns past N and rows past M), for the row-statistics producer.
 template <int ACT, bool OUT_F32>
 __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void* __restrict__ Cv, int ldc,
                                        const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
                                        bool vec, const float* __restrict__ colscale = nullptr,
-                                       float rowscale = 1.f) {
+                                       float rowscale = 1.f, f32x4* stored = nullptr) {
+  if (stored != nullptr) *stored = f32x4{0.f, 0.f, 0.f, 0.f};
   if (m >= M) return;
   if (vec && n + 3 < N) {
     if (colscale != nullptr) v *= *reinterpret_cast<const f32x4*>(colscale + n) * rowscale;
@@ -66,6 +69,9 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
       pk.x = pack2bf(v[0], v[1]);
       pk.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + n) = pk;
+      if (stored != nullptr)
+        *stored = f32x4{__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                        __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
     }
     return;
   }
@@ -78,10 +84,79 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
       if (ACT == ACT_RELU) x = fmaxf(x, 0.f);
       if (ACT == ACT_GELU) x = gelu_erf(x);
       if (R != nullptr) x += bf2f(R[(size_t)m * ldr + nn]);
-      if (OUT_F32) reinterpret_cast<float*>(Cv)[(size_t)m * ldc + nn] = x;
-      else reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + nn] = f2bf(x);
+      if (OUT_F32) {
+        reinterpret_cast<float*>(Cv)[(size_t)m * ldc + nn] = x;
+      } else {
+        const bf16_t b = f2bf(x);
+        reinterpret_cast<bf16_t*>(Cv)[(size_t)m * ldc + nn] = b;
+        if (stored != nullptr) (*stored)[r] = bf2f(b);
+      }
     }
   }
+}
+
+// Row-statistics partial of one 16-column output tile, produced in the
+// epilogue of a residual-writing decode GEMM so that the
+// next pre-norm projection merges ~N/16 partials per row instead of
+// re-deriving the statistics from its activations in every column-tile
+// workgroup.  Transposed-accumulator layout: lane (fr = l & 15, fg = l >> 4)
+// holds row m's columns n0 + 4 fg .. + 3 (``x``: the stored bf16 values, 0
+// past N).  Writes {mean, sum of squared deviations} of the tile's valid
+// columns (two-pass over registers: no cancellation whatever the row mean)
+// to rs[m * ld + n0 / 16] from lane group 0.  Every lane must call it.
+__device__ __forceinline__ void epi_rowstat16(const f32x4& x, int m, int n0, int M, int N, float2* __restrict__ rs,
+                                              int ld, int lane) {
+  const int nt = min(16, N - n0);  // >= 1: the tile starts inside the row
+  const int nv = min(4, max(0, N - n0 - 4 * (lane >> 4)));
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s += r < nv ? x[r] : 0.f;
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  const float mean = s / (float)nt;
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float d = r < nv ? x[r] - mean : 0.f;
+    q = fmaf(d, d, q);
+  }
+  q += __shfl_xor(q, 16, 64);
+  q += __shfl_xor(q, 32, 64);
+  if (lane < 16 && m < M) rs[(size_t)m * ld + (n0 >> 4)] = make_float2(mean, q);
+}
+
+// Consumer side: (mean, rstd) of row ``row`` of a K-wide activation from its
+// ceil(K/16) tile partials rs[row * ld + i] = {mean_i, M2_i} (epi_rowstat16),
+// merged by TPR adjacent lanes, each holding up to SPT partials (``p`` =
+// partials sub, sub + TPR, ...; ``p0`` = partial 0).  Shifted by partial 0's
+// mean c:  mean = c + S1 / K,  M2 = sum M2_i + S2 - S1^2 / K  with
+// S1 = sum n_i (mean_i - c), S2 = sum n_i (mean_i - c)^2 — robust for any
+// |mean| / std.  RMS (NORM 1): c = 0 and E[x^2] = (sum M2_i + S2) / K.
+template <int NORM, int TPR, int SPT>
+__device__ __forceinline__ float2 rowstat_merge(const float2 (&p)[SPT], float2 p0, int sub, int K, float eps) {
+  const int np = (K + 15) >> 4;
+  const float c = NORM == 2 ? p0.x : 0.f;
+  float s1 = 0.f, s2 = 0.f, sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < SPT; ++i) {
+    const int idx = sub + i * TPR;
+    if (idx < np) {
+      const float ni = (float)min(16, K - 16 * idx);
+      const float d = p[i].x - c;
+      s1 = fmaf(ni, d, s1);
+      s2 = fmaf(ni * d, d, s2);
+      sm += p[i].y;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+    sm += __shfl_xor(sm, o, 64);
+  }
+  const float invk = 1.f / (float)K;
+  const float var = NORM == 2 ? fmaxf((sm + s2 - s1 * s1 * invk) * invk, 0.f) : (sm + s2) * invk;
+  return make_float2(NORM == 2 ? c + s1 * invk : 0.f, rsqrtf(var + eps));
 }
 
 // Widened bf16 store for two horizontally adjacent 16x16 transposed tiles

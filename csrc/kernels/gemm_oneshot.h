@@ -49,6 +49,7 @@
 namespace dnn {
 
 constexpr int OS_SB = 512;  // A bytes per row per LDS step (bf16: 8 chunks of 32 k; W8: 4 chunks of 64 k)
+constexpr int OS_RS_SPT = 16;  // producer row-statistics partials per thread (consumer merge)
 
 template <int MT, int STEPS>
 constexpr int os_lds_bytes() {
@@ -63,7 +64,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
                                                               const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                               int nch, int cps, const float* __restrict__ colsum,
                                                               float eps, int kelems, float* __restrict__ slab,
-                                                              int ntiles, int mgroups) {
+                                                              int ntiles, int mgroups,
+                                                              float2* __restrict__ rs_out = nullptr, int rs_ld = 0,
+                                                              const float2* __restrict__ rs_in = nullptr,
+                                                              int rs_ld_in = 0) {
   using Cfg = StrCfg<W8>;
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
@@ -93,14 +97,29 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 
   char* img = os_lds + wave * IMG;
   const int fr = lane & 15, fg = lane >> 4;
+  // producer-side row statistics (rs_in, no SPLIT; host: ceil(K/16) <= OS_RS_SPT
+  // x TPR): the partials of the workgroup's rows are loaded first of all, so
+  // the explicit vmcnt waits below (which count only the weights) cover them
+  constexpr int TPR = 256 / MP, SPT = OS_RS_SPT;
+  const bool rsi = NORM != 0 && !SPLIT && rs_in != nullptr;  // uniform
+  float2 rsp[SPT], rs0 = make_float2(0.f, 0.f);
+  if (rsi) {
+    const float2* p = rs_in + (size_t)min(m0 + tid / TPR, M - 1) * rs_ld_in;
+    const int np = (kelems + 15) >> 4, sub = tid % TPR;
+    rs0 = p[0];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) rsp[i] = p[min(sub + i * TPR, np - 1)];
+  }
   float shift[MT], s1s[MT], s2s[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     shift[t] = 0.f;
     s1s[t] = s2s[t] = 0.f;
     if constexpr (NORM == 2) {
-      const int row = min(m0 + 16 * t + fr, M - 1);
-      shift[t] = bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)row * lda_b));
+      if (!rsi) {
+        const int row = min(m0 + 16 * t + fr, M - 1);
+        shift[t] = bf2f(*reinterpret_cast<const bf16_t*>(A + (size_t)row * lda_b));
+      }
     }
   }
   // ---- issue: every A row segment of the wave's range by LDS-DMA (full
@@ -141,7 +160,18 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 
   // ---- row statistics of this wave's K range from its image (the 4 lane
   // groups hold disjoint k), while the weight loads are outstanding
-  if constexpr (NORM != 0) {
+  if (rsi) {
+    // merge the producer's partials instead (they and the image were issued
+    // before the weights): mean / rstd of row tid / TPR into LDS
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const float2 mr = rowstat_merge<NORM, TPR, SPT>(rsp, rs0, tid % TPR, kelems, eps);
+    if (tid % TPR == 0) {
+      st_lds[(tid / TPR) * 2 + 0] = mr.x;
+      st_lds[(tid / TPR) * 2 + 1] = mr.y;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  } else if constexpr (NORM != 0) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");  // the image (issued first)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -226,7 +256,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   }
 
   // ---- row statistics of this wave's K range: the 4 lane groups hold disjoint k
-  if constexpr (NORM != 0) {
+  if (NORM != 0 && !rsi) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       float a = s1s[t], q = s2s[t];
@@ -263,10 +293,12 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     const int n = nb + fg * 4;
     float a = 0.f, q2 = 0.f;
     if constexpr (NORM != 0) {
+      if (!rsi) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        a += st_lds[((w * MT + t) * 2 + 0) * 16 + fr];
-        q2 += st_lds[((w * MT + t) * 2 + 1) * 16 + fr];
+        for (int w = 0; w < 4; ++w) {
+          a += st_lds[((w * MT + t) * 2 + 0) * 16 + fr];
+          q2 += st_lds[((w * MT + t) * 2 + 1) * 16 + fr];
+        }
       }
     }
     if constexpr (SPLIT) {
@@ -287,9 +319,13 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       }
       if constexpr (NORM != 0) {
         const float invk = 1.f / (float)kelems, d = a * invk;
-        const float mean = NORM == 2 ? shift[t] + d : 0.f;
+        float mean = NORM == 2 ? shift[t] + d : 0.f;
         const float var = NORM == 2 ? fmaxf(q2 * invk - d * d, 0.f) : q2 * invk;
-        const float rstd = rsqrtf(var + eps);
+        float rstd = rsqrtf(var + eps);
+        if (rsi) {
+          mean = st_lds[ml * 2 + 0];
+          rstd = st_lds[ml * 2 + 1];
+        }
         if constexpr (NORM == 2) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = rstd * (v[r] - mean * (n + r < N ? colsum[n + r] : 0.f));
@@ -300,6 +336,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
       if constexpr (ACT == ACT_SILU_MUL) {
         epi_silu_t4<false>(v, m, nb / 2, M, N / 2, Cv, ldc, vec, lane);
+      } else if (rs_out != nullptr) {  // uniform: row-statistics partials of the stored tile
+        f32x4 x;
+        epi_t4<ACT, false>(v, m, n, M, N, Cv, ldc, bias, R, ldr, vec, nullptr, 1.f, &x);
+        epi_rowstat16(x, m, nb, M, N, rs_out, rs_ld, lane);
       } else {
         epi_t4<ACT, false>(v, m, n, M, N, Cv, ldc, bias, R, ldr, vec);
       }

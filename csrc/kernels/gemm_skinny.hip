@@ -103,7 +103,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
                                                            const float* __restrict__ bias,
                                                            const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                            int kbytes, const float* __restrict__ colsum = nullptr,
-                                                           float eps = 0.f, const uint8_t* __restrict__ Wsh = nullptr) {
+                                                           float eps = 0.f, const uint8_t* __restrict__ Wsh = nullptr,
+                                                           float2* __restrict__ rs_out = nullptr, int rs_ld = 0) {
   static_assert(NORM == NORM_NONE || !FP8, "fused norm needs bf16 activations");
   static_assert(!(FP8 && W8), "W8 = fp8 weights with bf16 activations; FP8 = both fp8");
   constexpr int AU = W8 ? 2 : 1;        // 16-B A loads per chunk per M tile (W8: a chunk is 64 k = 128 B of A)
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     if (sa != nullptr) sa += mo;
     Cv = reinterpret_cast<char*>(Cv) + (size_t)mo * ldc * (OUT_F32 ? 4 : 2);
     if (R != nullptr) R += (size_t)mo * ldr;
+    if (rs_out != nullptr) rs_out += (size_t)mo * rs_ld;
     M = min(16, M - mo);
   } else {
     n0 = blockIdx.x * (16 * NT);
@@ -349,6 +351,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
         }
         epi_silu_t4<OUT_F32>(s[j], m, (n0 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
       }
+    } else if (!OUT_F32 && !FP8 && rs_out != nullptr) {  // uniform: row-statistics partials of the stored tiles
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        f32x4 x;
+        epi_t4<ACT, OUT_F32>(s[j], m, n0 + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr, vec, nullptr, rs,
+                             &x);
+        epi_rowstat16(x, m, n0 + j * 16, M, N, rs_out, rs_ld, lane);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
@@ -363,6 +373,40 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 using namespace dnn;
 
 constexpr int SKINNY_MAX_M = 256;  // M > 64 only through the M split (medium-batch decode)
+
+// Producer-side row statistics (gemm_epilogue.h
+// epi_rowstat16 / rowstat_merge): dnn_gemm_rowstats() arms the NEXT decode
+// GEMM call of this thread — ``out`` (float2 [M][ld], ld >= ceil(N/16)): the
+// call's kernel writes per-16-column-tile partials of its bf16 output rows;
+// ``in``: the partials of the call's input rows, merged instead of deriving
+// the pre-norm statistics from the activations.  The request is consumed by
+// that call whatever runs; dnn_gemm_rowstats_written() reports whether its
+// kernel wrote ``out`` (the one-shot and skinny kernels do; the stream /
+// split-K paths do not, and their consumer then derives its own).
+struct RowStatReq {
+  float2* out = nullptr;
+  int out_ld = 0;
+  const float2* in = nullptr;
+  int in_ld = 0;
+};
+static thread_local RowStatReq g_rs_req, g_rs_cur;
+static thread_local int g_rs_written = 0;
+
+extern "C" int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld) {
+  g_rs_req.out = reinterpret_cast<float2*>(out);
+  g_rs_req.out_ld = out_ld;
+  g_rs_req.in = reinterpret_cast<const float2*>(in);
+  g_rs_req.in_ld = in_ld;
+  g_rs_written = 0;
+  return 0;
+}
+
+// Whether the armed call's kernel wrote the partials; also drops a request no
+// decode GEMM consumed (a call that took the prefill path).
+extern "C" int dnn_gemm_rowstats_written() {
+  g_rs_req = RowStatReq{};
+  return g_rs_written;
+}
 
 // ---- stream kernel dispatch (gemm_stream.h): 17..64 rows, fragment-order
 // weights of >= g_stream_min_bytes; narrow N splits K across workgroups into
@@ -531,9 +575,15 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
   const dim3 grid(ntiles * mgroups * splitk), block(256);
   const size_t smem = os_lds_bytes<MT, STEPS>();
   if (splitk == 1) {
+    // row statistics: partials of the output (not for the half-width SwiGLU
+    // output); merged partials of the input when they fit OS_RS_SPT per thread
+    float2* rso = ACT != ACT_SILU_MUL ? g_rs_cur.out : nullptr;
+    const float2* rsi = (NORM != 0 && (kelems + 15) / 16 <= OS_RS_SPT * (256 / MP)) ? g_rs_cur.in : nullptr;
     hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS>), grid, block, smem, st,
                        (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N,
-                       nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups);
+                       nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups, rso, g_rs_cur.out_ld, rsi,
+                       g_rs_cur.in_ld);
+    if (rso != nullptr) g_rs_written = 1;
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, true, STEPS>), grid, block, smem, st,
@@ -639,9 +689,11 @@ static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const vo
   while (ks > 1 && kbytes / 64 < ks) ks >>= 1;
   size_t smem = (size_t)ks * NT * MT * 64 * sizeof(f32x4);
   if (NORM != NORM_NONE) smem += (size_t)ks * MT * 2 * 16 * sizeof(float);
+  float2* rso = (!F32 && !FP8 && ACT != ACT_SILU_MUL) ? g_rs_cur.out : nullptr;
   hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8, MS>), dim3(groups), dim3(64 * ks), smem,
                      st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
-                     ldr, M, N, kbytes, colsum, eps, (const uint8_t*)Wsh);
+                     ldr, M, N, kbytes, colsum, eps, (const uint8_t*)Wsh, rso, g_rs_cur.out_ld);
+  if (rso != nullptr) g_rs_written = 1;
   return (int)hipGetLastError();
 }
 
@@ -650,6 +702,14 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
                          void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
                          hipStream_t st, const float* colsum = nullptr, float eps = 0.f,
                          const void* Wsh = nullptr, void* ws = nullptr, long long ws_bytes = 0) {
+  // this call consumes the row-statistics request (dnn_gemm_rowstats); it is
+  // in effect for this call's launch only
+  struct Scope {
+    ~Scope() { g_rs_cur = RowStatReq{}; }
+  } scope;
+  g_rs_cur = g_rs_req;
+  g_rs_req = RowStatReq{};
+  g_rs_written = 0;
   if constexpr (!F32 && !FP8 && ACT != ACT_RELU) {
     OsCfg oc;
     if (os_eligible<ACT, NORM, W8>(A, lda_b, Wsh, M, kbytes) && os_plan<W8>(M, N, kbytes, ws != nullptr, ws_bytes, oc))

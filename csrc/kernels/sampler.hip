@@ -16,10 +16,26 @@ __device__ __forceinline__ void argmax_merge(float& best, int& bi, float v, int 
   if (v > best || (v == best && i < bi)) { best = v; bi = i; }
 }
 
+// Token history (multi-step decode graphs): `hist[row * hist_ld + pos]` gets
+// the sampled id at the row's position before the advance, so K decode steps
+// replayed as one graph leave every step's token in device memory (no host
+// bookkeeping per step); positions outside [0, hist_ld) are not written.
+__device__ __forceinline__ void step_tail(int row, int bi, int* out, int* out2, int* pos_inc, int* hist,
+                                          int hist_ld) {
+  out[row] = bi;
+  if (out2 != nullptr) out2[row] = bi;
+  if (pos_inc != nullptr) {
+    const int p = pos_inc[row];
+    if (hist != nullptr && p >= 0 && p < hist_ld) hist[(size_t)row * hist_ld + p] = bi;
+    pos_inc[row] = p + 1;
+  }
+}
+
 template <bool F32, int TH, int NV>
 __global__ __launch_bounds__(TH) void argmax_rows_kernel(const void* __restrict__ xv, int ld, int M, int N,
                                                          int* __restrict__ out, int* __restrict__ out2,
-                                                         int* __restrict__ pos_inc) {
+                                                         int* __restrict__ pos_inc, int* __restrict__ hist,
+                                                         int hist_ld) {
   const int row = blockIdx.x;
   if (row >= M) return;
   float best = -INFINITY;
@@ -65,9 +81,7 @@ __global__ __launch_bounds__(TH) void argmax_rows_kernel(const void* __restrict_
   if (threadIdx.x == 0) {
     for (int w = 1; w < TH / 64; ++w) argmax_merge(best, bi, sv[w], si[w]);
     bi = bi == 0x7fffffff ? 0 : bi;  // all-NaN row: token 0
-    out[row] = bi;
-    if (out2 != nullptr) out2[row] = bi;
-    if (pos_inc != nullptr) pos_inc[row] += 1;
+    step_tail(row, bi, out, out2, pos_inc, hist, hist_ld);
   }
 }
 
@@ -125,7 +139,8 @@ __global__ __launch_bounds__(256) void argmax_part_kernel(const bf16_t* __restri
 
 __global__ __launch_bounds__(256) void argmax_final_kernel(const int2* __restrict__ part, int S, int M,
                                                            int* __restrict__ out, int* __restrict__ out2,
-                                                           int* __restrict__ pos_inc) {
+                                                           int* __restrict__ pos_inc, int* __restrict__ hist,
+                                                           int hist_ld) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -143,9 +158,7 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(const int2* __restric
   }
   if (lane == 0) {
     bi = bi == 0x7fffffff ? 0 : bi;  // all-NaN row: token 0
-    out[row] = bi;
-    if (out2 != nullptr) out2[row] = bi;
-    if (pos_inc != nullptr) pos_inc[row] += 1;
+    step_tail(row, bi, out, out2, pos_inc, hist, hist_ld);
   }
 }
 
@@ -288,20 +301,23 @@ extern "C" int dnn_sample_topk(const void* x, int ld, int M, int N, int* out, fl
 // The second pass of a row-split argmax whose partials another kernel wrote
 // (part[row * S + s]; gemm_head.h writes one per workgroup), with the decode
 // step tail.
-extern "C" int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st) {
+extern "C" int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st,
+                                int* hist, int hist_ld) {
   if (M <= 0) return 0;
   if (S <= 0 || part == nullptr) return -1;
+  if (hist != nullptr && (pos_inc == nullptr || hist_ld <= 0)) return -1;
   hipLaunchKernelGGL(argmax_final_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const int2*)part, S, M, out, out2,
-                     pos_inc);
+                     pos_inc, hist, hist_ld);
   return (int)hipGetLastError();
 }
 
 // part (optional, >= M * 64 int2): workspace of the row-split path (bf16 rows,
 // fewer than 512 rows x segments otherwise); nullptr = one workgroup per row.
 extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, int f32in, hipStream_t st,
-                               int* out2, int* pos_inc, void* part) {
+                               int* out2, int* pos_inc, void* part, int* hist, int hist_ld) {
   if (M <= 0) return 0;
   if (!f32in && (ld % 8) != 0) return -1;
+  if (hist != nullptr && (pos_inc == nullptr || hist_ld <= 0)) return -1;
   if (!f32in && part != nullptr && M < 256) {
     // segments per row: ~512 workgroups in all, >= 2048 entries per segment
     int S = (512 + M - 1) / M;
@@ -320,19 +336,20 @@ extern "C" int dnn_argmax_rows(const void* x, int ld, int M, int N, int* out, in
                            (int2*)part);
       }
       hipLaunchKernelGGL(argmax_final_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const int2*)part, S, M, out, out2,
-                         pos_inc);
+                         pos_inc, hist, hist_ld);
       return (int)hipGetLastError();
     }
   }
   if (f32in) {
-    hipLaunchKernelGGL((argmax_rows_kernel<true, 256, 1>), dim3(M), dim3(256), 0, st, x, ld, M, N, out, out2, pos_inc);
+    hipLaunchKernelGGL((argmax_rows_kernel<true, 256, 1>), dim3(M), dim3(256), 0, st, x, ld, M, N, out, out2, pos_inc,
+                       hist, hist_ld);
   } else if (M <= 16) {
     // few rows: a wide workgroup per row (Llama-3 128K vocabulary: 16 loads per lane)
     hipLaunchKernelGGL((argmax_rows_kernel<false, 1024, 16>), dim3(M), dim3(1024), 0, st, x, ld, M, N, out, out2,
-                       pos_inc);
+                       pos_inc, hist, hist_ld);
   } else {
     hipLaunchKernelGGL((argmax_rows_kernel<false, 256, 8>), dim3(M), dim3(256), 0, st, x, ld, M, N, out, out2,
-                       pos_inc);
+                       pos_inc, hist, hist_ld);
   }
   return (int)hipGetLastError();
 }

@@ -125,10 +125,13 @@ def set_fp8_tile(tile: int = 0) -> None:
 def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, norm: int = 0,
               colsum: Optional[torch.Tensor] = None, eps: float = 0.0,
-              ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+              ws: Optional[torch.Tensor] = None, rs_out: Optional[torch.Tensor] = None,
+              rs_in: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight-only fp8 GEMM for decode-sized M (<= 256): bf16 x (M, K) times e4m3 w, bf16 out.
     ``norm`` (1 RMS / 2 LN, with ``colsum`` for LN) fuses a folded pre-norm.
-    ``ws``: ``gemm.decode_workspace`` (split-K partials of the decode stream GEMM)."""
+    ``ws``: ``gemm.decode_workspace`` (split-K partials of the decode stream GEMM).
+    ``rs_out`` / ``rs_in``: producer-side row statistics (``gemm.linear``,
+    ``gemm.linear_norm``)."""
     M, K = x.shape
     N, kp = w.q.shape
     if M > 256 or (w.k and w.k != K) or kp < K or K % 64:
@@ -143,7 +146,10 @@ def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None
     if w.shuf is not None and w.shuf.numel() != -(-N // 16) * 16 * K:
         raise ValueError("linear_w8: shuf is not shuffle_weight(w.q[:, :K])")
     wsp, wsb = (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
+    from .gemm import _LAST_RS, _RowStats
+    rs = _RowStats(rs_out, rs_in, M)
     check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0), ptr(bias),
                                ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, act, norm,
                                ptr(colsum), eps, stream_ptr(), ptr(w.shuf), wsp, wsb), "gemm_skinny_w8")
+    _LAST_RS[0] = rs.done()
     return out

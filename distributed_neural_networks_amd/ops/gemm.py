@@ -75,6 +75,48 @@ def set_oneshot_gemm(on: int = 1, mt: int = 0, ntw: int = 0, steps: int = 0, spl
     check(lib().gemm_set_oneshot(int(on), int(mt), int(ntw), int(steps), int(splitk)), "gemm_set_oneshot")
 
 
+ROWSTATS = True  # producer-side decode row statistics (A/B switch; runtime/transformer.py)
+
+
+def rowstats_buffer(rows: int, width: int, device) -> torch.Tensor:
+    """Row-statistics partials of ``rows`` activation rows of ``width``
+    columns: one {mean, M2} float2 per 16-column tile (gemm_epilogue.h
+    epi_rowstat16), as fp32 (rows, 2 ceil(width / 16))."""
+    return torch.zeros((rows, 2 * -(-width // 16)), dtype=torch.float32, device=device)
+
+
+class _RowStats:
+    """Arms the next decode GEMM call with row-statistics buffers
+    (gemm_skinny.hip ``dnn_gemm_rowstats``): ``out`` receives the partials of
+    the call's output rows, ``inp`` holds those of its input rows (merged
+    instead of re-deriving a folded pre-norm's statistics).  ``written`` after
+    the call: whether its kernel wrote ``out``."""
+
+    def __init__(self, out: Optional[torch.Tensor], inp: Optional[torch.Tensor], M: int):
+        for t, nm in ((out, "rs_out"), (inp, "rs_in")):
+            if t is not None and (t.dtype != torch.float32 or t.dim() != 2 or t.shape[0] < M or t.stride(1) != 1
+                                  or t.stride(0) % 2):
+                raise ValueError(f"{nm}: fp32 (>= {M}, 2P) row-statistics buffer expected")
+        self.active = out is not None or inp is not None
+        self.written = False
+        if self.active:
+            lib().gemm_rowstats(ptr(out), 0 if out is None else out.stride(0) // 2, ptr(inp),
+                                0 if inp is None else inp.stride(0) // 2)
+
+    def done(self) -> bool:
+        if self.active:
+            self.written = bool(lib().gemm_rowstats_written())
+        return self.written
+
+
+_LAST_RS = [False]
+
+
+def rowstats_written() -> bool:
+    """Whether the last ``rs_out=`` call's kernel wrote the row statistics."""
+    return _LAST_RS[0]
+
+
 def _ws_args(ws: Optional[torch.Tensor]):
     return (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
 
@@ -83,8 +125,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_dtype: torch.dtype = torch.bfloat16, w_shuf: Optional[torch.Tensor] = None,
            rowstat: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
-           ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+           ws: Optional[torch.Tensor] = None, rs_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``w_shuf``: ``shuffle_weight(w)``, streamed instead of ``w`` on the skinny path (``skinny_rows``).
+    ``rs_out`` (decode): row-statistics partials of the output (``rowstats_buffer``);
+    ``rowstats_written()`` tells whether the kernel that ran wrote them.
     ``ws``: ``decode_workspace`` for the decode stream GEMM's split-K partials.
     ``rowstat`` ((M, 2) fp32 from ``transformer_ops.row_stats``) / ``colsum``: a
     folded pre-norm applied in the epilogue, ``rstd (x W^T) - mean rstd colsum``
@@ -118,10 +162,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if colsum is not None and (rowstat is None or colsum.dtype != torch.float32 or colsum.numel() < N):
         raise ValueError("linear: colsum needs rowstat and N fp32 entries")
     wsp, wsb = _ws_args(ws)
+    rs = _RowStats(rs_out, None, M)
     check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
                           ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
                           1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf), ptr(rowstat),
                           ptr(colsum), wsp, wsb), "gemm_bf16")
+    _LAST_RS[0] = rs.done()
     return out
 
 
@@ -208,8 +254,11 @@ def fold_norm(w: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor]
 def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, std_buf: Optional[torch.Tensor] = None,
                 ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
-                s8: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  Decode-sized M (<= 64):
+                s8: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                rs_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  ``rs_in`` (decode):
+    the row-statistics partials of ``x`` written by its producer (``linear(...,
+    rs_out=)``), merged instead of deriving the statistics from ``x``.  Decode-sized M (<= 64):
     one skinny-GEMM launch that accumulates the row statistics from the A
     fragments it streams (bf16 weights, or e4m3 weights converted in registers).
     Larger M: the norm kernel standardises x into ``std_buf`` (gamma = ``ones``,
@@ -246,7 +295,7 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         xs = layernorm(x, ones, None, std_buf[:M], f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
         return linear(xs[:M], f.w, f.bias, a, residual, out)
     if w8:
-        return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps, ws=ws)
+        return linear_w8(x, f.w, f.bias, a, residual, out, f.norm, f.colsum, f.eps, ws=ws, rs_in=rs_in)
     if K % 32:
         raise ValueError(f"linear_norm: K={K} must be a multiple of 32")
     Nout = N // 2 if a == ACT_SILU_MUL else N
@@ -259,9 +308,11 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
     if f.ws is not None and f.ws.numel() != -(-N // 16) * 16 * K * 2:
         raise ValueError("linear_norm: ws is not shuffle_weight(w)")
     wsp, wsb = _ws_args(ws)
+    rs = _RowStats(None, rs_in, M)
     check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0), ptr(f.bias),
                                  ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, a, f.norm,
                                  ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws), wsp, wsb), "gemm_skinny_norm")
+    rs.done()
     return out
 
 QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)
@@ -324,12 +375,14 @@ def set_fused_head(on: bool = True) -> None:
 
 
 def head_argmax(x: torch.Tensor, f: FoldedLinear, logits: torch.Tensor, part: torch.Tensor, out: torch.Tensor,
-                also: Optional[torch.Tensor] = None, advance: Optional[torch.Tensor] = None) -> bool:
+                also: Optional[torch.Tensor] = None, advance: Optional[torch.Tensor] = None,
+                hist: Optional[torch.Tensor] = None) -> bool:
     """Greedy decode head (gemm_head.h): ``logits = linear(norm(x), W)`` for a
     folded-norm head with a fragment-order copy (bf16 or W8A16), and the
     argmax of every row in the same pass — each workgroup writes its winner
     per row to ``part``, a merge launch (``argmax_final``) writes ``out`` and
-    the decode step tail (``also`` = copy of the ids, ``advance += 1``).
+    the decode step tail (``also`` = copy of the ids, ``hist[row, advance]``
+    = the id, ``advance += 1``).
     Returns False with nothing launched where it does not apply (more than 64
     rows, a width without an instantiated config, a vocabulary over two
     column tiles per wave): the caller then runs the GEMM and argmax_rows."""
@@ -349,6 +402,8 @@ def head_argmax(x: torch.Tensor, f: FoldedLinear, logits: torch.Tensor, part: to
     for t, nm in ((out, "out"), (also, "also"), (advance, "advance")):
         if t is not None and (t.dtype != torch.int32 or t.numel() < M or not t.is_contiguous()):
             raise ValueError(f"head_argmax: {nm} must be contiguous int32 with >= {M} entries")
+    from .transformer_ops import check_hist
+    hist_ld = check_hist(hist, advance, M, "head_argmax")
     S = lib().gemm_head(ptr(x), x.stride(0), ptr(wsh), ptr(f.w.scale) if w8 else 0, ptr(f.colsum), ptr(f.bias),
                         f.eps, f.norm, ptr(logits), logits.stride(0), M, N, K, 1 if w8 else 0, ptr(part),
                         HEAD_PART_PER_ROW, stream_ptr())
@@ -356,7 +411,8 @@ def head_argmax(x: torch.Tensor, f: FoldedLinear, logits: torch.Tensor, part: to
         return False
     if S <= 0:
         raise RuntimeError(f"gemm_head failed ({S})")
-    check(lib().argmax_final(ptr(part), S, M, ptr(out), ptr(also), ptr(advance), stream_ptr()), "argmax_final")
+    check(lib().argmax_final(ptr(part), S, M, ptr(out), ptr(also), ptr(advance), stream_ptr(), ptr(hist), hist_ld),
+          "argmax_final")
     return True
 
 

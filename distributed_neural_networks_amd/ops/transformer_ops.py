@@ -214,24 +214,39 @@ ARGMAX_PART_PER_ROW = 64  # int2 partials per row of the row-split argmax worksp
 ARGMAX_SPLIT = True  # use the workspace when one is given (A/B switch, bench/probes/decode_ab.py)
 
 
+def check_hist(hist: Optional[torch.Tensor], advance: Optional[torch.Tensor], M: int, who: str) -> int:
+    """Token-history buffer of the decode step tail: (>= M, L) int32, rows
+    contiguous; needs ``advance`` (the positions it is indexed by).  Returns L."""
+    if hist is None:
+        return 0
+    if advance is None:
+        raise ValueError(f"{who}: hist needs advance (the positions)")
+    if hist.dtype != torch.int32 or hist.dim() != 2 or hist.shape[0] < M or hist.stride(1) != 1:
+        raise ValueError(f"{who}: hist must be int32 (>= {M}, L) with contiguous rows")
+    return hist.stride(0)
+
+
 def argmax_rows(x: torch.Tensor, out: torch.Tensor, n: Optional[int] = None, also: Optional[torch.Tensor] = None,
-                advance: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None) -> torch.Tensor:
+                advance: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None,
+                hist: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-row argmax (ties -> smallest index) into ``out`` (int32).  Decode
-    step tail in the same launch: ``also`` receives a copy of the ids and
-    ``advance[row] += 1`` (int32 positions).  ``part`` (int32, >= 128 M
-    entries): workspace that lets small batches split each row over many
-    workgroups (a partial and a merge launch, sampler.hip)."""
+    step tail in the same launch: ``also`` receives a copy of the ids,
+    ``hist[row, advance[row]]`` the id (token history of a multi-step decode
+    graph) and ``advance[row] += 1`` (int32 positions).  ``part`` (int32, >=
+    128 M entries): workspace that lets small batches split each row over
+    many workgroups (a partial and a merge launch, sampler.hip)."""
     M = x.shape[0]
     N = n if n is not None else x.shape[1]
     for t, nm in ((out, "out"), (also, "also"), (advance, "advance")):
         if t is not None and (t.dtype != torch.int32 or t.numel() < M or not t.is_contiguous()):
             raise ValueError(f"argmax_rows: {nm} must be contiguous int32 with >= {M} entries")
+    hist_ld = check_hist(hist, advance, M, "argmax_rows")
     if part is not None and (part.dtype != torch.int32 or part.numel() < 2 * ARGMAX_PART_PER_ROW * M
                              or not part.is_contiguous()):
         raise ValueError(f"argmax_rows: part must be contiguous int32 with >= {2 * ARGMAX_PART_PER_ROW * M} entries")
     check(lib().argmax_rows(ptr(x), x.stride(0), M, N, ptr(out), 1 if x.dtype == torch.float32 else 0,
-                            stream_ptr(), ptr(also), ptr(advance), ptr(part if ARGMAX_SPLIT else None)),
-          "argmax_rows")
+                            stream_ptr(), ptr(also), ptr(advance), ptr(part if ARGMAX_SPLIT else None), ptr(hist),
+                            hist_ld), "argmax_rows")
     return out
 
 

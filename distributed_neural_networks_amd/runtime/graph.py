@@ -16,7 +16,11 @@ import torch
 
 class GraphedStep:
     def __init__(self, fn: Callable[[], object], device: Optional[torch.device] = None, warmup: int = 2,
-                 pool=None):
+                 pool=None, reset: Optional[Callable[[], None]] = None):
+        """``reset`` (optional) runs on the capture stream after the warmup
+        runs and before the capture: state the warmup advanced (decode
+        positions, input ids) is put back, so the captured run starts where
+        the caller's state was."""
         self.fn = fn
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.graph = torch.cuda.CUDAGraph()
@@ -25,6 +29,8 @@ class GraphedStep:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.result = fn()
+            if reset is not None:
+                reset()
             s.synchronize()
             # thread-local capture: ProcessGroupNCCL's watchdog thread keeps
             # polling its events while a multi-GPU rank captures its decode step

@@ -305,14 +305,25 @@ class DecodeRing:
     """
 
     def __init__(self, stages: Sequence, links: RingLinks, n_groups: int, M: int, B: int,
-                 use_graphs: bool = True, record: bool = True, progress: Progress = None, lanes: int = 0):
+                 use_graphs: bool = True, record: bool = True, progress: Progress = None, lanes: int = 0,
+                 multi_step: int = -1):
         """``lanes`` (one group, M > 1, GPU): the M microbatch steps of a round
         replay on this many HIP streams (0 = one stream, -1 = min(M, 4));
         scratch rows follow the KV rows (``TransformerStage.step``), so
         concurrent microbatches share no buffer.  Off by default: measured on
         GPT-2 4-stage (profiles/archive/r2_decode_lanes_gpt2.jsonl) concurrent small
         microbatches beat the same microbatches on one stream (16 x 4: 2.17 ->
-        0.88 ms/round) but not one large batch (64 x 1: 0.60 ms)."""
+        0.88 ms/round) but not one large batch (64 x 1: 0.60 ms).
+
+        ``multi_step`` (one group, GPU, graphs, no lanes): K >= 2 decode rounds
+        of all M microbatches are also captured as ONE HIP graph, and
+        ``decode_rounds`` replays it while K or more rounds remain (single-step
+        graphs for the rest): the graph-to-graph boundary after every step's
+        argmax (profiles/r4_gpt2_b64_decode_gaps.md) is paid once per K steps.
+        Positions and input ids live on the device; a greedy last stage writes
+        each step's token into a device history (``hist``, indexed by
+        position) in its argmax launch, so recording costs nothing per step.
+        -1 = ``$DNN_DECODE_MULTISTEP`` or 8; 0 / 1 = off."""
         self.stages = list(stages)
         self.links = links
         self.G, self.M, self.B = n_groups, M, B
@@ -354,6 +365,18 @@ class DecodeRing:
         n_lanes = min(M, 4) if lanes < 0 else min(M, lanes)
         self.lanes = ([torch.cuda.Stream(dev) for _ in range(n_lanes)]
                       if n_groups == 1 and n_lanes > 1 and dev.type == "cuda" else [])
+        import os
+        self.multi_step = int(os.environ.get("DNN_DECODE_MULTISTEP", "8")) if multi_step < 0 else multi_step
+        self.graph_k = None  # the K-round graph (capture)
+        self.graph_k_steps = 0
+        # device token history (one group, greedy fused tail): hist[m][b, p] =
+        # the token sampled at position p; tokens() reads it past the prefill
+        tail = self.last and getattr(self.stages[-1], "fuses_step_tail", False)
+        cap = min((getattr(s, "max_seq", 0) for s in self.stages), default=0)
+        self.hist = ([torch.zeros((B, cap), dtype=torch.int32, device=dev) for _ in range(M)]
+                     if n_groups == 1 and tail and cap > 0 and dev.type == "cuda" else None)
+        self.hist_base = [0] * M  # position of the first decode token of the current generation
+        self.hist_n = [0] * M  # decode tokens recorded in hist since then
 
     # -- one microbatch through this rank's stages --------------------------
     def _run(self, x, m: int, T: int, out=None, advance=None):
@@ -372,7 +395,8 @@ class DecodeRing:
         # (one group) and advances the positions — no separate copy / add kernels
         if self.last and getattr(self.stages[-1], "fuses_step_tail", False):
             ids = self.cur[m].view(self.B) if self.G == 1 else None
-            self._run(x, m, 1, out=self.out[m], advance=(ids, self.pos[m]))
+            adv = (ids, self.pos[m]) if self.hist is None else (ids, self.pos[m], self.hist[m])
+            self._run(x, m, 1, out=self.out[m], advance=adv)
             return None
         self._run(x, m, 1, out=self.out[m])
         self.pos[m].add_(1)
@@ -493,6 +517,7 @@ class DecodeRing:
                         self.cur[m].copy_(self.out[m].view(B, 1))
                         if self.record:
                             self.toks[m].append(self.out[m].clone())
+                            self.hist_base[m], self.hist_n[m] = T, 0
                     else:
                         self._send(m)
                 self.progress()
@@ -518,6 +543,35 @@ class DecodeRing:
             if cur is not None:
                 self.cur[m].copy_(cur)
         torch.cuda.synchronize(self.dev)
+        self._capture_multi_step()
+
+    def _capture_multi_step(self) -> None:
+        K = self.multi_step
+        if (K < 2 or self.G != 1 or self.lanes or not self.graphs or (self.record and self.hist is None)):
+            return
+        # the warmup and the capture each write K positions past the current
+        # one into the KV caches: only when they fit
+        cap = min(getattr(s, "max_seq", 1 << 30) for s in self.stages)
+        if int(max(int(p.max().item()) for p in self.pos)) + K > cap:
+            return
+        from .graph import GraphedStep
+        snap = [p.clone() for p in self.pos]
+        cur = [c.clone() for c in self.cur] if self.first else None
+
+        def body():
+            for _ in range(K):
+                for m in range(self.M):
+                    self._decode_body(m)
+
+        def reset():
+            for m in range(self.M):
+                self.pos[m].copy_(snap[m])
+                if cur is not None:
+                    self.cur[m].copy_(cur[m])
+        self.graph_k = GraphedStep(body, self.dev, warmup=1, reset=reset)
+        self.graph_k_steps = K
+        reset()  # the capture run advanced them again
+        torch.cuda.synchronize(self.dev)
 
     def decode_round(self, mbs: Optional[Sequence[int]] = None) -> None:
         """Every microbatch (or those in ``mbs``; every rank must pass the same
@@ -539,6 +593,18 @@ class DecodeRing:
             for _ in range(n):
                 self._decode_round_lanes()
             return
+        if self.graph_k is not None and mbs is None:
+            K = self.graph_k_steps
+            while n >= K and self.multi_step >= K:
+                with trace.span("decode", "compute", mb=-1, step=self.steps_done, rounds=K):
+                    self.graph_k()
+                self.steps_done += K
+                for m in range(self.M):
+                    self.hist_n[m] += K
+                self.progress()
+                n -= K
+            if n == 0:
+                return
         order = list(range(self.M) if mbs is None else mbs)
         seq = [m for _ in range(n) for m in order]
         G = self.G
@@ -562,7 +628,7 @@ class DecodeRing:
             if self.first and G > 1:
                 self.pending[m] = True
             if self.first and G == 1 and self.record:
-                self.toks[m].append(self.cur[m].view(self.B).clone())
+                self._record_step(m)
             if i + 1 == len(seq) or (i + 1) % len(order) == 0:
                 self.steps_done += 1
             self.progress()
@@ -583,7 +649,7 @@ class DecodeRing:
                     else:
                         self._decode_body(m)
                 if self.record:
-                    self.toks[m].append(self.cur[m].view(self.B).clone())
+                    self._record_step(m)
             self.progress()
         for s in self.lanes:
             cur.wait_stream(s)
@@ -615,5 +681,19 @@ class DecodeRing:
         self.drain()
         return self.tokens() if self.first else None
 
+    def _record_step(self, m: int) -> None:
+        """One group: the token of microbatch m's decode step just queued."""
+        if self.hist is not None:
+            self.hist_n[m] += 1  # written on the device by the argmax launch
+        else:
+            self.toks[m].append(self.cur[m].view(self.B).clone())
+
     def tokens(self) -> torch.Tensor:
-        return torch.cat([torch.stack(t, 1) for t in self.toks], 0).cpu()
+        rows = []
+        for m, t in enumerate(self.toks):
+            parts = [torch.stack(t, 1)] if t else []
+            if self.hist is not None and self.hist_n[m]:
+                b = self.hist_base[m]
+                parts.append(self.hist[m][:, b:b + self.hist_n[m]])
+            rows.append(torch.cat(parts, 1))
+        return torch.cat(rows, 0).cpu()

@@ -34,11 +34,21 @@ import torch
 
 from ..models import model_info
 from ..models.llama3 import rope_tables
+from ..ops import gemm as G_
 from ..ops import transformer_ops as T_
 from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, HEAD_PART_PER_ROW, decode_workspace, fold_norm, head_argmax,
                         linear, linear_norm,
                         pack_gate_up, qkv_scatter_norm, skinny_rows)
 from .stages import StageCompute, StageOutput
+
+
+def _advance3(advance):
+    """``step(advance=...)``: (ids, positions) or (ids, positions, token history)."""
+    if advance is None:
+        return None, None, None
+    if len(advance) == 2:
+        return advance[0], advance[1], None
+    return advance[0], advance[1], advance[2]
 
 
 def _bf(t, dev):
@@ -330,6 +340,7 @@ class TransformerStage(StageCompute):
         # fused decode head's per-workgroup argmax partials (ops/gemm.py head_argmax)
         self.head_part = (torch.empty((self.max_batch * 2 * HEAD_PART_PER_ROW,), dtype=torch.int32, device=dev)
                           if self.last else None)
+        self.rowstat = G_.rowstats_buffer(self.max_batch, d, dev)  # decode rows only
         self.q8 = self.s8 = None
         if self.fp8:
             from ..ops.fp8 import kpad_of
@@ -341,13 +352,18 @@ class TransformerStage(StageCompute):
             self.logits = torch.empty((ntok, self.Vpad), dtype=bf, device=dev)
             self.next_ids = torch.empty((ntok,), dtype=torch.int32, device=dev)
 
-    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None, ws=None):
+    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None, ws=None, rs_out=None):
+        """``rs_out``: decode row-statistics partials of the output (see ``step``);
+        returns (out, whether they were written)."""
+        from ..ops.gemm import rowstats_written
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
             if skinny_rows(x.shape[0], w.q.shape[0], w8=True):  # decode: weight-only fp8 (bf16 activations)
-                return linear_w8(x, w, b, act, residual, out, ws=ws)
-            return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8)
-        return linear(x, w, b, act, residual, out, w_shuf=w_shuf, ws=ws)
+                y = linear_w8(x, w, b, act, residual, out, ws=ws, rs_out=rs_out)
+                return y, rs_out is not None and rowstats_written()
+            return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8), False
+        y = linear(x, w, b, act, residual, out, w_shuf=w_shuf, ws=ws, rs_out=rs_out)
+        return y, rs_out is not None and rowstats_written()
 
     # ------------------------------------------------------------------ specs
     act_dtype = torch.bfloat16  # stage-boundary hidden states
@@ -374,7 +390,7 @@ class TransformerStage(StageCompute):
         """Run this stage for B sequences x T new tokens at cache rows
         [b0, b0+B) and positions ``pos`` (device int32 (B,), tokens already
         cached).  Returns hidden (B*T, d) bf16, or StageOutput for the last stage.
-        ``advance`` = (ids or None, positions): greedy last stage only
+        ``advance`` = (ids or None, positions[, token history]): greedy last stage only
         (``fuses_step_tail``): the sampled ids are also written to ``ids`` and
         ``positions += 1``, in the argmax launch."""
         if advance is not None and not (self.fuses_step_tail and last_only):
@@ -409,6 +425,12 @@ class TransformerStage(StageCompute):
         ws = self.ws[r0 * self.ws_per_seq:] if T == 1 else self.ws
         # decode stream-GEMM split-K workspace: one per concurrent microbatch slot
         gws = decode_workspace(self.device, b0 // B) if T == 1 else None
+        # decode row statistics produced by the residual-writing projections
+        # (O, c_proj: per-16-column {mean, M2} partials of h) and merged by the
+        # next folded pre-norm projection (c_fc, the next layer's QKV) instead
+        # of every column-tile workgroup re-deriving them
+        rs = self.rowstat[r0:r1] if (T == 1 and self.fuse_norm and G_.ROWSTATS) else None
+        have_rs = False
         for li, L in enumerate(self.layers):
             kc, vc = self.kc[li, b0:b0 + B], self.vc[li, b0:b0 + B]
             att = self.buf_att[r0:r1]
@@ -419,10 +441,10 @@ class TransformerStage(StageCompute):
                 pass  # prefill (no RoPE): c_attn wrote q head-major and K / V straight into the caches
             elif self.fuse_norm:
                 qkv = linear_norm(h_in, L.w_qkv, out=self.buf_qkv[r0:r1], std_buf=a, ones=self.ones, q8=q8,
-                                  s8=s8, ws=gws)
+                                  s8=s8, ws=gws, rs_in=rs if have_rs else None)
             else:
                 T_.layernorm(h_in, L.ln1_w, L.ln1_b, a, self.eps, self.rms, rows=ntok)
-                qkv = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[r0:r1])
+                qkv, _ = self._lin(a, L.w_qkv, L.b_qkv, out=self.buf_qkv[r0:r1])
             if scattered:
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
             elif T == 1:  # decode: split/RoPE/cache write fused into the attention launch
@@ -433,15 +455,15 @@ class TransformerStage(StageCompute):
             else:
                 T_.qkv_split(qkv, self.buf_q, kc, vc, B, T, self.H, self.Hkv, self.hd, pos, self.cos, self.sin)
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
-            self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s, ws=gws)
+            _, have_rs = self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s, ws=gws, rs_out=rs)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
             if self.fuse_norm:
                 f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[r0:r1], std_buf=a, ones=self.ones, q8=q8,
-                                s8=s8, ws=gws)
+                                s8=s8, ws=gws, rs_in=rs if have_rs else None)
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
-                f = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[r0:r1])
-            self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s, ws=gws)
+                f, _ = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[r0:r1])
+            _, have_rs = self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s, ws=gws, rs_out=rs)
             h_in = h
         if not self.last:
             if out is not None:
@@ -458,9 +480,9 @@ class TransformerStage(StageCompute):
             # partials; one merge launch takes the ids and the step tail
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
             dst = out if out is not None else self.next_ids[r0:r0 + rows]
-            also, adv = advance if advance is not None else (None, None)
+            also, adv, hist = _advance3(advance)
             if head_argmax(x_last, self.w_head, logits[:, :self.V], self.head_part[r0 * 2 * HEAD_PART_PER_ROW:], dst,
-                           also, adv):
+                           also, adv, hist):
                 return StageOutput(logits[:, :self.V], dst)
         if self.fuse_norm:
             x_last = torch.as_strided(src, (rows, d), (ldx, 1))
@@ -480,9 +502,9 @@ class TransformerStage(StageCompute):
                 out.copy_(nxt)
             return StageOutput(logits[:, :self.V], nxt)
         dst = out if (last_only and out is not None) else nxt
-        also, adv = advance if advance is not None else (None, None)
+        also, adv, hist = _advance3(advance)
         part = self.amx_part[r0 * 2 * T_.ARGMAX_PART_PER_ROW:] if last_only else None
-        T_.argmax_rows(logits, dst, n=self.V, also=also, advance=adv, part=part)
+        T_.argmax_rows(logits, dst, n=self.V, also=also, advance=adv, part=part, hist=hist)
         return StageOutput(logits[:, :self.V], dst)
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None):

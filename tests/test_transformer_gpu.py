@@ -345,13 +345,21 @@ def test_argmax_rows_step_tail(M, N, ld, split):
     cur = torch.full((M,), -1, dtype=torch.int32, device=DEV)
     pos = torch.arange(M, dtype=torch.int32, device=DEV)
     part = torch.full((2 * T.ARGMAX_PART_PER_ROW * M,), -7, dtype=torch.int32, device=DEV) if split else None
-    T.argmax_rows(x, out, n=N, also=cur, advance=pos, part=part)
+    L = max(2, M // 2)  # rows past column L + 2 (the row stride) write nothing
+    hist = torch.full((M, L + 3), -5, dtype=torch.int32, device=DEV)[:, :L]  # ld = the row stride = L + 3
+    T.argmax_rows(x, out, n=N, also=cur, advance=pos, part=part, hist=hist)
     torch.cuda.synchronize()
     xs = x[:, :N].float().cpu()
     ref = torch.tensor([int((row == row.max()).nonzero()[0]) for row in xs])
     assert torch.equal(out.long().cpu(), ref)
     assert torch.equal(cur.cpu(), out.cpu())
     assert torch.equal(pos.cpu(), torch.arange(M, dtype=torch.int32) + 1)
+    # token history: row r's id at column pos = r (before the advance), nothing else written
+    full = torch.as_strided(hist, (M, L + 3), (L + 3, 1)).cpu()
+    for r in range(M):
+        for c in range(L + 3):
+            want = int(ref[r]) if (c == r and r < L + 3) else -5
+            assert int(full[r, c]) == want, (r, c)
     if M > 2:
         assert int(out[2]) == 5
 
@@ -936,6 +944,37 @@ def test_decode_ring_lanes_match_one_stream(model):
         assert torch.equal(v, ref), k
 
 
+@pytest.mark.parametrize("model,K", [("gpt2-tiny", 4), ("gpt2-tiny", 8), ("llama3-tiny", 4)])
+def test_decode_ring_multi_step_graph_tokens(model, K):
+    """K decode rounds of every microbatch replayed as ONE HIP graph (with the
+    device token history written by the argmax launch) give the same greedy
+    tokens as single-step graphs and as eager launches, for a step count that
+    is not a multiple of K (the remainder runs as single steps)."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models import model_info
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    n = model_info(model).num_layers
+    ranges = [(0, n // 2 - 1), (n // 2, n - 1)]
+    M, B, T, steps = 2, 3, 12, 2 * K + 3
+    sds = [ckpt.random_stage_state_dict(model, a, b, i == 0, i == 1, 9, nontrivial=True)
+           for i, (a, b) in enumerate(ranges)]
+    g = torch.Generator().manual_seed(12)
+    prompts = [torch.randint(0, model_info(model).cfg.vocab_size, (B, T), generator=g) for _ in range(M)]
+    toks = {}
+    for ms, graphs in ((K, True), (0, True), (0, False)):
+        st = [TransformerStage(model, sds[i], a, b, i == 0, i == 1, DEV, max_batch=M * B, max_seq=T + steps + K + 2)
+              for i, (a, b) in enumerate(ranges)]
+        ring = DecodeRing(st, RingLinks(), 1, M, B, use_graphs=graphs, multi_step=ms)
+        toks[(ms, graphs)] = ring.generate(prompts, T, steps)
+        assert (ring.graph_k is not None) == (ms > 1 and graphs)
+        torch.cuda.synchronize()
+    ref = toks[(0, False)]
+    assert ref.shape == (M * B, steps)
+    for k, v in toks.items():
+        assert torch.equal(v, ref), k
+
+
 @pytest.mark.parametrize("M,N,K,rms,act", [(1000, 2304, 768, False, "none"), (700, 3072, 768, False, "gelu"),
                                            (600, 2 * 1024, 512, True, "silu_mul"), (4096, 768, 768, False, "none")])
 def test_linear_norm_prefill_fold_vs_normalised_copy(M, N, K, rms, act):
@@ -1267,3 +1306,94 @@ def test_fp8_split_activation_planes(M, K):
     e1, e2 = _rel(one.float(), ref), _rel(two.float(), ref)
     print(f"fp8 GEMM M={M} K={K}: e4m3 activations {e1:.4f}, split {e2:.5f}")
     assert e2 < 4e-3 and e2 < e1 / 4
+
+
+@pytest.mark.parametrize("M,N,K,N2", [(64, 768, 768, 2304), (64, 768, 3072, 3072), (64, 1600, 1600, 4800),
+                                      (64, 1600, 6400, 6400), (48, 768, 768, 2304)])
+@pytest.mark.parametrize("w8", [False, True])
+def test_rowstats_producer_consumer(M, N, K, N2, w8):
+    """Producer-side decode row statistics: a residual-
+    writing projection (one-shot / skinny kernel) writes {mean, M2} per 16-
+    column tile of its bf16 output rows — checked against torch on the stored
+    output, including rows with |mean| / std >= 50 — and the next folded-LN
+    projection merging them (``rs_in``) matches the same projection deriving
+    its own statistics and the fp32 golden."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, fold_norm, linear, linear_norm,
+                                                         rowstats_buffer, rowstats_written)
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    h0 = torch.randn(M, N, device=DEV)
+    h0[:4] += 60.0  # |mean| / std >= 50 on the first rows
+    h0 = h0.bfloat16()
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = torch.randn(N, device=DEV) * 0.1
+    rs = rowstats_buffer(M, N, DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    if w8:
+        wq = attach_shuffled(quantize_weight(W, DEV))
+        linear_w8(x, wq, bias, 0, h0, out, rs_out=rs)
+    else:
+        linear(x, W.bfloat16(), bias, None, h0, out, w_shuf=attach_shuffled(W.bfloat16()), rs_out=rs)
+    assert rowstats_written()
+    torch.cuda.synchronize()
+    tiles = out.float().view(M, N // 16, 16)
+    mean = tiles.mean(-1)
+    m2 = ((tiles - mean[..., None]) ** 2).sum(-1)
+    got = rs.view(M, N // 16, 2)
+    assert torch.allclose(got[..., 0], mean, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(got[..., 1], m2, rtol=1e-3, atol=1e-3)
+    # consumer: folded LayerNorm projection of `out`
+    of = out.float()
+    assert (of[:4].mean(1).abs() / of[:4].std(1)).min().item() >= 50
+    gamma = torch.rand(N, device=DEV) + 0.5
+    beta = torch.randn(N, device=DEV) * 0.1
+    W2 = torch.randn(N2, N, device=DEV) / math.sqrt(N)
+    b2 = torch.randn(N2, device=DEV) * 0.1
+    f = attach_shuffled(fold_norm(W2, gamma, beta, b2, False, 1e-5, DEV, fp8=w8))
+    ref = F.layer_norm(of, (N,), gamma, beta, 1e-5) @ W2.t() + b2
+    ones = torch.ones(N, device=DEV)
+    std_buf = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y0 = linear_norm(out, f, out=torch.empty(M, N2, device=DEV, dtype=torch.bfloat16), std_buf=std_buf, ones=ones)
+    y1 = linear_norm(out, f, out=torch.empty(M, N2, device=DEV, dtype=torch.bfloat16), std_buf=std_buf, ones=ones,
+                     rs_in=rs)
+    torch.cuda.synchronize()
+    tol = 6e-2 if w8 else 1.5e-2
+    assert _rel(y1, ref) < tol, _rel(y1, ref)
+    assert _rel(y1, y0) < 4e-3, _rel(y1, y0)
+
+
+def test_rowstats_decode_stage_matches_own_statistics(monkeypatch):
+    """GPT-2 (bf16) and GPT-2 XL fp8 decode at B = 64 with producer row
+    statistics on vs off: logits within 1e-2 of each other for 4 decode steps
+    on the same tokens (the merge only reorders fp32 sums)."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.ops import gemm as G
+    from distributed_neural_networks_amd.runtime.transformer import TransformerStage
+    for model, fp8 in (("gpt2", False), ("gpt2-xl", True)):
+        B, T, steps = 64, 16, 4
+        sd = ckpt.random_stage_state_dict(model, 0, 1, True, True, 3, device=DEV, nontrivial=True)
+        st = TransformerStage(model, sd, 0, 1, True, True, DEV, max_batch=B, max_seq=T + steps + 1, fp8=fp8)
+        del sd
+        ids = torch.randint(0, 50257, (B, T), generator=torch.Generator().manual_seed(1)).to(DEV, torch.int32)
+        ref_toks, logs = None, {}
+        for on in (False, True):
+            monkeypatch.setattr(G, "ROWSTATS", on)
+            st.reset()
+            pos = torch.zeros(B, dtype=torch.int32, device=DEV)
+            o = st.step(ids, pos, B, T)
+            pos.add_(T)
+            x = o.pred.view(B, 1).clone()
+            feed, lg = [], []
+            for k in range(steps):
+                xin = x if ref_toks is None else ref_toks[k]  # the same tokens on both sides
+                feed.append(xin)
+                o = st.step(xin.to(torch.int32).contiguous(), pos, B, 1)
+                pos.add_(1)
+                lg.append(o.probs.float().clone())
+                x = o.pred.view(B, 1).clone()
+            if ref_toks is None:
+                ref_toks = feed
+            logs[on] = lg
+        for k in range(steps):
+            assert _rel(logs[True][k], logs[False][k]) < 1e-2, (model, k)
