@@ -48,7 +48,7 @@ def parse(argv=None):
     ap.add_argument("--kv", default="bf16", choices=["bf16", "fp8"], help="KV cache dtype (fp8: OCP e4m3)")
     ap.add_argument("--kv_scale", default="calibrated", choices=["calibrated", "unit"],
                     help="fp8 KV cache scale: per-layer, from the first prefill's amax, or unit")
-    ap.add_argument("--fp8_prefill", default="split", choices=["split", "e4m3"],
+    ap.add_argument("--fp8_prefill", default="e4m3", choices=["split", "e4m3"],
                     help="fp8 weights: prefill activations split (e4m3 hi + residual, ~0.1 %% logits error) or one "
                          "e4m3 byte (2x faster prefill GEMMs, ~6 %% logits error)")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
@@ -63,7 +63,7 @@ def parse(argv=None):
 
 
 def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf16", kv_scale="calibrated",
-                 fp8_prefill="split"):
+                 fp8_prefill="e4m3"):
     from distributed_neural_networks_amd import checkpoint as ckpt
     from distributed_neural_networks_amd.runtime.stages import TorchStage
     from distributed_neural_networks_amd.runtime.transformer import TransformerStage
@@ -143,7 +143,7 @@ def run(args=None, shutdown: bool = True):
     fp8 = args.dtype == "fp8"
     kv = getattr(args, "kv", "bf16")
     stages = (_build_group(model, ranges, stage_ids, dev, B * M, max_seq, fp8, kv, getattr(args, "kv_scale", "calibrated"),
-                           getattr(args, "fp8_prefill", "split"))
+                           getattr(args, "fp8_prefill", "e4m3"))
               if stage_ids else [])
     base = rep * groups
     prev = make_link(base + grp - 1, dev) if grp > 0 else None

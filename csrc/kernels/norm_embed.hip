@@ -144,80 +144,92 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict
 // still in registers) is scaled by its own amax/448 and written as OCP e4m3
 // with the K padding zeroed, plus the per-row scale — the layout
 // quant_fp8_rows produces — so the activation never round-trips through bf16.
-template <int NC, bool RMS, bool SPLIT = false>
+// R rows per wave (prefill, tens of thousands of rows): every load of the R
+// rows is issued before the first reduction (row_stats_kernel's fix: one row
+// per wave left 32768 latency-bound waves in four residency rounds).
+template <int NC, bool RMS, bool SPLIT = false, int R = 1>
 __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ w,
                                                       const float* __restrict__ b, uint8_t* __restrict__ q, int ldq,
                                                       float* __restrict__ sq, int M, int N, int kpad, float eps) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const bf16_t* xr = x + (size_t)row * ldx;
-  float v[NC][8];
-  float s = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
+  bf16x8 raw[R][NC];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < N) {
-      const bf16x8 p = *reinterpret_cast<const bf16x8*>(xr + c);
+  for (int r = 0; r < R; ++r) {
+    const bf16_t* xr = x + (size_t)min(row0 + r, M - 1) * ldx;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { v[i][j] = bf2f_s(p[j]); s += v[i][j]; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      raw[r][i] = c < N ? *reinterpret_cast<const bf16x8*>(xr + c) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-  float mean = 0.f;
-  if (!RMS) mean = wave_sum(s) / N;
-  float qs = 0.f;
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < N) {
+  for (int r = 0; r < R; ++r) {
+    const int row = row0 + r;
+    float v[NC][8];
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; qs += d * d; }
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(qs) / N + eps);
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < N) {
+    for (int i = 0; i < NC; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float bj = (!RMS && b != nullptr) ? b[c + j] : 0.f;
-        v[i][j] = (v[i][j] - mean) * rstd * w[c + j] + bj;
-        amax = fmaxf(amax, fabsf(v[i][j]));
+        v[i][j] = bf2f_s(raw[r][i][j]);
+        s += v[i][j];
+      }
+    float mean = 0.f;
+    if (!RMS) mean = wave_sum(s) / N;
+    float qs = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; qs += d * d; }
       }
     }
-  }
-  amax = wave_max(amax);
-  const float sc = amax > 0.f ? amax / 448.f : 1.f;
-  const float inv = 1.f / sc;
-  if (lane == 0) sq[row] = sc;
-  uint8_t* qr = q + (size_t)row * ldq;
+    const float rstd = rsqrtf(wave_sum(qs) / N + eps);
+    float amax = 0.f;
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < kpad) {
-      if constexpr (SPLIT) {  // hi plane + residual plane at +kpad (quant_fp8_rows' split layout)
-        float y[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = c < N ? v[i][j] * inv : 0.f;
-        int h0, h1, l0, l1;
-        q8_split8(y, h0, h1, l0, l1);
-        *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)h0, (uint32_t)h1);
-        *reinterpret_cast<uint2*>(qr + kpad + c) = make_uint2((uint32_t)l0, (uint32_t)l1);
-        continue;
-      }
-      int lo = 0, hi = 0;
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
       if (c < N) {
-        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
-        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
-        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, hi, false);
-        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float bj = (!RMS && b != nullptr) ? b[c + j] : 0.f;
+          v[i][j] = (v[i][j] - mean) * rstd * w[c + j] + bj;
+          amax = fmaxf(amax, fabsf(v[i][j]));
+        }
       }
-      *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)lo, (uint32_t)hi);
+    }
+    amax = wave_max(amax);
+    if (row >= M) continue;  // wave-uniform (after the reductions)
+    const float sc = amax > 0.f ? amax / 448.f : 1.f;
+    const float inv = 1.f / sc;
+    if (lane == 0) sq[row] = sc;
+    uint8_t* qr = q + (size_t)row * ldq;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < kpad) {
+        if constexpr (SPLIT) {  // hi plane + residual plane at +kpad (quant_fp8_rows' split layout)
+          float y[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = c < N ? v[i][j] * inv : 0.f;
+          int h0, h1, l0, l1;
+          q8_split8(y, h0, h1, l0, l1);
+          *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)h0, (uint32_t)h1);
+          *reinterpret_cast<uint2*>(qr + kpad + c) = make_uint2((uint32_t)l0, (uint32_t)l1);
+          continue;
+        }
+        int lo = 0, hi = 0;
+        if (c < N) {
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, hi, false);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+        }
+        *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)lo, (uint32_t)hi);
+      }
     }
   }
 }
@@ -320,24 +332,37 @@ extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, 
 extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq,
                                 int M, int N, int kpad, float eps, int rms, hipStream_t st, int split) {
   if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad * (split ? 2 : 1) || sq == nullptr) return -1;
+  if (M <= 0) return 0;
   const int nc = (kpad / 8 + 63) / 64;
-  dim3 grid((M + 3) / 4), blk(256);
-#define LQ(NCV)                                                                                                   \
-  if (nc <= NCV) {                                                                                                \
-    if (split) {                                                                                                  \
-      if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, \
-                                  b, (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                      \
-      else hipLaunchKernelGGL((norm_q8_kernel<NCV, false, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b, \
-                              (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                             \
-      return (int)hipGetLastError();                                                                              \
-    }                                                                                                             \
-    if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,       \
-                                (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                           \
-    else hipLaunchKernelGGL((norm_q8_kernel<NCV, false>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,          \
-                            (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                               \
-    return (int)hipGetLastError();                                                                                \
+  // 4 rows per wave once the grid would exceed one residency round (as
+  // dnn_row_stats); DNN_NORMQ8_R=1 forces one row per wave (A/B)
+  const char* re = getenv("DNN_NORMQ8_R");
+  const int R = re != nullptr ? atoi(re) : (M >= 8192 && nc <= 4 ? 4 : 1);
+  dim3 blk(256);
+#define LQK(NCV, RV)                                                                                               \
+  {                                                                                                                \
+    dim3 grid((M + 4 * RV - 1) / (4 * RV));                                                                        \
+    if (split) {                                                                                                   \
+      if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true, true, RV>), grid, blk, 0, st, (const bf16_t*)x, ldx,  \
+                                  w, b, (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                    \
+      else hipLaunchKernelGGL((norm_q8_kernel<NCV, false, true, RV>), grid, blk, 0, st, (const bf16_t*)x, ldx, w,  \
+                              b, (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                           \
+    } else if (rms) {                                                                                              \
+      hipLaunchKernelGGL((norm_q8_kernel<NCV, true, false, RV>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,    \
+                         (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                                   \
+    } else {                                                                                                       \
+      hipLaunchKernelGGL((norm_q8_kernel<NCV, false, false, RV>), grid, blk, 0, st, (const bf16_t*)x, ldx, w, b,   \
+                         (uint8_t*)q, ldq, sq, M, N, kpad, eps);                                                   \
+    }                                                                                                              \
+    return (int)hipGetLastError();                                                                                 \
+  }
+#define LQ(NCV)                      \
+  if (nc <= NCV) {                   \
+    if (R == 4 && NCV <= 4) LQK(NCV, 4) \
+    LQK(NCV, 1)                      \
   }
   LQ(1) LQ(2) LQ(4) LQ(8) LQ(16)
 #undef LQ
+#undef LQK
   return -1;
 }

@@ -64,7 +64,7 @@ class PipelineConfig:
     dtype: Optional[str] = None
     kv_cache_dtype: str = "bf16"              # "fp8": OCP e4m3 KV cache (half the decode K/V bytes)
     kv_cache_scale: str = "calibrated"        # fp8 cache: per-layer scale from the first prefill's amax, or "unit"
-    fp8_prefill: str = "split"                # dtype fp8: prefill activations "split" (e4m3 hi + residual) or "e4m3"
+    fp8_prefill: str = "e4m3"                 # dtype fp8: prefill activations "e4m3" (one byte, per-row scale) or "split" (e4m3 hi + residual)
     transport: str = "grpc"
     micro_batch_size: int = 1
     num_microbatches: int = 1
@@ -203,7 +203,7 @@ def parse_pipeline(cfg: Dict[str, Any], path: str = "<config>") -> PipelineConfi
     kvd = cfg.get("kv_cache_dtype", "bf16")
     if kvd not in ("bf16", "fp8"):
         raise ConfigError(f"ERROR: 'kv_cache_dtype' must be 'bf16' or 'fp8', got {kvd!r}")
-    fpp = cfg.get("fp8_prefill", "split")
+    fpp = cfg.get("fp8_prefill", "e4m3")
     if fpp not in ("split", "e4m3"):
         raise ConfigError(f"ERROR: 'fp8_prefill' must be 'split' or 'e4m3', got {fpp!r}")
     kvs = cfg.get("kv_cache_scale", "calibrated")

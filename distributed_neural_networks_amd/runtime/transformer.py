@@ -81,12 +81,18 @@ class TransformerStage(StageCompute):
     def __init__(self, model: str, sd: Dict[str, torch.Tensor], start: int, end: int, first: bool, last: bool,
                  device, max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
                  fp8: bool = False, temperature: float = 0.0, top_k: int = 0, seed: int = 0,
-                 kv_dtype: str = "bf16", kv_scale: str = "calibrated", fp8_prefill: str = "split"):
+                 kv_dtype: str = "bf16", kv_scale: str = "calibrated", fp8_prefill: str = "e4m3"):
         info = model_info(model)
-        # fp8 weights, prefill (W8A8) activations: "split" = e4m3 hi + e4m3
-        # residual planes against [W | W/16] (ops/fp8.py attach_split; ~0.1 %
-        # logits error), "e4m3" = one e4m3 byte per activation (2x faster
-        # GEMMs, ~6 % logits error on GPT-2 XL); decode is W8A16 either way
+        # fp8 weights, prefill (W8A8) activations: "e4m3" (default) = one e4m3
+        # byte per activation, per-row scale, at the fp8 MFMA rate; "split" =
+        # e4m3 hi + e4m3 residual planes against [W | W/16] (ops/fp8.py
+        # attach_split: bf16-equivalent MFMA work).  Against the fp32 model on
+        # the UNQUANTISED weights the e4m3 weights themselves dominate: GPT-2
+        # XL logits 9.6 % (split) vs 11.4 % (e4m3) from the golden, the same
+        # 81 % greedy agreement, at 268 k vs 378 k prefill tok/s (bf16 weights:
+        # 1.6 %, 330 k; profiles/r5_fp8_fidelity_gpt2xl_48layers.json,
+        # profiles/r5b_bench_n1.json), so the byte path is the default; decode
+        # is W8A16 either way
         if fp8_prefill not in ("split", "e4m3"):
             raise ValueError(f"fp8_prefill {fp8_prefill!r}: split or e4m3")
         self.fp8_prefill = fp8_prefill
@@ -552,7 +558,7 @@ def _e4m3_amax(t: torch.Tensor) -> float:
 def build_device_stage(model: str, sd, start: int, end: int, first: bool, last: bool, device, dtype=None,
                        max_batch: int = 8, max_seq: int = 1024, max_tokens: Optional[int] = None,
                        temperature: float = 0.0, top_k: int = 0, seed: int = 0, kv_dtype: str = "bf16",
-                       kv_scale: str = "calibrated", fp8_prefill: str = "split"):
+                       kv_scale: str = "calibrated", fp8_prefill: str = "e4m3"):
     fp8 = dtype in ("fp8", "float8_e4m3fn", "fp8_e4m3")
     info = model_info(model)
     max_seq = min(max_seq, getattr(info.cfg, "block_size", getattr(info.cfg, "max_seq", max_seq)))

@@ -129,13 +129,13 @@ def test_kv_cache_dtype():
 
 
 def test_fp8_prefill_option():
-    """``fp8_prefill`` (dtype fp8): "split" activations (default: e4m3 hi +
-    residual planes, ~0.1 % logits error) or one "e4m3" byte per activation."""
+    """``fp8_prefill`` (dtype fp8): one "e4m3" byte per activation (default)
+    or "split" activations (e4m3 hi + residual planes)."""
     c = json.loads(json.dumps(REF))
     c.update(model="gpt2-xl", dtype="fp8")
-    assert resolve_node(c, "node1").pipeline.fp8_prefill == "split"
-    c["fp8_prefill"] = "e4m3"
     assert resolve_node(c, "node1").pipeline.fp8_prefill == "e4m3"
+    c["fp8_prefill"] = "split"
+    assert resolve_node(c, "node1").pipeline.fp8_prefill == "split"
     c["fp8_prefill"] = "mx"
     with pytest.raises(ConfigError, match="fp8_prefill"):
         resolve_node(c, "node1")
