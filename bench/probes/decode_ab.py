@@ -58,6 +58,9 @@ def apply(switch: str, v: int) -> None:
         gemm.set_gemm_split_tail(int(v))
     elif switch == "fused_head":  # decode head + argmax partials in one launch (gemm_head.h)
         gemm.set_fused_head(bool(v))
+    elif switch == "mx_prefill":  # MX-scaled e4m3 prefill activations (ops/fp8.py MX_PREFILL)
+        from distributed_neural_networks_amd.ops import fp8
+        fp8.MX_PREFILL = bool(v)
     elif switch == "rowstats":  # producer-side decode row statistics (ops/gemm.py ROWSTATS)
         gemm.ROWSTATS = bool(v)
     elif switch == "multistep":  # K decode rounds per HIP graph (runtime/scheduler.py DecodeRing multi_step)

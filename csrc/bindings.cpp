@@ -76,6 +76,24 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_rowstats(reinterpret_cast<void*>(static_cast<uintptr_t>(out)), out_ld, CP(in), in_ld);
   });
   m.def("gemm_rowstats_written", []() { return dnn_gemm_rowstats_written(); });
+  m.def("quant_fp8_mx", [](u64 x, int ldx, u64 q, int ldq, u64 sx, int M, int K, int kpad, u64 st) {
+    return dnn_quant_fp8_mx(CP(x), ldx, P(q), ldq, P(sx), M, K, kpad, ST(st));
+  });
+  m.def("layernorm_q8_mx", [](u64 x, int ldx, u64 w, u64 b, u64 q, int ldq, u64 sx, int M, int N, int kpad, float eps,
+                              int rms, u64 st) {
+    return dnn_layernorm_q8_mx(CP(x), ldx, CFP(w), CFP(b), P(q), ldq, P(sx), M, N, kpad, eps, rms, ST(st));
+  });
+  m.def("gemm_fp8_mx", [](u64 a, u64 sx, u64 w, u64 sw, u64 c, int ldc, u64 bias, u64 r, int ldr, int M, int N, int Kb,
+                          int act, u64 qo, int ldq, u64 sxo, int kpo, u64 st) {
+    return dnn_gemm_fp8_mx(CP(a), CP(sx), CP(w), CFP(sw), P(c), ldc, CFP(bias), CP(r), ldr, M, N, Kb, act, P(qo), ldq,
+                           P(sxo), kpo, ST(st));
+  });
+  m.def("gemm_fp8_qkv_scatter_mx", [](u64 a, u64 sx, u64 w, u64 sw, u64 bias, u64 q, u64 kc, u64 vc, u64 pos, int B,
+                                      int T, int H, int Hkv, int hd, int S, int Kb, u64 st) {
+    return dnn_gemm_fp8_qkv_scatter_mx(CP(a), CP(sx), CP(w), CFP(sw), CFP(bias), P(q), P(kc), P(vc),
+                                       reinterpret_cast<const int*>(static_cast<uintptr_t>(pos)), B, T, H, Hkv, hd, S,
+                                       Kb, ST(st));
+  });
   m.def("argmax_final", [](u64 part, int S, int M, u64 out, u64 out2, u64 pos_inc, u64 st, u64 hist, int hist_ld) {
     return dnn_argmax_final(CP(part), S, M, IP(out), IP(out2), IP(pos_inc), ST(st), IP(hist), hist_ld);
   });

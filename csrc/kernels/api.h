@@ -56,6 +56,16 @@ int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, cons
 int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st,
                      int* hist = nullptr, int hist_ld = 0);
 int dnn_gemm_set_split_tail(int on);
+// MX-scaled W8A8 prefill (e8m0 per (row, 128 columns), common.h mx_index)
+int dnn_quant_fp8_mx(const void* x, int ldx, void* q, int ldq, void* sx, int M, int K, int kpad, hipStream_t st);
+int dnn_layernorm_q8_mx(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, void* sx, int M,
+                        int N, int kpad, float eps, int rms, hipStream_t st);
+int dnn_gemm_fp8_mx(const void* A8, const void* sx, const void* W8, const float* sw, void* C, int ldc,
+                    const float* bias, const void* R, int ldr, int M, int N, int Kb, int act, void* qo, int ldq,
+                    void* sxo, int kpo, hipStream_t st);
+int dnn_gemm_fp8_qkv_scatter_mx(const void* A8, const void* sx, const void* W8, const float* sw, const float* bias,
+                                void* q, void* kc, void* vc, const int* pos, int B, int T, int H, int Hkv, int hd,
+                                int S, int Kb, hipStream_t st);
 // producer-side row statistics for the next decode GEMM call of this thread (gemm_skinny.hip)
 int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld);
 int dnn_gemm_rowstats_written();  // prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)

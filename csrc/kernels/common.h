@@ -138,6 +138,31 @@ __device__ __forceinline__ void q8_split8(const float (&y)[8], int& h0, int& h1,
   l1 = __builtin_amdgcn_cvt_pk_fp8_f32(r[6], r[7], l1, true);
 }
 
+// MX (block-scaled) fp8 activations for the W8A8 prefill GEMM: one e8m0
+// scale per (row, 128-column K-tile), applied by the scaled MFMA itself
+// (v_mfma_scale_f32_16x16x128_f8f6f4's per-lane B scale), so every
+// quantiser — a row pass or a GEMM epilogue — decides its scales from the
+// 128 columns it holds, with no whole-row amax.  Byte of (row m, K-tile t) in
+// a buffer of Mpad = ceil(M / 64) * 64 rows per K-tile: within a 64-row block
+// the 4 bytes of rows r, r + 16, r + 32, r + 48 are one dword, so the GEMM's
+// lane (row r of each of its 4 16-row fragments) loads them with one load and
+// selects byte i with the MFMA's op_sel.
+__host__ __device__ __forceinline__ size_t mx_index(int m, int t, int mpad) {
+  return ((size_t)t * (mpad >> 6) + (m >> 6)) * 64 + (m & 15) * 4 + ((m >> 4) & 3);
+}
+__host__ __device__ __forceinline__ int mx_mpad(int M) { return (M + 63) & ~63; }
+
+// e8m0 block scale: the power of two 2^e >= amax / 448 as its biased exponent
+// byte (fp32 and e8m0 share the bias 127) and its reciprocal; clamped to
+// [2^-126, 2^126] (never the NaN code 255, never a subnormal reciprocal).
+__device__ __forceinline__ uint32_t e8m0_of(float amax, float& inv) {
+  const uint32_t b = __float_as_uint(amax * (1.f / 448.f));
+  uint32_t e = ((b >> 23) & 0xffu) + ((b & 0x7fffffu) != 0u ? 1u : 0u);
+  e = e < 1u ? 1u : (e > 253u ? 253u : e);
+  inv = __uint_as_float((254u - e) << 23);  // 2^(127 - e)
+  return e;
+}
+
 // Bijective XCD-aware block remap: blocks that the dispatcher places on the same
 // XCD (b % 8 equal) get a contiguous range of logical tile ids (guide §5, T1).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

@@ -550,12 +550,47 @@ __device__ __forceinline__ void bg_mfma_f8(f32x4 (&acc)[MI][NJ], const bf16x8 (&
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int ACT, bool SCATTER = false, int NQ = 2>
+// MX e8m0 scales of the activations on the scaled MFMA (MXA, common.h
+// mx_index: one dword per lane per 128-row half-tile and K-tile, byte i =
+// fragment i): acc carries the activation scales, the epilogue only the
+// weight channel scale.
+template <int MI, int NJ>
+__device__ __forceinline__ void bg_mfma_f8x(f32x4 (&acc)[MI][NJ], const bf16x8 (&a)[MI][2], const bf16x8 (&b)[NJ][2],
+                                            uint32_t s) {
+  static_assert(MI == 4, "one op_sel byte per A fragment");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const i32x8_t bj = f8_cat(b[j][0], b[j][1]);
+    acc[0][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bj, f8_cat(a[0][0], a[0][1]), acc[0][j], 0, 0, 0,
+                                                                 0x7f7f7f7f, 0, s);
+    acc[1][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bj, f8_cat(a[1][0], a[1][1]), acc[1][j], 0, 0, 0,
+                                                                 0x7f7f7f7f, 1, s);
+    acc[2][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bj, f8_cat(a[2][0], a[2][1]), acc[2][j], 0, 0, 0,
+                                                                 0x7f7f7f7f, 2, s);
+    acc[3][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bj, f8_cat(a[3][0], a[3][1]), acc[3][j], 0, 0, 0,
+                                                                 0x7f7f7f7f, 3, s);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// QOUT (GELU c_fc of the MX prefill): the epilogue quantises its own output
+// tile for the next GEMM — e4m3 bytes q_out[M][ldq] with one e8m0 scale per
+// (row, 128 columns) from the tile's columns alone (the 4 waves sharing a row
+// agree through LDS), so the c_proj input never exists in bf16 and no
+// quantise pass reads it back.  Columns >= N are written as zeros up to kpo.
+template <int ACT, bool SCATTER = false, int NQ = 2, bool MXA = false, bool QOUT = false>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     const uint8_t* __restrict__ A8, const float* __restrict__ sa, const uint8_t* __restrict__ W8,
     const float* __restrict__ sw, bf16_t* __restrict__ C, int ldc, const float* __restrict__ bias,
-    const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb, QkvScatter scat = {}) {
+    const bf16_t* __restrict__ R, int ldr, int M, int N, int Kb, QkvScatter scat = {},
+    const uint32_t* __restrict__ sx = nullptr, uint8_t* __restrict__ qo = nullptr, int ldq = 0,
+    uint8_t* __restrict__ sxo = nullptr, int kpo = 0) {
+  // (QOUT reuses the operand LDS after the main loop: see the epilogue)
   static_assert(NQ == 1 || NQ == 2, "256x256 or 256x128 tiles");
+  static_assert(!MXA || NQ == 2, "MX activations: 256^2 tiles");
+  static_assert(!QOUT || (MXA && ACT == ACT_GELU && !SCATTER), "quantised output: the MX c_fc");
   constexpr int TN = 128 * NQ;  // NQ = 1: the 256x128 variant (tail-split launches), as the bf16 kernel's
   __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -625,6 +660,18 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     }
     if (t < nk) ktile1(t, std::integral_constant<int, 0>{});
   } else {
+  // MXA: the scale dwords of K-tile t (half-tiles 0 / 1 of A) in scl[t & 1];
+  // tile t + 1's are loaded in tile t's first phase, so the phase-4 vmcnt(4)
+  // (which retires everything but the last four DMAs) has retired them too
+  uint32_t scl[2][2] = {{0x7f7f7f7fu, 0x7f7f7f7fu}, {0x7f7f7f7fu, 0x7f7f7f7fu}};
+  const int nb64 = mx_mpad(M) >> 6;
+  auto ldsx = [&](int t, uint32_t (&d)[2]) {
+    t = t < nk ? t : nk - 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      d[h] = sx[((size_t)t * nb64 + min((m0 >> 6) + 2 * h + wr, nb64 - 1)) * 16 + (lane & 15)];
+  };
+  if constexpr (MXA) ldsx(0, scl[0]);
   stA(0, 0, 0);
   stB(0, 1, 0);
   stA(0, 1, 0);
@@ -635,30 +682,35 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   bg_barrier();
   if (wr == 1) bg_barrier();
 
+  auto mm = [&](f32x4 (&c)[4][2], const bf16x8 (&bb)[2][2], uint32_t s) {
+    if constexpr (MXA) bg_mfma_f8x<4, 2>(c, af, bb, s);
+    else bg_mfma_f8<4, 2>(c, af, bb);
+  };
   auto ktile = [&](const int t, auto ucst) {
     constexpr int u = decltype(ucst)::value;
     bg_read<2>(b0, half(u, 2), brow, lane);
     __builtin_amdgcn_sched_barrier(0);
     bg_read<4>(af, half(u, 0), arow, lane);
     stA(u ^ 1, 1, t + 1);
+    if constexpr (MXA) ldsx(t + 1, scl[u ^ 1]);
     bg_barrier();
-    bg_mfma_f8<4, 2>(acc[0][0], af, b0);
+    mm(acc[0][0], b0, scl[u][0]);
     bg_barrier();
     bg_read<2>(b1, half(u, 3), brow, lane);
     stB(u ^ 1, 0, t + 1);
     bg_barrier();
-    bg_mfma_f8<4, 2>(acc[0][1], af, b1);
+    mm(acc[0][1], b1, scl[u][0]);
     bg_barrier();
     bg_read<4>(af, half(u, 1), arow, lane);
     stA(u, 0, t + 2);
     bg_barrier();
-    bg_mfma_f8<4, 2>(acc[1][1], af, b1);
+    mm(acc[1][1], b1, scl[u][1]);
     bg_barrier();
     bg_read<2>(b0, half(u, 2), brow, lane);
     stB(u, 1, t + 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     bg_barrier();
-    bg_mfma_f8<4, 2>(acc[1][0], af, b0);
+    mm(acc[1][0], b0, scl[u][1]);
     bg_barrier();
   };
   int t = 0;
@@ -671,6 +723,71 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
 
+  if constexpr (QOUT) {
+    // bias + GELU in place, then per (row, 128-column half nq) amax: the lane's
+    // 8 columns, the 4 lane rows of the wave (xor 16 / 32), the 4 waves of the
+    // wave row through LDS (the operand buffers are dead), one barrier
+    float* red = reinterpret_cast<float*>(smem);  // [mq][nq][i][wr][16][wc]
+    __syncthreads();  // every wave past its last operand read and DMA (vmcnt(0) above)
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < NQ; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float am = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
+            f32x4 cs, bs;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              cs[r] = n + r < N ? sw[n + r] : 0.f;
+              bs[r] = (bias != nullptr && n + r < N) ? bias[n + r] : 0.f;
+            }
+            f32x4 v = acc[mq][nq][i][j] * cs + bs;
+            const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+            v = f32x4{g0[0], g0[1], g1[0], g1[1]};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] = n + r < N ? v[r] : 0.f;
+              am = fmaxf(am, fabsf(v[r]));
+            }
+            acc[mq][nq][i][j] = v;
+          }
+          am = fmaxf(am, __shfl_xor(am, 16, 64));
+          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          if (lane < 16) red[((((mq * 2 + nq) * 4 + i) * 2 + wr) * 16 + lane) * 4 + wc] = am;
+        }
+    __syncthreads();
+    const int mpad = mx_mpad(M);
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < NQ; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 a4 =
+              *reinterpret_cast<const f32x4*>(red + ((((mq * 2 + nq) * 4 + i) * 2 + wr) * 16 + (lane & 15)) * 4);
+          float inv;
+          const uint32_t e = e8m0_of(fmaxf(fmaxf(a4[0], a4[1]), fmaxf(a4[2], a4[3])), inv);
+          const f32x4 v0 = acc[mq][nq][i][0] * inv, v1 = acc[mq][nq][i][1] * inv;
+          int x = __builtin_amdgcn_cvt_pk_fp8_f32(v0[0], v0[1], 0, false);
+          x = __builtin_amdgcn_cvt_pk_fp8_f32(v0[2], v0[3], x, true);
+          int y = __builtin_amdgcn_cvt_pk_fp8_f32(v1[0], v1[1], 0, false);
+          y = __builtin_amdgcn_cvt_pk_fp8_f32(v1[2], v1[3], y, true);
+          // as epi_pair_bf16: one permlane16_swap hands every lane 8 contiguous columns
+          const auto sw2 = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)y, false, false);
+          const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
+          const int q = lane >> 4;
+          const int cb = n0 + nq * 128 + wc * 32;
+          const int c = cb + ((q & 1) << 4) + ((q >> 1) << 3);
+          if (m < M && c < kpo) *reinterpret_cast<uint2*>(qo + (size_t)m * ldq + c) = make_uint2(sw2[0], sw2[1]);
+          const int t = (n0 + nq * 128) >> 7;
+          if (wc == 0 && q == 0 && m < M && t * 128 < kpo) sxo[mx_index(m, t, mpad)] = (uint8_t)e;
+        }
+    return;
+  }
   const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
   // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
@@ -694,7 +811,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
         const int nb = n0 + nq * 128 + wc * 32;
-        const float rs = m < M ? sa[m] : 0.f;
+        const float rs = MXA ? 1.f : (m < M ? sa[m] : 0.f);  // MXA: the activation scales are in acc
         f32x4 v[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1015,4 +1132,57 @@ extern "C" int dnn_gemm_fp8_256(const void* A, const float* sa, const void* W, c
   F8L(ACT_NONE) F8L(ACT_RELU) F8L(ACT_GELU) F8L(ACT_SILU_MUL)
 #undef F8L
   return -2;
+}
+
+// MX-scaled W8A8 GEMM on the 256^2 kernel: A8 [M][Kb]
+// e4m3 with e8m0 scales sx per (row, 128-column K-tile) (common.h mx_index;
+// dnn_quant_fp8_mx / dnn_layernorm_q8_mx / a QOUT epilogue write them), W8 /
+// sw per-channel e4m3.  qo != nullptr (act GELU): the output is quantised in
+// the epilogue instead (QOUT: qo [M][ldq] e4m3 with scales sxo, kpo columns,
+// the next GEMM's MX input) and C is not written.  -3: not a 256^2 shape (the
+// caller keeps the per-row path).
+extern "C" int dnn_gemm_fp8_mx(const void* A8, const void* sx, const void* W8, const float* sw, void* C, int ldc,
+                               const float* bias, const void* R, int ldr, int M, int N, int Kb, int act, void* qo,
+                               int ldq, void* sxo, int kpo, hipStream_t st) {
+  if (Kb % 128 != 0 || M <= 0 || N <= 0 || sx == nullptr || sw == nullptr) return -1;
+  if (M < 256 || N < 256) return -3;
+  if (qo != nullptr && (act != ACT_GELU || sxo == nullptr || kpo % 128 != 0 || kpo < N || ldq < kpo ||
+                        (ldq & 7) != 0 || ((uintptr_t)qo & 7) != 0))
+    return -1;
+  if (act == ACT_SILU_MUL && N % 16 != 0) return -1;
+  const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+  const uint32_t* sxw = reinterpret_cast<const uint32_t*>(sx);
+  if (qo != nullptr) {
+    hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_GELU, false, 2, true, true>), dim3(tiles), dim3(512), 0, st,
+                       (const uint8_t*)A8, (const float*)nullptr, (const uint8_t*)W8, sw, (bf16_t*)nullptr, 0, bias,
+                       (const bf16_t*)nullptr, 0, M, N, Kb, QkvScatter{}, sxw, (uint8_t*)qo, ldq, (uint8_t*)sxo, kpo);
+    return (int)hipGetLastError();
+  }
+#define F8M(a)                                                                                                      \
+  if (act == a) {                                                                                                   \
+    hipLaunchKernelGGL((gemm_fp8_256_kernel<a, false, 2, true>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A8, \
+                       (const float*)nullptr, (const uint8_t*)W8, sw, (bf16_t*)C, ldc, bias, (const bf16_t*)R, ldr, M, \
+                       N, Kb, QkvScatter{}, sxw);                                                                   \
+    return (int)hipGetLastError();                                                                                  \
+  }
+  F8M(ACT_NONE) F8M(ACT_RELU) F8M(ACT_GELU) F8M(ACT_SILU_MUL)
+#undef F8M
+  return -2;
+}
+
+// fp8 c_attn with the QKV scatter epilogue on MX-scaled activations
+// (dnn_layernorm_q8_mx): as dnn_gemm_fp8_qkv_scatter, sx instead of sa.
+extern "C" int dnn_gemm_fp8_qkv_scatter_mx(const void* A8, const void* sx, const void* W8, const float* sw,
+                                           const float* bias, void* q, void* kc, void* vc, const int* pos, int B, int T,
+                                           int H, int Hkv, int hd, int S, int Kb, hipStream_t st) {
+  const int M = B * T, N = (H + 2 * Hkv) * hd;
+  if (Kb % 128 != 0 || M <= 0 || hd % 8 != 0 || sx == nullptr || sw == nullptr) return -1;
+  if (N % 32 != 0 || M < 256 || N < 256 || ((uintptr_t)bias & 15) != 0) return -3;
+  if ((hd & (hd - 1)) != 0 || M >= (1 << 24)) return -3;
+  QkvScatter sc{(bf16_t*)q, (bf16_t*)kc, (bf16_t*)vc, pos, T, H, Hkv, __builtin_ctz(hd), S, 1.0f / (float)T};
+  const int tiles = ((M + BG_M - 1) / BG_M) * ((N + BG_N - 1) / BG_N);
+  hipLaunchKernelGGL((gemm_fp8_256_kernel<ACT_NONE, true, 2, true>), dim3(tiles), dim3(512), 0, st, (const uint8_t*)A8,
+                     (const float*)nullptr, (const uint8_t*)W8, sw, (bf16_t*)q, hd, bias, (const bf16_t*)nullptr, 0, M,
+                     N, Kb, sc, reinterpret_cast<const uint32_t*>(sx));
+  return (int)hipGetLastError();
 }

@@ -162,9 +162,57 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
   }
 }
 
+// MX quantisation bf16 -> e4m3 (common.h mx_index): one e8m0 scale per (row,
+// 128-column block), one wave per row, one pass — the 16 lanes of a block
+// take its amax with 4 xor-shuffles, so no row amax and no second read.
+// Columns K..kpad-1 are written as zeros (scale of an all-zero block: 2^-126).
+__global__ __launch_bounds__(256) void quant_fp8_mx_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                           uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ sx,
+                                                           int M, int K, int kpad) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  uint8_t* qr = q + (size_t)row * ldq;
+  const int mpad = mx_mpad(M);
+  for (int c0 = 0; c0 < kpad; c0 += 512) {  // wave-uniform: every lane joins the shuffles
+    const int c = c0 + lane * 8;
+    bf16x8 p = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < K) p = *reinterpret_cast<const bf16x8*>(xr + c);
+    float v[8], amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = bf2f_s(p[j]);
+      amax = fmaxf(amax, fabsf(v[j]));
+    }
+    amax = group_max<16>(amax);
+    float inv;
+    const uint32_t e = e8m0_of(amax, inv);
+    if (c < kpad) {
+      int lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+      *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)lo, (uint32_t)hi);
+      if ((lane & 15) == 0) sx[mx_index(row, c >> 7, mpad)] = (uint8_t)e;
+    }
+  }
+}
+
 }  // namespace dnn
 
 using namespace dnn;
+
+// MX-scaled e4m3 rows (the W8A8 prefill's activations, gemm_fp8_256 MXA):
+// q [M][ldq bytes] (ldq >= kpad), sx = mx_mpad(M) * kpad / 128 scale bytes.
+extern "C" int dnn_quant_fp8_mx(const void* x, int ldx, void* q, int ldq, void* sx, int M, int K, int kpad,
+                                hipStream_t st) {
+  if (K % 8 != 0 || kpad % 128 != 0 || kpad < K || ldq < kpad || (ldq & 7) != 0 || M <= 0) return M <= 0 ? 0 : -1;
+  hipLaunchKernelGGL(quant_fp8_mx_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, ldx, (uint8_t*)q,
+                     ldq, (uint8_t*)sx, M, K, kpad);
+  return (int)hipGetLastError();
+}
 
 // 0 = auto, 128 / 256 force a tile (A/B benchmarking, tests)
 static int g_fp8_tile = 0;

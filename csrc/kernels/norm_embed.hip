@@ -147,10 +147,14 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict
 // R rows per wave (prefill, tens of thousands of rows): every load of the R
 // rows is issued before the first reduction (row_stats_kernel's fix: one row
 // per wave left 32768 latency-bound waves in four residency rounds).
-template <int NC, bool RMS, bool SPLIT = false, int R = 1>
+// MX: one e8m0 scale per (row, 128-column block) instead of the row scale
+// (common.h mx_index; the 16 lanes of a block agree on it by 4 shuffles).
+template <int NC, bool RMS, bool SPLIT = false, int R = 1, bool MX = false>
 __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ w,
                                                       const float* __restrict__ b, uint8_t* __restrict__ q, int ldq,
-                                                      float* __restrict__ sq, int M, int N, int kpad, float eps) {
+                                                      float* __restrict__ sq, int M, int N, int kpad, float eps,
+                                                      uint8_t* __restrict__ sx = nullptr) {
+  static_assert(!(MX && SPLIT), "MX scales with one e4m3 byte per activation");
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= M) return;
@@ -200,6 +204,33 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__
           amax = fmaxf(amax, fabsf(v[i][j]));
         }
       }
+    }
+    if constexpr (MX) {
+      if (row >= M) continue;  // wave-uniform
+      uint8_t* qr = q + (size_t)row * ldq;
+      const int mpad = mx_mpad(M);
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int c = (lane + 64 * i) * 8;
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) am = c < N ? fmaxf(am, fabsf(v[i][j])) : am;
+        am = group_max<16>(am);  // the 128-column block of lanes 16g..16g+15
+        float inv;
+        const uint32_t e = e8m0_of(am, inv);
+        if (c < kpad) {
+          int lo = 0, hi = 0;
+          if (c < N) {
+            lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
+            lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+            hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, hi, false);
+            hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+          }
+          *reinterpret_cast<uint2*>(qr + c) = make_uint2((uint32_t)lo, (uint32_t)hi);
+          if ((lane & 15) == 0) sx[mx_index(row, c >> 7, mpad)] = (uint8_t)e;
+        }
+      }
+      continue;
     }
     amax = wave_max(amax);
     if (row >= M) continue;  // wave-uniform (after the reductions)
@@ -329,6 +360,37 @@ extern "C" int dnn_embed_gpt2(const int* idx, const void* wte, const void* wpe, 
 
 // Normalise (w, b; LayerNorm or RMSNorm) and quantise rows to e4m3 with per-row
 // scales: q [M][ldq bytes] (columns N..kpad-1 zeroed), sq [M].
+// Normalise + MX-quantise (e8m0 per (row, 128-column block), common.h
+// mx_index): sx holds mx_mpad(M) * kpad / 128 bytes.
+extern "C" int dnn_layernorm_q8_mx(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, void* sx,
+                                   int M, int N, int kpad, float eps, int rms, hipStream_t st) {
+  if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 128 != 0 || ldq < kpad || (ldq & 7) != 0 || sx == nullptr)
+    return -1;
+  if (M <= 0) return 0;
+  const int nc = (kpad / 8 + 63) / 64;
+  const char* re = getenv("DNN_NORMQ8_R");
+  const int R = re != nullptr ? atoi(re) : (M >= 8192 && nc <= 4 ? 4 : 1);
+  dim3 blk(256);
+#define LQM(NCV, RV)                                                                                              \
+  {                                                                                                               \
+    dim3 grid((M + 4 * RV - 1) / (4 * RV));                                                                       \
+    if (rms) hipLaunchKernelGGL((norm_q8_kernel<NCV, true, false, RV, true>), grid, blk, 0, st, (const bf16_t*)x, \
+                                ldx, w, b, (uint8_t*)q, ldq, (float*)nullptr, M, N, kpad, eps, (uint8_t*)sx);    \
+    else hipLaunchKernelGGL((norm_q8_kernel<NCV, false, false, RV, true>), grid, blk, 0, st, (const bf16_t*)x,    \
+                            ldx, w, b, (uint8_t*)q, ldq, (float*)nullptr, M, N, kpad, eps, (uint8_t*)sx);        \
+    return (int)hipGetLastError();                                                                                \
+  }
+#define LQ(NCV)                         \
+  if (nc <= NCV) {                      \
+    if (R == 4 && NCV <= 4) LQM(NCV, 4) \
+    LQM(NCV, 1)                         \
+  }
+  LQ(1) LQ(2) LQ(4) LQ(8) LQ(16)
+#undef LQ
+#undef LQM
+  return -1;
+}
+
 extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const float* b, void* q, int ldq, float* sq,
                                 int M, int N, int kpad, float eps, int rms, hipStream_t st, int split) {
   if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad * (split ? 2 : 1) || sq == nullptr) return -1;

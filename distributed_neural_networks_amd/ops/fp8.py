@@ -79,19 +79,81 @@ def quant_rows(x: torch.Tensor, q_out: torch.Tensor, s_out: torch.Tensor, rows: 
           "quant_fp8_rows")
 
 
+MX_PREFILL = True  # e4m3 prefill activations with MX e8m0 block scales (A/B switch)
+
+
+def mx_mpad(M: int) -> int:
+    return -(-M // 64) * 64
+
+
+def mx_scale_bytes(M: int, kpad: int) -> int:
+    """Bytes of the MX scales of M rows x kpad columns: one e8m0 per (row, 128
+    columns), rows padded to 64 (csrc/kernels/common.h mx_index)."""
+    return mx_mpad(M) * (kpad // 128)
+
+
+def mx_ok(M: int, N: int, w: Fp8Weight) -> bool:
+    """The MX W8A8 path applies: the 256^2 fp8 kernel's shapes, one e4m3 byte
+    per activation (no split planes)."""
+    return MX_PREFILL and M >= 256 and N >= 256 and w.q2 is None
+
+
+def quant_rows_mx(x: torch.Tensor, q_out: torch.Tensor, sx_out: torch.Tensor, rows: Optional[int] = None) -> None:
+    """MX e4m3 quantisation: q_out (M, kpad) bytes, one e8m0 scale per (row,
+    128 columns) in sx_out (``mx_scale_bytes``); K padding zeroed."""
+    M = rows if rows is not None else x.shape[0]
+    K = x.shape[-1]
+    kp = kpad_of(K)
+    if q_out.numel() * q_out.element_size() < M * kp or sx_out.numel() * sx_out.element_size() < mx_scale_bytes(M, kp):
+        raise ValueError("quant_rows_mx: bad output buffer")
+    check(lib().quant_fp8_mx(ptr(x), x.stride(0), ptr(q_out), kp, ptr(sx_out), M, K, kp, stream_ptr()),
+          "quant_fp8_mx")
+
+
 def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None, act: int = 0,
                residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                qbuf: Optional[torch.Tensor] = None, sbuf: Optional[torch.Tensor] = None,
-               prequantized: bool = False) -> torch.Tensor:
+               prequantized: bool = False, sx: Optional[torch.Tensor] = None,
+               q_out: Optional[tuple] = None) -> torch.Tensor:
     """W8A8 GEMM.  ``prequantized``: ``qbuf``/``sbuf`` already hold the e4m3
     rows and scales of x (``transformer_ops.layernorm_q8``); x only gives M, K.
     Prefill rows with ``w.q2`` (``attach_split``) run on split activations
-    (2 Kpad bytes per row; a prequantized buffer must be split too)."""
+    (2 Kpad bytes per row; a prequantized buffer must be split too).
+
+    ``sx`` (a byte buffer of ``mx_scale_bytes``): where ``mx_ok``, the
+    activations carry MX e8m0 scales per (row, 128 columns) applied by the
+    scaled MFMA (``quant_rows_mx`` / ``layernorm_q8_mx`` write them; with
+    ``prequantized`` they are already in ``qbuf`` / ``sx``).  ``q_out`` =
+    (bytes, scales) with act GELU: the epilogue quantises its output for the
+    next GEMM (MX) and ``out`` is not written — the c_fc of the MX prefill."""
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
     N, kp = w.q.shape
     if kp != kpad_of(K) or (w.k and w.k != K):
         raise ValueError(f"linear_fp8: x K={K} vs weight K={w.k} (padded {kp})")
+    if sx is not None and mx_ok(M, N, w):
+        if not prequantized:
+            if qbuf is None or qbuf.numel() * qbuf.element_size() < M * kp:
+                raise ValueError("linear_fp8: MX needs a qbuf of M x kpad bytes")
+            quant_rows_mx(x2, qbuf, sx, M)
+        qo, sxo, kpo = (None, None, 0)
+        if q_out is not None:
+            qo, sxo = q_out
+            kpo = kpad_of(N)
+            if act != 2 or qo.numel() * qo.element_size() < M * kpo or \
+                    sxo.numel() * sxo.element_size() < mx_scale_bytes(M, kpo):
+                raise ValueError("linear_fp8: q_out needs act GELU and M x kpad(N) bytes + scales")
+        elif out is None:
+            out = torch.empty((M, N // 2 if act == 3 else N), dtype=torch.bfloat16, device=x.device)
+        o2 = out.reshape(-1, out.shape[-1]) if out is not None else None
+        r2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
+        check(lib().gemm_fp8_mx(ptr(qbuf), ptr(sx), ptr(w.q), ptr(w.scale), ptr(o2),
+                                0 if o2 is None else o2.stride(0), ptr(bias), ptr(r2),
+                                0 if r2 is None else r2.stride(0), M, N, kp, act, ptr(qo), kpo, ptr(sxo), kpo,
+                                stream_ptr()), "gemm_fp8_mx")
+        return out
+    if q_out is not None or (prequantized and sx is not None):
+        raise ValueError("linear_fp8: q_out / MX-prequantized input off the MX path (mx_ok)")
     split = w.q2 is not None and M > 64
     kq = 2 * kp if split else kp
     if prequantized:

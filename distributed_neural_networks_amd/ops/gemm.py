@@ -255,7 +255,8 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
                 out: Optional[torch.Tensor] = None, std_buf: Optional[torch.Tensor] = None,
                 ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
                 s8: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                rs_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+                rs_in: Optional[torch.Tensor] = None, sx: Optional[torch.Tensor] = None,
+                q_out: Optional[tuple] = None) -> torch.Tensor:
     """``linear(norm(x), W, b)`` for a ``FoldedLinear``.  ``rs_in`` (decode):
     the row-statistics partials of ``x`` written by its producer (``linear(...,
     rs_out=)``), merged instead of deriving the statistics from ``x``.  Decode-sized M (<= 64):
@@ -265,6 +266,7 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
     no beta), then the plain GEMM with the folded weight and bias (bf16, or the
     W8A8 fp8 GEMM with the ``q8``/``s8`` activation-quantisation buffers)."""
     from .fp8 import Fp8Weight, linear_fp8, linear_w8
+    from .fp8 import mx_ok as fp8_mx_ok
     a = _ACTS[act] if not isinstance(act, int) else act
     M, K = x.shape
     w8 = isinstance(f.w, Fp8Weight)
@@ -275,6 +277,15 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         from .transformer_ops import layernorm, layernorm_q8
         if std_buf is None or ones is None:
             raise ValueError("linear_norm: large M needs std_buf and ones")
+        if w8 and q8 is not None and sx is not None and fp8_mx_ok(M, N, f.w):
+            # standardise + MX-quantise in one pass (e8m0 per 128 columns); the
+            # scaled MFMA applies the scales
+            from .transformer_ops import layernorm_q8_mx
+            kp = f.w.q.shape[1]
+            layernorm_q8_mx(x, ones, None, q8, sx, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+            return linear_fp8(x, f.w, f.bias, a, residual, out, q8, None, prequantized=True, sx=sx, q_out=q_out)
+        if q_out is not None:
+            raise ValueError("linear_norm: q_out needs the MX fp8 prefill path")
         if w8 and q8 is not None and s8 is not None:
             # standardise + quantise in one pass: the e4m3 rows feed the W8A8 GEMM directly
             kp = f.w.q.shape[1]
@@ -321,7 +332,7 @@ QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)
 def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q: torch.Tensor, kc: torch.Tensor,
                      vc: torch.Tensor, pos: torch.Tensor, B: int, T: int, H: int, Hkv: int, hd: int,
                      ones: Optional[torch.Tensor] = None, q8: Optional[torch.Tensor] = None,
-                     s8: Optional[torch.Tensor] = None) -> bool:
+                     s8: Optional[torch.Tensor] = None, sx: Optional[torch.Tensor] = None) -> bool:
     """Prefill c_attn (folded pre-norm, no RoPE) with the QKV scatter epilogue
     (gemm_bf16.hip ``dnn_gemm_bf16_qkv_scatter``): q lands in ``q`` as (B, H, T,
     hd) and K / V straight in the bf16 caches at rows ``pos[b] + t``, so the head-
@@ -340,6 +351,16 @@ def qkv_scatter_norm(x: torch.Tensor, f: FoldedLinear, std_buf: torch.Tensor, q:
         return False
     if not (kc.is_contiguous() and vc.is_contiguous()) or q.numel() < M * H * hd or pos.dtype != torch.int32:
         return False
+    if w8 and sx is not None and q8 is not None and ones is not None and N % 32 == 0:
+        from .fp8 import mx_ok
+        if mx_ok(M, N, f.w):  # MX-scaled activations (e8m0 per 128 columns) on the scaled MFMA
+            from .transformer_ops import layernorm_q8_mx
+            kp = f.w.q.shape[1]
+            layernorm_q8_mx(x, ones, None, q8, sx, kp, f.eps, f.norm == NORM_RMS, rows=M, ldx=x.stride(0))
+            check(lib().gemm_fp8_qkv_scatter_mx(ptr(q8), ptr(sx), ptr(f.w.q), ptr(f.w.scale), ptr(f.bias), ptr(q),
+                                                ptr(kc), ptr(vc), ptr(pos), B, T, H, Hkv, hd, kc.shape[2], kp,
+                                                stream_ptr()), "gemm_fp8_qkv_scatter_mx")
+            return True
     if w8:
         if ones is None or q8 is None or s8 is None or N % 32 or M < 256:
             return False

@@ -75,6 +75,29 @@ def layernorm_q8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_
     return q_out
 
 
+def layernorm_q8_mx(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], q_out: torch.Tensor,
+                    sx_out: torch.Tensor, kpad: int, eps: float = 1e-5, rms: bool = False,
+                    rows: Optional[int] = None, ldx: Optional[int] = None) -> torch.Tensor:
+    """``layernorm_q8`` with MX scales: one e8m0 byte per (row, 128 columns)
+    in ``sx_out`` (``fp8.mx_scale_bytes``; csrc/kernels/common.h mx_index)
+    instead of a per-row fp32 scale — the input layout of ``fp8.linear_fp8(...,
+    sx=)``."""
+    from .fp8 import mx_scale_bytes
+    _bf16_2d(x, "layernorm_q8_mx")
+    N = x.shape[-1]
+    M = rows if rows is not None else x.numel() // N
+    ldx = ldx if ldx is not None else N
+    if w.dtype != torch.float32 or (b is not None and b.dtype != torch.float32):
+        raise TypeError("layernorm_q8_mx: fp32 weight/bias expected")
+    if N % 8 or N > 8192 or kpad < N or kpad % 128:
+        raise ValueError(f"layernorm_q8_mx: unsupported width {N} / kpad {kpad}")
+    if q_out.numel() * q_out.element_size() < M * kpad or sx_out.numel() * sx_out.element_size() < mx_scale_bytes(M, kpad):
+        raise ValueError("layernorm_q8_mx: output too small")
+    check(lib().layernorm_q8_mx(ptr(x), ldx, ptr(w), ptr(b), ptr(q_out), kpad, ptr(sx_out), M, N, kpad, eps,
+                                1 if rms else 0, stream_ptr()), "layernorm_q8_mx")
+    return q_out
+
+
 def embed(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], out: torch.Tensor,
           pos: Optional[torch.Tensor]) -> torch.Tensor:
     """out[b*T+t] = wte[idx[b,t]] (+ wpe[pos[b]+t]). idx int32 (B,T)."""

@@ -169,6 +169,11 @@ class HostStagedLink(P2PLink):
         self._thread = threading.Thread(target=run, name=f"hostlink-send-{peer}", daemon=True)
         self._thread.start()
         self._stop = weakref.finalize(self, q.put, None)
+        # not at interpreter exit: waking the thread while the process group
+        # and its gloo threads are torn down aborted the non-first ranks of the
+        # gloo_gpu ring ("terminate called without an active exception"); a
+        # daemon thread blocked in q.get() is simply dropped at exit, as before
+        self._stop.atexit = False
 
     def close(self, timeout_s: float = 30.0) -> None:
         """Stop the sender thread after the sends already queued are posted."""

@@ -35,6 +35,7 @@ import torch
 from ..models import model_info
 from ..models.llama3 import rope_tables
 from ..ops import gemm as G_
+from ..ops.fp8 import mx_ok as fp8_mx_ok
 from ..ops import transformer_ops as T_
 from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_SILU_MUL, HEAD_PART_PER_ROW, decode_workspace, fold_norm, head_argmax,
                         linear, linear_norm,
@@ -348,26 +349,38 @@ class TransformerStage(StageCompute):
                           if self.last else None)
         self.rowstat = G_.rowstats_buffer(self.max_batch, d, dev)  # decode rows only
         self.q8 = self.s8 = None
+        self.sx8 = self.q8b = self.sx8b = None
         if self.fp8:
-            from ..ops.fp8 import kpad_of
+            from ..ops.fp8 import kpad_of, mx_scale_bytes
             kmax = max(kpad_of(d), kpad_of(ffn)) * (2 if self.fp8_prefill == "split" else 1)
             self.q8 = torch.empty((ntok * kmax,), dtype=torch.uint8, device=dev)
             self.s8 = torch.empty((ntok,), dtype=torch.float32, device=dev)
+            if self.fp8_prefill == "e4m3":
+                # MX prefill (ops/fp8.py linear_fp8 sx=): the e8m0 scales of the
+                # projection inputs, and the c_fc output quantised by its own
+                # epilogue for c_proj (bytes + scales)
+                self.sx8 = torch.empty((mx_scale_bytes(ntok, kmax),), dtype=torch.uint8, device=dev)
+                self.q8b = torch.empty((ntok * kpad_of(ffn),), dtype=torch.uint8, device=dev)
+                self.sx8b = torch.empty((mx_scale_bytes(ntok, kpad_of(ffn)),), dtype=torch.uint8, device=dev)
         if self.last:
             self.buf_lnf = torch.empty((ntok, d), dtype=bf, device=dev)
             self.logits = torch.empty((ntok, self.Vpad), dtype=bf, device=dev)
             self.next_ids = torch.empty((ntok,), dtype=torch.int32, device=dev)
 
-    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None, ws=None, rs_out=None):
+    def _lin(self, x, w, b, act=ACT_NONE, residual=None, out=None, ncols=None, w_shuf=None, ws=None, rs_out=None,
+             mx_in=None):
         """``rs_out``: decode row-statistics partials of the output (see ``step``);
-        returns (out, whether they were written)."""
+        ``mx_in`` (fp8 prefill): (bytes, scales) of x already MX-quantised by its
+        producer.  Returns (out, whether the row statistics were written)."""
         from ..ops.gemm import rowstats_written
         if self.fp8:
             from ..ops.fp8 import linear_fp8, linear_w8
             if skinny_rows(x.shape[0], w.q.shape[0], w8=True):  # decode: weight-only fp8 (bf16 activations)
                 y = linear_w8(x, w, b, act, residual, out, ws=ws, rs_out=rs_out)
                 return y, rs_out is not None and rowstats_written()
-            return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8), False
+            if mx_in is not None:
+                return linear_fp8(x, w, b, act, residual, out, mx_in[0], None, prequantized=True, sx=mx_in[1]), False
+            return linear_fp8(x, w, b, act, residual, out, self.q8, self.s8, sx=self.sx8), False
         y = linear(x, w, b, act, residual, out, w_shuf=w_shuf, ws=ws, rs_out=rs_out)
         return y, rs_out is not None and rowstats_written()
 
@@ -442,7 +455,7 @@ class TransformerStage(StageCompute):
             att = self.buf_att[r0:r1]
             scattered = (T > 1 and self.cos is None and self.fuse_norm and
                          qkv_scatter_norm(h_in, L.w_qkv, a, self.buf_q, kc, vc, pos, B, T, self.H, self.Hkv,
-                                          self.hd, ones=self.ones, q8=q8, s8=s8))
+                                          self.hd, ones=self.ones, q8=q8, s8=s8, sx=self.sx8 if T > 1 else None))
             if scattered:
                 pass  # prefill (no RoPE): c_attn wrote q head-major and K / V straight into the caches
             elif self.fuse_norm:
@@ -463,13 +476,22 @@ class TransformerStage(StageCompute):
                 T_.flash_attn(self.buf_q, kc, vc, att, B, T, self.H, self.Hkv, self.hd, pos)
             _, have_rs = self._lin(att, L.w_o, L.b_o, residual=h_in, out=h, w_shuf=L.w_o_s, ws=gws, rs_out=rs)
             up_act = ACT_GELU if self.family == "gpt2" else ACT_SILU_MUL
+            mx_f = None
             if self.fuse_norm:
+                # fp8 MX prefill: the GELU c_fc quantises its own output for c_proj
+                if (self.q8b is not None and T > 1 and up_act == ACT_GELU
+                        and fp8_mx_ok(ntok, L.w_up.w.shape[0], L.w_up.w)):
+                    mx_f = (self.q8b, self.sx8b)
                 f = linear_norm(h, L.w_up, act=up_act, out=self.buf_f[r0:r1], std_buf=a, ones=self.ones, q8=q8,
-                                s8=s8, ws=gws, rs_in=rs if have_rs else None)
+                                s8=s8, ws=gws, rs_in=rs if have_rs else None,
+                                sx=self.sx8 if T > 1 else None, q_out=mx_f)
+                if mx_f is not None:
+                    f = self.buf_f[r0:r1]  # shape only: c_proj reads the e4m3 bytes in mx_f
             else:
                 T_.layernorm(h, L.ln2_w, L.ln2_b, a, self.eps, self.rms, rows=ntok)
                 f, _ = self._lin(a, L.w_up, L.b_up, act=up_act, out=self.buf_f[r0:r1])
-            _, have_rs = self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s, ws=gws, rs_out=rs)
+            _, have_rs = self._lin(f, L.w_down, L.b_down, residual=h, out=h, w_shuf=L.w_down_s, ws=gws, rs_out=rs,
+                                   mx_in=mx_f)
             h_in = h
         if not self.last:
             if out is not None:

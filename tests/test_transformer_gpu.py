@@ -1234,7 +1234,7 @@ def _gpt2_fp8_golden(st, sd):
 
 @pytest.mark.parametrize("B,T,prefill,tol_prefill,tol_decode", [
     (2, 24, "split", 2e-2, 2e-2), (2, 64, "split", 2e-2, 2e-2), (2, 192, "split", 2e-2, 2e-2),
-    (64, 512, "split", 2e-2, 2e-2), (2, 192, "e4m3", 8e-2, 4e-2)])
+    (64, 512, "split", 2e-2, 2e-2), (2, 192, "e4m3", 8e-2, 4e-2), (64, 512, "e4m3", 8e-2, 4e-2)])
 def test_gpt2_xl_fp8_two_blocks_full_width_vs_golden(B, T, prefill, tol_prefill, tol_decode):
     """GPT-2 XL at real width with fp8 weights — d 1600, 25 heads (hd 64),
     c_attn N = 4800 (partial 256-column tiles), the 50257-wide head — as one
@@ -1410,3 +1410,86 @@ def test_rowstats_decode_stage_matches_own_statistics(monkeypatch):
             logs[on] = lg
         for k in range(steps):
             assert _rel(logs[True][k], logs[False][k]) < 1e-2, (model, k)
+
+
+def _mx_dequant(q, sx, M, kp):
+    """fp32 values of MX e4m3 rows: byte x 2^(e - 127), e the e8m0 scale of
+    (row, 128-column block) at csrc/kernels/common.h mx_index."""
+    mpad = (M + 63) // 64 * 64
+    t = torch.arange(kp // 128)
+    m = torch.arange(M)
+    idx = (t[None, :] * (mpad // 64) + (m[:, None] // 64)) * 64 + (m[:, None] % 16) * 4 + (m[:, None] // 16) % 4
+    e = sx.reshape(-1)[idx.to(sx.device)].float()
+    sc = torch.exp2(e - 127.0).repeat_interleave(128, dim=1)
+    return q.reshape(-1)[:M * kp].view(M, kp).view(torch.float8_e4m3fn).float() * sc
+
+
+@pytest.mark.parametrize("M,K", [(300, 1600), (1024, 768), (8200, 1600)])
+def test_mx_quantisers(M, K):
+    """MX e4m3 (e8m0 per (row, 128 columns)): quant_rows_mx and layernorm_q8_mx
+    reconstruct their input to e4m3 rounding (<= 2^-4 relative per element,
+    block amax at <= 448 after scaling), the K padding is zero."""
+    from distributed_neural_networks_amd.ops import transformer_ops as T
+    from distributed_neural_networks_amd.ops.fp8 import kpad_of, mx_scale_bytes, quant_rows_mx
+    torch.manual_seed(5)
+    x = (torch.randn(M, K, device=DEV) * torch.rand(M, 1, device=DEV) * 8).bfloat16()
+    x[3, 100:228] *= 1000  # one loud block: its neighbours keep their own scales
+    kp = kpad_of(K)
+    q = torch.full((M, kp), 7, dtype=torch.uint8, device=DEV)
+    sx = torch.zeros(mx_scale_bytes(M, kp), dtype=torch.uint8, device=DEV)
+    quant_rows_mx(x, q, sx)
+    torch.cuda.synchronize()
+    d = _mx_dequant(q, sx, M, kp)
+    xf = x.float()
+    err = (d[:, :K] - xf).abs()
+    # per-element e4m3 rounding: <= 2^-4 of the value (normals) + the block's subnormal step
+    assert (err <= xf.abs() * 2 ** -4 + 1e-30 + d[:, :K].abs().amax(1, keepdim=True) * 2 ** -9).all()
+    assert _rel(d[:, :K], xf) < 3e-2
+    if kp > K:
+        assert int(q[:, K:].sum().item()) == 0
+    # the normalised variant
+    w = torch.ones(K, device=DEV)
+    q2 = torch.full((M, kp), 7, dtype=torch.uint8, device=DEV)
+    sx2 = torch.zeros_like(sx)
+    T.layernorm_q8_mx(x, w, None, q2, sx2, kp, 1e-5, False)
+    torch.cuda.synchronize()
+    ref = F.layer_norm(xf, (K,), eps=1e-5)
+    assert _rel(_mx_dequant(q2, sx2, M, kp)[:, :K], ref) < 3e-2
+
+
+@pytest.mark.parametrize("M,N,K,act,res", [(512, 768, 1536, 0, True), (384, 1600, 6400, 0, True),
+                                           (512, 6400, 1600, 2, False), (300, 4800, 1600, 0, False)])
+def test_gemm_fp8_mx(M, N, K, act, res):
+    """The MX W8A8 256^2 GEMM (e8m0 activation scales on the scaled MFMA's op_sel
+    bytes) against fp32 torch on the dequantised operands; with GELU also the
+    QOUT epilogue (the output quantised for the next GEMM, its own MX scales)."""
+    from distributed_neural_networks_amd.ops.fp8 import (kpad_of, linear_fp8, mx_scale_bytes, quant_rows_mx,
+                                                         quantize_weight)
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = quantize_weight(torch.randn(N, K, device=DEV) / math.sqrt(K), DEV)
+    bias = torch.randn(N, device=DEV) * 0.1
+    r = torch.randn(M, N, device=DEV).bfloat16() if res else None
+    kp = kpad_of(K)
+    q = torch.empty(M * kp, dtype=torch.uint8, device=DEV)
+    sx = torch.empty(mx_scale_bytes(M, kp), dtype=torch.uint8, device=DEV)
+    out = linear_fp8(x, w, bias, act, r, None, q, None, sx=sx)
+    torch.cuda.synchronize()
+    xd = _mx_dequant(q, sx, M, kp)[:, :K]
+    wd = w.q[:, :K].float() * w.scale[:, None]
+    ref = xd @ wd.t() + bias
+    if act == 2:
+        ref = F.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    assert _rel(out.float(), ref) < 1e-2, _rel(out.float(), ref)
+    if act == 2:  # QOUT: quantised output for the next GEMM
+        kpo = kpad_of(N)
+        qo = torch.full((M * kpo,), 7, dtype=torch.uint8, device=DEV)
+        sxo = torch.zeros(mx_scale_bytes(M, kpo), dtype=torch.uint8, device=DEV)
+        linear_fp8(x, w, bias, act, None, None, q, None, prequantized=True, sx=sx, q_out=(qo, sxo))
+        torch.cuda.synchronize()
+        back = _mx_dequant(qo, sxo, M, kpo)
+        assert _rel(back[:, :N], ref) < 4e-2, _rel(back[:, :N], ref)
+        if kpo > N:
+            assert int(qo.view(M, kpo)[:, N:].sum().item()) == 0
