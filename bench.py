@@ -57,7 +57,8 @@ BASELINE_IMG_S = 4150.0  # reference CIFAR-10 2-stage, best batch (
 METRIC = "images/sec CIFAR-10 2-stage"
 DTYPE_LABEL = {"fp32": "fp32 (bf16x3 split emulation, ~2^-16 per product)", "bf16": "bf16"}
 CPU_DTYPE_LABEL = "fp32 (torch CPU golden stages over gloo: schedule test, not a measurement)"
-FP8_LABEL = ("fp8-e4m3 weights (W8A16 decode; prefill W8A8 on fp8 MFMA, e4m3 activations with per-row scales), "
+FP8_LABEL = ("fp8-e4m3 weights (W8A16 decode; prefill W8A8 on the scaled fp8 MFMA, e4m3 activations with "
+             "MX e8m0 block scales per row x 128 columns), "
              "bf16 activations between kernels")
 
 

@@ -44,6 +44,10 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_DECODE_1P_KF"] = str(v)
     elif switch == "flash_db":  # flash prefill with double-buffered K/V LDS (attention.hip DNN_FLASH_DB)
         os.environ["DNN_FLASH_DB"] = str(v)
+    elif switch == "epi_pre":  # decode GEMM epilogue operands issued with the first loads (gemm_oneshot.h / skinny)
+        lib().gemm_set_epi_prefetch(v)
+    elif switch == "flash_pipe":  # hd-64 flash prefill software pipeline (attention.hip DNN_FLASH_PIPE)
+        os.environ["DNN_FLASH_PIPE"] = str(v)
     elif switch == "rowstats_r":  # prefill row statistics rows per wave (norm_embed.hip dnn_row_stats)
         os.environ["DNN_ROWSTATS_R"] = str(v)
     elif switch == "oneshot":  # one-shot decode GEMM: 0 off, 1 planned shapes, 2 every eligible shape

@@ -51,11 +51,16 @@ def main():
         flop = 4.0 * B * H * T * T * hd / 2
         t_o, t_r = timeit(ours), timeit(ref)
         dbs = {}
-        for db in (0, 1, 0, 1):  # double-buffered K/V LDS A/B in one process (attention.hip DNN_FLASH_DB)
-            os.environ["DNN_FLASH_DB"] = str(db)
-            t = timeit(ours)
-            dbs[f"db{db}_ms"] = round(min(t, dbs.get(f"db{db}_ms", 1e9)), 4)
+        # A/B in one process (attention.hip): DNN_FLASH_DB single vs double
+        # K/V buffer, DNN_FLASH_PIPE the hd-64 three-buffer software pipeline
+        for _ in range(3):
+            for db, pipe in ((0, 0), (1, 0), (1, 1)):
+                os.environ["DNN_FLASH_DB"], os.environ["DNN_FLASH_PIPE"] = str(db), str(pipe)
+                t = timeit(ours)
+                k = f"db{db}_pipe{pipe}_ms"
+                dbs[k] = round(min(t, dbs.get(k, 1e9)), 4)
         os.environ.pop("DNN_FLASH_DB", None)
+        os.environ.pop("DNN_FLASH_PIPE", None)
         print(json.dumps({"B": B, "T": T, "H": H, "Hkv": Hkv, "hd": hd, "ours_ms": round(t_o, 4),
                           "ours_tflops": round(flop / t_o / 1e9, 1), "torch_sdpa_ms": round(t_r, 4),
                           "torch_tflops": round(flop / t_r / 1e9, 1), **dbs}), flush=True)

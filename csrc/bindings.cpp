@@ -76,6 +76,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_rowstats(reinterpret_cast<void*>(static_cast<uintptr_t>(out)), out_ld, CP(in), in_ld);
   });
   m.def("gemm_rowstats_written", []() { return dnn_gemm_rowstats_written(); });
+  m.def("gemm_set_epi_prefetch", [](int on) { return dnn_gemm_set_epi_prefetch(on); });
   m.def("quant_fp8_mx", [](u64 x, int ldx, u64 q, int ldq, u64 sx, int M, int K, int kpad, u64 st) {
     return dnn_quant_fp8_mx(CP(x), ldx, P(q), ldq, P(sx), M, K, kpad, ST(st));
   });

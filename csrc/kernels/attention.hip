@@ -155,7 +155,18 @@ __device__ __forceinline__ int k_swz(int key, int chunk) {
 // blockIdx.x = query block the heavy workgroups were spread over the whole
 // dispatch and the last ones ran alone: GPT-2 B=64 T=512 0.1050 -> 0.0931 ms,
 // T=2048 0.140 -> 0.089, hd 128 T=4096 1.092 -> 0.781 (profiles/r4_flash_lpt_ab.jsonl)
-template <int HD, bool QKV = false, bool KV8 = false, bool DB = false>
+//
+// PIPE (hd 64, opt-in: DNN_FLASH_PIPE=1): three K/V buffers and
+// two score accumulators, so block j+1's S = K Q^T MFMAs are issued before
+// block j's softmax and P.V — the matrix pipe works through the softmax VALU
+// of the same wave instead of waiting on the S -> max -> exp -> P.V chain
+// (PMC before: MFMA 0.14 busy, profiles/r4_pmc_flash_lpt.md).
+// Measured slower, so off by default: GPT-2 B=64 T=512 0.0950 -> 0.1075 ms,
+// B=8 T=2048 0.0851 -> 0.0986, 4-stage prefill 4.21 -> 4.13 M tok/s
+// (profiles/r5_flash_pipe_ab.jsonl): the second accumulator takes the kernel
+// from 144 to 212 VGPRs and three buffers to 60 KB of LDS, i.e. from 3 to 2
+// workgroups per CU — the lost wave per SIMD overlapped the chain better.
+template <int HD, bool QKV = false, bool KV8 = false, bool DB = false, bool PIPE = false>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
                                                             const bf16_t* __restrict__ vc, bf16_t* __restrict__ o, int T,
                                                             int H, int Hkv, int S, const int* __restrict__ pos,
@@ -165,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
   using SM = FaSmem<HD>;
   // DB: two K/V buffers, one barrier per block (the block after next is staged
   // into the other buffer while this one is read)
-  __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL * (DB ? 2 : 1)];
+  __shared__ __attribute__((aligned(16))) char smem[SM::TOTAL * (PIPE ? 3 : DB ? 2 : 1)];
   char* ks = smem;
   char* vs = smem + SM::K_BYTES;
   constexpr int NKS = HD / 16;  // k-steps of the QK^T contraction
@@ -268,20 +279,21 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
       *reinterpret_cast<i32x4*>(vs + key * SM::V_STRIDE + c * 16) = pv[it];
     }
   };
-  auto compute = [&](int kb0) __attribute__((always_inline)) {
-    if (kb0 <= wave_qmax) {
-      // ---- S^T for two 32-key tiles ----
-      f32x16 sacc[2];
+  // ---- S^T for two 32-key tiles of the block staged at kbuf ----
+  auto s_mfma = [&](const char* kbuf, f32x16(&sacc)[2]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        sacc[kt] = f32x16{};
-        const int key = kt * 32 + r32;
+    for (int kt = 0; kt < 2; ++kt) {
+      sacc[kt] = f32x16{};
+      const int key = kt * 32 + r32;
 #pragma unroll
-        for (int s = 0; s < NKS; ++s) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + key * HD * 2 + (k_swz<HD>(key, 2 * s + h) << 4));
-          sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
-        }
+      for (int s = 0; s < NKS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbuf + key * HD * 2 + (k_swz<HD>(key, 2 * s + h) << 4));
+        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
       }
+    }
+  };
+  auto softmax_pv = [&](int kb0, f32x16(&sacc)[2], const char* vbuf) __attribute__((always_inline)) {
+    {
       // ---- mask + online softmax (lane = one query; keys in registers) ----
       // VALU is the bound at hd 64 (2 x 8 MFMAs per 64 keys vs ~5 VALU slots per
       // score), so: the mask only runs on blocks that cross this wave's diagonal
@@ -353,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const int dcol = dt * 32 + gsub * 16 + 4 * (lane & 3);
-            const char* a0 = vs + krow * SM::V_STRIDE + dcol * 2;
+            const char* a0 = vbuf + krow * SM::V_STRIDE + dcol * 2;
             const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a0));
             const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a0 + 8 * SM::V_STRIDE));
             bf16x8 vf;
@@ -364,7 +376,52 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const bf16_t* __rest
         }
     }
   };
-  if constexpr (!DB) {
+  auto compute = [&](int kb0) __attribute__((always_inline)) {
+    if (kb0 <= wave_qmax) {
+      f32x16 sacc[2];
+      s_mfma(ks, sacc);
+      softmax_pv(kb0, sacc, vs);
+    }
+  };
+  if constexpr (PIPE) {
+    // blocks j and j+1 staged in buffers j % 3, (j+1) % 3; block j+2 in the
+    // prefetch registers; sc = S of block j.  One barrier per block: past it
+    // every wave is done with block j-1, whose buffer takes block j+2.
+    auto buf = [&](int j) __attribute__((always_inline)) { return smem + (j % 3) * SM::TOTAL; };
+    if (kv_end > 0) {
+      fetch(0, pkA, pvA);
+      ks = buf(0);
+      vs = ks + SM::K_BYTES;
+      stage(pkA, pvA);
+      if (FA_KB < kv_end) {
+        fetch(FA_KB, pkA, pvA);
+        ks = buf(1);
+        vs = ks + SM::K_BYTES;
+        stage(pkA, pvA);
+        if (2 * FA_KB < kv_end) fetch(2 * FA_KB, pkA, pvA);
+      }
+    }
+    __syncthreads();
+    f32x16 sa[2], sb[2];
+    if (kv_end > 0) s_mfma(buf(0), sa);  // block 0 <= wave_qmax always (p0 >= 0)
+    auto iter = [&](int j, f32x16(&sc)[2], f32x16(&sn)[2]) __attribute__((always_inline)) {
+      const int kb0 = j * FA_KB;
+      __syncthreads();
+      if (kb0 + 2 * FA_KB < kv_end) {
+        ks = buf(j + 2);
+        vs = ks + SM::K_BYTES;
+        stage(pkA, pvA);
+        if (kb0 + 3 * FA_KB < kv_end) fetch(kb0 + 3 * FA_KB, pkA, pvA);
+      }
+      if (kb0 + FA_KB < kv_end && kb0 + FA_KB <= wave_qmax) s_mfma(buf(j + 1), sn);
+      if (kb0 <= wave_qmax) softmax_pv(kb0, sc, buf(j) + SM::K_BYTES);
+    };
+    for (int j = 0; j * FA_KB < kv_end; j += 2) {
+      iter(j, sa, sb);
+      if ((j + 1) * FA_KB >= kv_end) break;
+      iter(j + 1, sb, sa);
+    }
+  } else if constexpr (!DB) {
     if (kv_end > 0) fetch(0, pkA, pvA);
     for (int kb0 = 0; kb0 < kv_end; kb0 += FA_KB) {
       stage(pkA, pvA);
@@ -1293,6 +1350,14 @@ static void launch_flash(dim3 grid, hipStream_t st, const bf16_t* q, const bf16_
   // hd 128 T=512 0.251 -> 0.243, T=4096 1.123 -> 1.092 (profiles/r3_flash_double_buffer.jsonl);
   // DNN_FLASH_DB=0 keeps the single buffer (A/B)
   const char* e = getenv("DNN_FLASH_DB");
+  if constexpr (HD == 64) {  // hd 128: three buffers would leave one workgroup per CU
+    const char* ep = getenv("DNN_FLASH_PIPE");
+    if ((e == nullptr || atoi(e) != 0) && ep != nullptr && atoi(ep) != 0) {
+      hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, true, true>), grid, dim3(256), 0, st, q, kc, vc, o, T, H,
+                         Hkv, S, pos, sl2, ldq, kco, vco);
+      return;
+    }
+  }
   if (e == nullptr || atoi(e) != 0)
     hipLaunchKernelGGL((flash_attn_kernel<HD, QKV, KV8, true>), grid, dim3(256), 0, st, q, kc, vc, o, T, H, Hkv, S,
                        pos, sl2, ldq, kco, vco);

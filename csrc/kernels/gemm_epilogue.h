@@ -95,6 +95,35 @@ __device__ __forceinline__ void epi_t4(f32x4 v, int m, int n, int M, int N, void
   }
 }
 
+// epi_t4's vector path with the bias and residual already in registers (the
+// decode one-shot GEMM issues them with its first loads, so the epilogue pays
+// no memory round trip after the workgroup's reduction).  Caller: m < M,
+// n + 3 < N, 16-B aligned rows (epi_vec_ok).
+template <int ACT>
+__device__ __forceinline__ void epi_t4_pre(f32x4 v, int m, int n, void* __restrict__ Cv, int ldc, bool has_b,
+                                           const f32x4& b4, bool has_r, const bf16x4& r4, f32x4* stored = nullptr) {
+  if (has_b) v += b4;
+  if constexpr (ACT == ACT_GELU) {
+    const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+    v = f32x4{g0[0], g0[1], g1[0], g1[1]};
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (ACT == ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+  }
+  if (has_r) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += bf2f((bf16_t)r4[r]);
+  }
+  uint2 pk;
+  pk.x = pack2bf(v[0], v[1]);
+  pk.y = pack2bf(v[2], v[3]);
+  *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + (size_t)m * ldc + n) = pk;
+  if (stored != nullptr)
+    *stored = f32x4{__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u), __uint_as_float(pk.y << 16),
+                    __uint_as_float(pk.y & 0xffff0000u)};
+}
+
 // Row-statistics partial of one 16-column output tile, produced in the
 // epilogue of a residual-writing decode GEMM so that the
 // next pre-norm projection merges ~N/16 partials per row instead of

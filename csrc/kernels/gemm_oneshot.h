@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
                                                               int ntiles, int mgroups,
                                                               float2* __restrict__ rs_out = nullptr, int rs_ld = 0,
                                                               const float2* __restrict__ rs_in = nullptr,
-                                                              int rs_ld_in = 0) {
+                                                              int rs_ld_in = 0, int epi_pre = 1) {
   using Cfg = StrCfg<W8>;
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
@@ -109,6 +109,31 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     rs0 = p[0];
 #pragma unroll
     for (int i = 0; i < SPT; ++i) rsp[i] = p[min(sub + i * TPR, np - 1)];
+  }
+  // ---- epilogue operands first of all (as the row-statistics partials): the
+  // channel scales, column sums, bias and residual of the wave's output tiles
+  // land with the image, so the epilogue after the cross-wave reduction pays
+  // no memory round trip.  Uniform: vector-aligned operands, N % 4 == 0.
+  constexpr int QPW = (NTW * MT + 3) / 4;  // epilogue tiles per wave
+  const bool pre = epi_pre && !SPLIT && ACT != ACT_SILU_MUL && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
+                   ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
+  f32x4 pre_sw[QPW], pre_cs[QPW], pre_b[QPW];
+  bf16x4 pre_r[QPW];
+#pragma unroll
+  for (int k = 0; k < QPW; ++k) {
+    pre_sw[k] = pre_cs[k] = pre_b[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pre_r[k] = bf16x4{0, 0, 0, 0};
+    const int q = wave + 4 * k;
+    if (pre && q < NTW * MT) {
+      const int nn = min((tile * NTW + q / MT) * 16 + fg * 4, N - 4);
+      const int mm = min(m0 + 16 * (q % MT) + fr, M - 1);
+      if constexpr (W8) pre_sw[k] = *reinterpret_cast<const f32x4*>(sw + nn);
+      if constexpr (NORM == 2) {
+        if (colsum != nullptr) pre_cs[k] = *reinterpret_cast<const f32x4*>(colsum + nn);
+      }
+      if (bias != nullptr) pre_b[k] = *reinterpret_cast<const f32x4*>(bias + nn);
+      if (R != nullptr) pre_r[k] = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + nn);
+    }
   }
   float shift[MT], s1s[MT], s2s[MT];
 #pragma unroll
@@ -282,7 +307,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 
   const int Ns = ntiles * BN;
   const int MPT = mgroups * MP;
-  for (int q = wave; q < NTW * MT; q += 4) {
+#pragma unroll
+  for (int k = 0; k < QPW; ++k) {
+    const int q = wave + 4 * k;
+    if (q >= NTW * MT) break;  // wave-uniform
     const int j = q / MT, t = q % MT;
     f32x4 v = reinterpret_cast<const f32x4*>(os_lds)[(j * MT + t) * 64 + lane];
 #pragma unroll
@@ -314,8 +342,12 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       continue;
     } else {
       if constexpr (W8) {
+        if (pre) {
+          v *= n < N ? pre_sw[k] : f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= n + r < N ? sw[n + r] : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] *= n + r < N ? sw[n + r] : 0.f;
+        }
       }
       if constexpr (NORM != 0) {
         const float invk = 1.f / (float)kelems, d = a * invk;
@@ -327,8 +359,12 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
           rstd = st_lds[ml * 2 + 1];
         }
         if constexpr (NORM == 2) {
+          if (pre) {
+            v = rstd * (v - mean * (n < N ? pre_cs[k] : f32x4{0.f, 0.f, 0.f, 0.f}));
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = rstd * (v[r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+            for (int r = 0; r < 4; ++r) v[r] = rstd * (v[r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+          }
         } else {
           v *= rstd;
         }
@@ -336,6 +372,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
       if constexpr (ACT == ACT_SILU_MUL) {
         epi_silu_t4<false>(v, m, nb / 2, M, N / 2, Cv, ldc, vec, lane);
+      } else if (pre && nb + 15 < N) {  // wave-uniform (epi_rowstat16 shuffles): the whole 16-column tile
+        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < M) epi_t4_pre<ACT>(v, m, n, Cv, ldc, bias != nullptr, pre_b[k], R != nullptr, pre_r[k], &x);
+        if (rs_out != nullptr) epi_rowstat16(x, m, nb, M, N, rs_out, rs_ld, lane);
       } else if (rs_out != nullptr) {  // uniform: row-statistics partials of the stored tile
         f32x4 x;
         epi_t4<ACT, false>(v, m, n, M, N, Cv, ldc, bias, R, ldr, vec, nullptr, 1.f, &x);

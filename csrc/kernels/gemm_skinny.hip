@@ -104,7 +104,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
                                                            const bf16_t* __restrict__ R, int ldr, int M, int N,
                                                            int kbytes, const float* __restrict__ colsum = nullptr,
                                                            float eps = 0.f, const uint8_t* __restrict__ Wsh = nullptr,
-                                                           float2* __restrict__ rs_out = nullptr, int rs_ld = 0) {
+                                                           float2* __restrict__ rs_out = nullptr, int rs_ld = 0,
+                                                           int epi_pre = 1) {
   static_assert(NORM == NORM_NONE || !FP8, "fused norm needs bf16 activations");
   static_assert(!(FP8 && W8), "W8 = fp8 weights with bf16 activations; FP8 = both fp8");
   constexpr int AU = W8 ? 2 : 1;        // 16-B A loads per chunk per M tile (W8: a chunk is 64 k = 128 B of A)
@@ -164,6 +165,33 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     int m = t * 16 + (lane & 15);
     m = m < M ? m : M - 1;
     ap[t] = A + (size_t)m * lda_b + lg * AU;
+  }
+  // epilogue operands first of all (as gemm_oneshot.h): wave t < MT finishes M
+  // tile t after the cross-wave reduction, so it issues that tile's channel
+  // scales, column sums, bias and residual now — they land under the main loop
+  // and the epilogue pays no memory round trip after the barrier.  Uniform.
+  // (14 VGPRs per column tile: only configs with room — the software-pipelined
+  // and the wide ones spilled with it)
+  constexpr bool PRE = NT <= 2 && MT * NT * U <= 8 && !PIPE && !OUT_F32 && !FP8 && ACT != ACT_SILU_MUL;
+  constexpr int NP = PRE ? NT : 1;
+  const bool pre = PRE && epi_pre && wave < MT && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
+                   ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
+  f32x4 pre_sw[NP], pre_cs[NP], pre_b[NP];
+  bf16x4 pre_r[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    pre_sw[j] = pre_cs[j] = pre_b[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pre_r[j] = bf16x4{0, 0, 0, 0};
+    if (pre) {
+      const int nn = min(n0 + j * 16 + (lane >> 4) * 4, N - 4);
+      const int mm = min(wave * 16 + (lane & 15), M - 1);
+      if constexpr (W8) pre_sw[j] = *reinterpret_cast<const f32x4*>(sw + nn);
+      if constexpr (NORM == NORM_LN) {
+        if (colsum != nullptr) pre_cs[j] = *reinterpret_cast<const f32x4*>(colsum + nn);
+      }
+      if (bias != nullptr) pre_b[j] = *reinterpret_cast<const f32x4*>(bias + nn);
+      if (R != nullptr) pre_r[j] = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + nn);
+    }
   }
   f32x4 acc[NT][MT];
 #pragma unroll
@@ -314,8 +342,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = n0 + j * 16 + (lane >> 4) * 4;
+        if (pre) {
+          s[j] *= n < N ? pre_sw[j % NP] : f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[j][r] *= n + r < N ? sw[n + r] : 0.f;
+          for (int r = 0; r < 4; ++r) s[j][r] *= n + r < N ? sw[n + r] : 0.f;
+        }
       }
     }
     if constexpr (NORM != NORM_NONE) {
@@ -334,8 +366,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
       for (int j = 0; j < NT; ++j) {
         if constexpr (NORM == NORM_LN) {
           const int n = n0 + j * 16 + (lane >> 4) * 4;
+          if (pre) {
+            s[j] = rstd * (s[j] - mean * (n < N ? pre_cs[j % NP] : f32x4{0.f, 0.f, 0.f, 0.f}));
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[j][r] = rstd * (s[j][r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+            for (int r = 0; r < 4; ++r) s[j][r] = rstd * (s[j][r] - mean * (n + r < N ? colsum[n + r] : 0.f));
+          }
         } else {
           s[j] *= rstd;
         }
@@ -351,13 +387,19 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
         }
         epi_silu_t4<OUT_F32>(s[j], m, (n0 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
       }
-    } else if (!OUT_F32 && !FP8 && rs_out != nullptr) {  // uniform: row-statistics partials of the stored tiles
+    } else if (!OUT_F32 && !FP8 && (pre || rs_out != nullptr)) {  // uniform
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        f32x4 x;
-        epi_t4<ACT, OUT_F32>(s[j], m, n0 + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr, vec, nullptr, rs,
-                             &x);
-        epi_rowstat16(x, m, n0 + j * 16, M, N, rs_out, rs_ld, lane);
+        const int n = n0 + j * 16 + (lane >> 4) * 4;
+        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pre && n0 + j * 16 + 15 < N) {  // wave-uniform: the whole 16-column tile
+          if (m < M)
+            epi_t4_pre<ACT>(s[j], m, n, Cv, ldc, bias != nullptr, pre_b[j % NP], R != nullptr, pre_r[j % NP], &x);
+        } else {
+          epi_t4<ACT, OUT_F32>(s[j], m, n, M, N, Cv, ldc, bias, R, ldr, vec, nullptr, rs, &x);
+        }
+        // row-statistics partials of the stored tile
+        if (rs_out != nullptr) epi_rowstat16(x, m, n0 + j * 16, M, N, rs_out, rs_ld, lane);
       }
     } else {
 #pragma unroll
@@ -390,6 +432,13 @@ struct RowStatReq {
   int in_ld = 0;
 };
 static thread_local RowStatReq g_rs_req, g_rs_cur;
+// decode epilogue operands issued with the first loads (gemm_oneshot.h /
+// gemm_skinny_kernel "pre"); 0 = after the reduction, as before (A/B)
+static int g_epi_pre = 1;
+extern "C" int dnn_gemm_set_epi_prefetch(int on) {
+  g_epi_pre = on ? 1 : 0;
+  return 0;
+}
 static thread_local int g_rs_written = 0;
 
 extern "C" int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld) {
@@ -582,7 +631,7 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
     hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS>), grid, block, smem, st,
                        (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N,
                        nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups, rso, g_rs_cur.out_ld, rsi,
-                       g_rs_cur.in_ld);
+                       g_rs_cur.in_ld, g_epi_pre);
     if (rso != nullptr) g_rs_written = 1;
     return (int)hipGetLastError();
   }
@@ -692,7 +741,7 @@ static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const vo
   float2* rso = (!F32 && !FP8 && ACT != ACT_SILU_MUL) ? g_rs_cur.out : nullptr;
   hipLaunchKernelGGL((gemm_skinny_kernel<ACT, F32, MT, NT, FP8, U, PIPE, NORM, W8, MS>), dim3(groups), dim3(64 * ks), smem,
                      st, (const uint8_t*)A, lda_b, sa, (const uint8_t*)W, ldw_b, sw, C, ldc, bias, (const bf16_t*)R,
-                     ldr, M, N, kbytes, colsum, eps, (const uint8_t*)Wsh, rso, g_rs_cur.out_ld);
+                     ldr, M, N, kbytes, colsum, eps, (const uint8_t*)Wsh, rso, g_rs_cur.out_ld, g_epi_pre);
   if (rso != nullptr) g_rs_written = 1;
   return (int)hipGetLastError();
 }

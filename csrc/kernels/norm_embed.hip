@@ -144,9 +144,8 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const bf16_t* __restrict
 // still in registers) is scaled by its own amax/448 and written as OCP e4m3
 // with the K padding zeroed, plus the per-row scale — the layout
 // quant_fp8_rows produces — so the activation never round-trips through bf16.
-// R rows per wave (prefill, tens of thousands of rows): every load of the R
-// rows is issued before the first reduction (row_stats_kernel's fix: one row
-// per wave left 32768 latency-bound waves in four residency rounds).
+// R rows per wave (DNN_NORMQ8_R; default 1 — with gamma / beta loaded once
+// per wave next to the rows, more rows per wave only lowered occupancy).
 // MX: one e8m0 scale per (row, 128-column block) instead of the row scale
 // (common.h mx_index; the 16 lanes of a block agree on it by 4 shuffles).
 template <int NC, bool RMS, bool SPLIT = false, int R = 1, bool MX = false>
@@ -166,6 +165,25 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__
     for (int i = 0; i < NC; ++i) {
       const int c = (lane + 64 * i) * 8;
       raw[r][i] = c < N ? *reinterpret_cast<const bf16x8*>(xr + c) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  // gamma / beta as 16-B vectors issued with the rows and shared by the R rows
+  // (per-element loads after the reductions were one dependent round trip per
+  // row and column chunk: 103 us per GPT-2 XL prefill pass against 28 us for the
+  // plain MX quantiser, profiles/r5_gpt2xl_fp8_b64_kernels_mx.md)
+  f32x4 wpf[NC][2], bpf[NC][2];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    wpf[i][0] = wpf[i][1] = bpf[i][0] = bpf[i][1] = z;
+    if (c < N) {
+      wpf[i][0] = *reinterpret_cast<const f32x4*>(w + c);
+      wpf[i][1] = *reinterpret_cast<const f32x4*>(w + c + 4);
+      if (!RMS && b != nullptr) {
+        bpf[i][0] = *reinterpret_cast<const f32x4*>(b + c);
+        bpf[i][1] = *reinterpret_cast<const f32x4*>(b + c + 4);
+      }
     }
   }
 #pragma unroll
@@ -199,8 +217,7 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(const bf16_t* __restrict__
       if (c < N) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float bj = (!RMS && b != nullptr) ? b[c + j] : 0.f;
-          v[i][j] = (v[i][j] - mean) * rstd * w[c + j] + bj;
+          v[i][j] = (v[i][j] - mean) * rstd * wpf[i][j >> 2][j & 3] + bpf[i][j >> 2][j & 3];
           amax = fmaxf(amax, fabsf(v[i][j]));
         }
       }
@@ -368,8 +385,11 @@ extern "C" int dnn_layernorm_q8_mx(const void* x, int ldx, const float* w, const
     return -1;
   if (M <= 0) return 0;
   const int nc = (kpad / 8 + 63) / 64;
+  // one row per wave: with gamma / beta issued with the rows, GPT-2 XL's
+  // 32768 x 1600 pass takes 38.5 us at R = 1, 45.7 at 2, 52.9 at 4
+  // (profiles/r5_norm_q8_probe.jsonl); DNN_NORMQ8_R=2/4 for A/B
   const char* re = getenv("DNN_NORMQ8_R");
-  const int R = re != nullptr ? atoi(re) : (M >= 8192 && nc <= 4 ? 4 : 1);
+  const int R = re != nullptr ? atoi(re) : 1;
   dim3 blk(256);
 #define LQM(NCV, RV)                                                                                              \
   {                                                                                                               \
@@ -383,6 +403,7 @@ extern "C" int dnn_layernorm_q8_mx(const void* x, int ldx, const float* w, const
 #define LQ(NCV)                         \
   if (nc <= NCV) {                      \
     if (R == 4 && NCV <= 4) LQM(NCV, 4) \
+    if (R == 2 && NCV <= 4) LQM(NCV, 2) \
     LQM(NCV, 1)                         \
   }
   LQ(1) LQ(2) LQ(4) LQ(8) LQ(16)
@@ -396,10 +417,9 @@ extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const fl
   if (N % 8 != 0 || N > 8192 || kpad < N || kpad % 8 != 0 || ldq < kpad * (split ? 2 : 1) || sq == nullptr) return -1;
   if (M <= 0) return 0;
   const int nc = (kpad / 8 + 63) / 64;
-  // 4 rows per wave once the grid would exceed one residency round (as
-  // dnn_row_stats); DNN_NORMQ8_R=1 forces one row per wave (A/B)
+  // one row per wave (as dnn_layernorm_q8_mx); DNN_NORMQ8_R=2/4 for A/B
   const char* re = getenv("DNN_NORMQ8_R");
-  const int R = re != nullptr ? atoi(re) : (M >= 8192 && nc <= 4 ? 4 : 1);
+  const int R = re != nullptr ? atoi(re) : 1;
   dim3 blk(256);
 #define LQK(NCV, RV)                                                                                               \
   {                                                                                                                \
@@ -421,6 +441,7 @@ extern "C" int dnn_layernorm_q8(const void* x, int ldx, const float* w, const fl
 #define LQ(NCV)                      \
   if (nc <= NCV) {                   \
     if (R == 4 && NCV <= 4) LQK(NCV, 4) \
+    if (R == 2 && NCV <= 4) LQK(NCV, 2) \
     LQK(NCV, 1)                      \
   }
   LQ(1) LQ(2) LQ(4) LQ(8) LQ(16)

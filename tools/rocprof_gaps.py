@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--after", default="flash_attn", help="decode region starts after the last kernel matching this")
+    ap.add_argument("--detail", default="argmax_final",
+                    help="also list every gap after the kernels matching this (sorted, us)")
     args = ap.parse_args()
     db = glob.glob(os.path.join(args.dir, "**", "*results.db"), recursive=True)[0]
     con = sqlite3.connect(db)
@@ -41,16 +43,28 @@ def main():
           f"idle between kernels {sum(gaps) / 1e3:.1f} us ({100 * sum(gaps) / span:.1f} %), "
           f"mean gap {sum(gaps) / len(gaps) / 1e3:.2f} us")
     print()
-    per = collections.defaultdict(lambda: [0, 0, 0])
+    # the median gap is the steady-state boundary; the mean also carries the
+    # few host-side pauses of the timing loop (synchronise, timers)
+    srt = sorted(gaps)
+    print(f"median gap {srt[len(srt) // 2] / 1e3:.2f} us, gaps under 20 us: "
+          f"{sum(g for g in gaps if g < 20e3) / 1e3:.1f} us "
+          f"({100 * sum(g for g in gaps if g < 20e3) / span:.1f} % of the span)")
+    print()
+    per = collections.defaultdict(lambda: [0, 0, []])
     for i, (n, s, e) in enumerate(dec[:-1]):
         p = per[short(n)]
         p[0] += 1
         p[1] += e - s
-        p[2] += gaps[i]
-    print("| kernel | calls | mean us | mean gap after us |")
-    print("|---|---|---|---|")
+        p[2].append(gaps[i])
+    if args.detail:
+        det = sorted(round(gaps[i] / 1e3, 2) for i, (n, _, _) in enumerate(dec[:-1]) if args.detail in n)
+        print(f"gaps after `{args.detail}` (sorted, us): {det}")
+        print()
+    print("| kernel | calls | mean us | mean gap after us | median gap after us |")
+    print("|---|---|---|---|---|")
     for n, (c, d, g) in sorted(per.items(), key=lambda kv: -kv[1][1]):
-        print(f"| `{n}` | {c} | {d / c / 1e3:.2f} | {g / c / 1e3:.2f} |")
+        med = sorted(g)[len(g) // 2]
+        print(f"| `{n}` | {c} | {d / c / 1e3:.2f} | {sum(g) / c / 1e3:.2f} | {med / 1e3:.2f} |")
 
 
 if __name__ == "__main__":
