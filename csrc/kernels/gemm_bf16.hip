@@ -739,11 +739,18 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
-            f32x4 cs, bs;
+            // 16-B channel-scale / bias loads (per-element ones were 8 scalar
+            // loads per quad)
+            f32x4 cs, bs = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (n + 3 < N) {
+              cs = *reinterpret_cast<const f32x4*>(sw + n);
+              if (bias != nullptr) bs = *reinterpret_cast<const f32x4*>(bias + n);
+            } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              cs[r] = n + r < N ? sw[n + r] : 0.f;
-              bs[r] = (bias != nullptr && n + r < N) ? bias[n + r] : 0.f;
+              for (int r = 0; r < 4; ++r) {
+                cs[r] = n + r < N ? sw[n + r] : 0.f;
+                bs[r] = (bias != nullptr && n + r < N) ? bias[n + r] : 0.f;
+              }
             }
             f32x4 v = acc[mq][nq][i][j] * cs + bs;
             const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
