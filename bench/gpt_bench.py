@@ -49,8 +49,9 @@ def parse(argv=None):
     ap.add_argument("--kv_scale", default="calibrated", choices=["calibrated", "unit"],
                     help="fp8 KV cache scale: per-layer, from the first prefill's amax, or unit")
     ap.add_argument("--fp8_prefill", default="e4m3", choices=["split", "e4m3"],
-                    help="fp8 weights: prefill activations split (e4m3 hi + residual, ~0.1 %% logits error) or one "
-                         "e4m3 byte (2x faster prefill GEMMs, ~6 %% logits error)")
+                    help="fp8 weights: prefill activations as one e4m3 byte with MX block scales (default) or "
+                         "split (e4m3 hi + residual, 2x the prefill MFMA work); GPT-2 XL 48 layers vs the fp32 model "
+                         "on the unquantised weights: prefill logits 0.115 vs 0.096 (the fp8 weights dominate)")
     ap.add_argument("--no_graph", action="store_true", help="eager decode launches (no HIP graph)")
     ap.add_argument("--cpu", action="store_true", help="schedule test mode: gloo + fp32 golden stages on CPU")
     ap.add_argument("--gloo_gpu", action="store_true",

@@ -115,7 +115,9 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   // land with the image, so the epilogue after the cross-wave reduction pays
   // no memory round trip.  Uniform: vector-aligned operands, N % 4 == 0.
   constexpr int QPW = (NTW * MT + 3) / 4;  // epilogue tiles per wave
-  const bool pre = epi_pre && !SPLIT && ACT != ACT_SILU_MUL && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
+  // (14 VGPRs per tile: up to 2 tiles per wave; the 64 x 64 tiles spilled with 4)
+  constexpr bool PRE = QPW <= 2 && !SPLIT && ACT != ACT_SILU_MUL;
+  const bool pre = PRE && epi_pre && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
                    ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
   f32x4 pre_sw[QPW], pre_cs[QPW], pre_b[QPW];
   bf16x4 pre_r[QPW];

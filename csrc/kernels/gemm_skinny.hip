@@ -528,7 +528,7 @@ static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const flo
   const long long threads = (long long)M * ((NO + 3) / 4);
   hipLaunchKernelGGL((gemm_stream_reduce<ACT, NORM, W8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
                      (const float*)ws, splitk, MP, ntiles * BN, (const uint8_t*)A, lda_b, sw, colsum, eps, kelems, C,
-                     ldc, bias, (const bf16_t*)R, ldr, M, N);
+                     ldc, bias, (const bf16_t*)R, ldr, M, N, g_epi_pre);
   return (int)hipGetLastError();
 }
 
@@ -642,7 +642,7 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
   const long long threads = (long long)M * ((NO + 3) / 4);
   hipLaunchKernelGGL((gemm_stream_reduce<ACT, NORM, W8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
                      (const float*)ws, splitk, mgroups * MP, ntiles * BN, (const uint8_t*)A, lda_b, sw, colsum, eps,
-                     kelems, C, ldc, bias, (const bf16_t*)R, ldr, M, N);
+                     kelems, C, ldc, bias, (const bf16_t*)R, ldr, M, N, g_epi_pre);
   return (int)hipGetLastError();
 }
 

@@ -124,6 +124,12 @@ __device__ __forceinline__ f32x4 str_combine4(const float* slab, int splitk, int
     const float w = s < splitk ? 1.f : 0.f;
     v += f32x4{part[s][0][0], part[s][0][1], part[s][1][0], part[s][1][1]} * w;
   }
+  if (n + 3 < N && ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0) {
+    if constexpr (W8) v *= *reinterpret_cast<const f32x4*>(sw + n);
+    if constexpr (NORM == 2) v = rstd * (v - mean * *reinterpret_cast<const f32x4*>(colsum + n));
+    if constexpr (NORM == 1) v *= rstd;
+    return v;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const bool ok = n + r < N;
@@ -142,7 +148,7 @@ __device__ __forceinline__ void str_combine_item(const float* slab, int splitk, 
                                                  const float* __restrict__ sw, const float* __restrict__ colsum,
                                                  float eps, int kelems, void* __restrict__ Cv, int ldc,
                                                  const float* __restrict__ bias, const bf16_t* __restrict__ R, int ldr,
-                                                 int M, int N) {
+                                                 int M, int N, bool pre = true) {
   float mean = 0.f, rstd = 1.f;
   if constexpr (NORM != 0)
     str_row_norm<NORM, SC1>(slab + (size_t)splitk * MP * Ns, splitk, MP, tile, m, A, lda_b, kelems, eps, mean, rstd);
@@ -158,8 +164,20 @@ __device__ __forceinline__ void str_combine_item(const float* slab, int splitk, 
       if (o + r < NO) C[r] = f2bf(silu(gt[r]) * up[r]);
   } else {
     if (o >= N) return;
+    const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
+    if (pre && vec && o + 3 < N && m < M) {
+      // bias and residual issued with the partials: one memory round trip for
+      // the item instead of two (Llama-3 down projection + residual)
+      f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x4 r4 = bf16x4{0, 0, 0, 0};
+      if (bias != nullptr) b4 = *reinterpret_cast<const f32x4*>(bias + o);
+      if (R != nullptr) r4 = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + o);
+      epi_t4_pre<ACT>(str_combine4<NORM, W8, SC1>(slab, splitk, MP, Ns, m, o, N, sw, colsum, mean, rstd), m, o, Cv,
+                      ldc, bias != nullptr, b4, R != nullptr, r4);
+      return;
+    }
     epi_t4<ACT, false>(str_combine4<NORM, W8, SC1>(slab, splitk, MP, Ns, m, o, N, sw, colsum, mean, rstd), m, o, M,
-                       N, Cv, ldc, bias, R, ldr, epi_vec_ok(Cv, ldc, bias, R, ldr));
+                       N, Cv, ldc, bias, R, ldr, vec);
   }
 }
 
@@ -466,13 +484,23 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const uint8_t* __re
       for (int t = 0; t < MT; ++t) {
         f32x4 v = acc[j][t];
         const int m = 16 * t + fr;
+        const bool v4 = n + 3 < N &&
+                        ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
         if constexpr (W8) {
+          if (v4) {
+            v *= *reinterpret_cast<const f32x4*>(sw + n);
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] *= n + r < N ? sw[n + r] : 0.f;
+            for (int r = 0; r < 4; ++r) v[r] *= n + r < N ? sw[n + r] : 0.f;
+          }
         }
         if constexpr (NORM == 2) {
+          if (v4) {
+            v = rstd[t] * (v - mean[t] * *reinterpret_cast<const f32x4*>(colsum + n));
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = rstd[t] * (v[r] - mean[t] * (n + r < N ? colsum[n + r] : 0.f));
+            for (int r = 0; r < 4; ++r) v[r] = rstd[t] * (v[r] - mean[t] * (n + r < N ? colsum[n + r] : 0.f));
+          }
         } else if constexpr (NORM == 1) {
           v *= rstd[t];
         }
@@ -495,14 +523,15 @@ __global__ __launch_bounds__(256) void gemm_stream_reduce(const float* __restric
                                                           const float* __restrict__ colsum, float eps, int kelems,
                                                           void* __restrict__ Cv, int ldc,
                                                           const float* __restrict__ bias,
-                                                          const bf16_t* __restrict__ R, int ldr, int M, int N) {
+                                                          const bf16_t* __restrict__ R, int ldr, int M, int N,
+                                                          int epi_pre = 1) {
   const int NO = ACT == ACT_SILU_MUL ? N / 2 : N;
   const int per_row = (NO + 3) / 4;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   const int m = idx / per_row, o = (idx - m * per_row) * 4;
   if (m >= M) return;
   str_combine_item<ACT, NORM, W8, false>(slab, splitk, MP, Ns, 0, m, o, A, lda_b, sw, colsum, eps, kelems, Cv, ldc,
-                                         bias, R, ldr, M, N);
+                                         bias, R, ldr, M, N, epi_pre != 0);
 }
 
 }  // namespace dnn
