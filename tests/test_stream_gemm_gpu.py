@@ -267,3 +267,53 @@ def test_oneshot_pinned_configs(cfg):
         torch.cuda.synchronize()
         ref = x.float() @ wref.T
         assert ((out.float() - ref).norm() / ref.norm()).item() < 1e-2, (cfg, w8)
+
+
+@pytest.mark.parametrize("path", ["oneshot", "skinny"])
+@pytest.mark.parametrize("N,K,w8", [(2304, 768, False), (768, 3072, False), (4800, 1600, True), (1600, 6400, True)])
+@pytest.mark.parametrize("epi", ["bias_res", "ln_gelu"])
+def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
+    """Epilogue operands issued with the first loads (gemm_oneshot.h /
+    gemm_skinny_kernel ``pre``, the default) change when the channel scales,
+    column sums, bias and residual arrive, not the operations: outputs match
+    the late-load epilogue (``gemm_set_epi_prefetch(0)``) up to the compiler's
+    mul-add contraction (fp32 ulps, so a rare bf16 rounding flip)."""
+    from distributed_neural_networks_amd.ops._lib import lib
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
+                                                          linear_norm, set_oneshot_gemm, shuffle_weight)
+    dev = torch.device("cuda", 0)
+    M = 64
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
+    w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    ws = decode_workspace(dev)
+    if epi == "ln_gelu":
+        f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
+                      bias, False, 1e-5, dev, w8)
+        attach_shuffled(f)
+        run = lambda: linear_norm(x, f, act="gelu", ws=ws)  # noqa: E731
+    elif w8:
+        q = quantize_weight(w, dev)
+        q.shuf = shuffle_weight(q.q[:, :K])
+        run = lambda: linear_w8(x, q, bias, 0, res, ws=ws)  # noqa: E731
+    else:
+        wb = w.bfloat16()
+        wsh = shuffle_weight(wb)
+        run = lambda: linear(x, wb, bias, None, res, w_shuf=wsh, ws=ws)  # noqa: E731
+    outs = []
+    try:
+        set_oneshot_gemm(2 if path == "oneshot" else 0)
+        for on in (0, 1):
+            lib().gemm_set_epi_prefetch(on)
+            outs.append(run().clone())
+        torch.cuda.synchronize()
+    finally:
+        lib().gemm_set_epi_prefetch(1)
+        set_oneshot_gemm(1)
+    a, b = outs[0].float(), outs[1].float()
+    ulp = torch.maximum(b.abs(), torch.full_like(b, 2.0 ** -126)) * 2.0 ** -7  # one bf16 step
+    assert bool(((a - b).abs() <= ulp).all()), (a - b).abs().max().item()
+    assert (a != b).float().mean().item() < 1e-3
