@@ -77,6 +77,10 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("gemm_rowstats_written", []() { return dnn_gemm_rowstats_written(); });
   m.def("gemm_set_epi_prefetch", [](int on) { return dnn_gemm_set_epi_prefetch(on); });
+  m.def("gemm_oneshot_ablate", [](u64 A, int lda, u64 Wsh, u64 sw, u64 C, int ldc, int M, int N, int K, int cfg,
+                                  int abl, u64 st) {
+    return dnn_gemm_oneshot_ablate(CP(A), lda, CP(Wsh), CFP(sw), P(C), ldc, M, N, K, cfg, abl, ST(st));
+  });
   m.def("quant_fp8_mx", [](u64 x, int ldx, u64 q, int ldq, u64 sx, int M, int K, int kpad, u64 st) {
     return dnn_quant_fp8_mx(CP(x), ldx, P(q), ldq, P(sx), M, K, kpad, ST(st));
   });

@@ -69,7 +69,9 @@ int dnn_gemm_fp8_qkv_scatter_mx(const void* A8, const void* sx, const void* W8, 
 // producer-side row statistics for the next decode GEMM call of this thread (gemm_skinny.hip)
 int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld);
 int dnn_gemm_rowstats_written();
-int dnn_gemm_set_epi_prefetch(int on);  // decode GEMM epilogue operands with the first loads (1, default) / after (0)
+int dnn_gemm_set_epi_prefetch(int on);
+int dnn_gemm_oneshot_ablate(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
+                            int K, int cfg, int abl, hipStream_t st);  // probe: one-shot launch with parts removed  // decode GEMM epilogue operands with the first loads (1, default) / after (0)
 // prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,

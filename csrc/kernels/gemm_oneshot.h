@@ -56,7 +56,11 @@ constexpr int os_lds_bytes() {
   return 4 * STEPS * MT * 16 * OS_SB + 4 * MT * 2 * 16 * 4;  // 4 wave images + row statistics
 }
 
-template <int MT, int NTW, bool W8, int NORM, int ACT, bool SPLIT, int STEPS>
+// ABL (probe only, bench/probes/oneshot_anatomy.py; 0 in every product launch):
+// bit 1 no weight loads, 2 no activation image, 4 no MFMAs, 8 no epilogue
+// stores, 32 return at once (the launch alone), 64 no cross-wave reduction
+// (each wave's own partial goes to the epilogue) — what each part costs.
+template <int MT, int NTW, bool W8, int NORM, int ACT, bool SPLIT, int STEPS, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                               const uint8_t* __restrict__ Wsh,
                                                               const float* __restrict__ sw, void* __restrict__ Cv,
@@ -68,6 +72,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
                                                               float2* __restrict__ rs_out = nullptr, int rs_ld = 0,
                                                               const float2* __restrict__ rs_in = nullptr,
                                                               int rs_ld_in = 0, int epi_pre = 1) {
+  if constexpr ((ABL & 32) != 0) return;
   using Cfg = StrCfg<W8>;
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
   i32x4 wv[NTW][CPW];
 #pragma unroll
-  for (int s = 0; s < STEPS; ++s) {
+  for (int s = 0; s < (ABL & 2 ? 0 : STEPS); ++s) {
 #pragma unroll
     for (int p = 0; p < GPS; ++p) {
       const int r = 2 * p + (lane >> 5);  // row inside the step image
@@ -179,7 +184,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 #pragma unroll
       for (int c = s * CS; c < (s + 1) * CS; ++c) {
         const int cc = min(min(w0 + c, max(w1, w0 + 1) - 1), nch - 1);
-        wv[j][c] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + (size_t)cc * 1024));
+        if constexpr (ABL & 1)
+          wv[j][c] = i32x4{cc, j, 0, 0};
+        else
+          wv[j][c] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + (size_t)cc * 1024));
       }
     }
   }
@@ -242,6 +250,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (ABL & 4) continue;
     const bool valid = c < nvalid;  // wave-uniform
     if (!valid) {
 #pragma unroll
@@ -301,11 +310,13 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   // image (its fragment reads are complete), then every wave reads all four
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   f32x4* red = reinterpret_cast<f32x4*>(img);
+  if constexpr ((ABL & 64) == 0) {
 #pragma unroll
-  for (int j = 0; j < NTW; ++j)
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
-    for (int t = 0; t < MT; ++t) red[(j * MT + t) * 64 + lane] = acc[j][t];
-  __syncthreads();
+      for (int t = 0; t < MT; ++t) red[(j * MT + t) * 64 + lane] = acc[j][t];
+    __syncthreads();
+  }
 
   const int Ns = ntiles * BN;
   const int MPT = mgroups * MP;
@@ -314,9 +325,14 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     const int q = wave + 4 * k;
     if (q >= NTW * MT) break;  // wave-uniform
     const int j = q / MT, t = q % MT;
-    f32x4 v = reinterpret_cast<const f32x4*>(os_lds)[(j * MT + t) * 64 + lane];
+    f32x4 v;
+    if constexpr ((ABL & 64) != 0) {
+      v = acc[j][t];
+    } else {
+      v = reinterpret_cast<const f32x4*>(os_lds)[(j * MT + t) * 64 + lane];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) v += reinterpret_cast<const f32x4*>(os_lds + w * IMG)[(j * MT + t) * 64 + lane];
+      for (int w = 1; w < 4; ++w) v += reinterpret_cast<const f32x4*>(os_lds + w * IMG)[(j * MT + t) * 64 + lane];
+    }
     const int ml = 16 * t + fr;       // row inside the m-group
     const int m = m0 + ml;
     const int nb = (tile * NTW + j) * 16;
@@ -372,7 +388,9 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
         }
       }
       const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
-      if constexpr (ACT == ACT_SILU_MUL) {
+      if constexpr (ABL & 8) {
+        if (v[0] == 12345.f) reinterpret_cast<float*>(Cv)[0] = v[1];  // keep the sums live, store nothing
+      } else if constexpr (ACT == ACT_SILU_MUL) {
         epi_silu_t4<false>(v, m, nb / 2, M, N / 2, Cv, ldc, vec, lane);
       } else if (pre && nb + 15 < N) {  // wave-uniform (epi_rowstat16 shuffles): the whole 16-column tile
         f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -611,7 +611,7 @@ static bool os_plan(int M, int N, int kbytes, bool have_ws, long long ws_bytes, 
   return true;
 }
 
-template <int MT, int NTW, int STEPS, int ACT, int NORM, bool W8>
+template <int MT, int NTW, int STEPS, int ACT, int NORM, bool W8, int ABL = 0>
 static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float* sw, void* C, int ldc,
                          const float* bias, const void* R, int ldr, int M, int N, int kbytes, const float* colsum,
                          float eps, hipStream_t st, void* ws, int splitk) {
@@ -628,7 +628,7 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
     // output); merged partials of the input when they fit OS_RS_SPT per thread
     float2* rso = ACT != ACT_SILU_MUL ? g_rs_cur.out : nullptr;
     const float2* rsi = (NORM != 0 && (kelems + 15) / 16 <= OS_RS_SPT * (256 / MP)) ? g_rs_cur.in : nullptr;
-    hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS>), grid, block, smem, st,
+    hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, ABL>), grid, block, smem, st,
                        (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N,
                        nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups, rso, g_rs_cur.out_ld, rsi,
                        g_rs_cur.in_ld, g_epi_pre);
@@ -702,6 +702,45 @@ extern "C" int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, c
                                            0.f, st, ws)
             : launch_os<ACT_NONE, 0, false>(c, A, lda * 2, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N, kbytes, nullptr,
                                             0.f, st, ws);
+}
+
+// Anatomy probe (bench/probes/oneshot_anatomy.py): the planned one-shot
+// launch with parts removed (gemm_oneshot_kernel ABL); cfg 0 = 2/4/2 W8 (GPT-2
+// XL c_attn, c_fc), 1 = 1/2/2 W8 (XL O), 2 = 2/2/1 bf16 (GPT-2 c_attn, c_fc).
+extern "C" int dnn_gemm_oneshot_ablate(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc,
+                                       int M, int N, int K, int cfg, int abl, hipStream_t st) {
+  const bool w8 = cfg != 2;
+  const int kbytes = w8 ? K : K * 2, lb = lda * (w8 ? 2 : 2);
+  if (!os_eligible<ACT_NONE, 0, false>(A, lb, Wsh, M, kbytes) || (w8 && sw == nullptr)) return -1;
+#define ABLC(CFG, MTV, NTV, SV, W8V)                                                                                   \
+  if (cfg == CFG) {                                                                                                    \
+    switch (abl) {                                                                                                     \
+      case 0: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 0>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 1: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 1>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 2: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 2>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 3: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 3>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 4: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 4>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 8: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 8>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 7: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 7>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, N,  \
+                                                                     kbytes, nullptr, 0.f, st, nullptr, 1);           \
+      case 32: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 32>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, \
+                                                                       N, kbytes, nullptr, 0.f, st, nullptr, 1);      \
+      case 64: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 64>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, \
+                                                                       N, kbytes, nullptr, 0.f, st, nullptr, 1);      \
+      case 67: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 67>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, \
+                                                                       N, kbytes, nullptr, 0.f, st, nullptr, 1);      \
+      default: return -2;                                                                                              \
+    }                                                                                                                  \
+  }
+  ABLC(0, 2, 4, 2, true) ABLC(1, 1, 2, 2, true) ABLC(2, 2, 2, 1, false)
+#undef ABLC
+  return -2;
 }
 
 template <int ACT, int NORM, bool W8>
