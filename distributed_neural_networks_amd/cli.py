@@ -30,6 +30,7 @@ import argparse
 import asyncio
 import os
 import sys
+import time
 import traceback
 from typing import List, Optional, Tuple
 
@@ -297,8 +298,15 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
                 await client.close()
             return 1
     rc = 0
+    # a CIFAR request is micro_batch_size x num_microbatches images (1 by default:
+    # the reference's single image); with --metrics, stage 0 records every
+    # request's end-to-end latency (forward, hop(s), result back) — the number
+    # BASELINE.md's survey measured for the reference
+    rows = ctx.pipeline.micro_batch_size * ctx.pipeline.num_microbatches if fam == "cifar" else 1
+    met = getattr(getattr(args, "_servicer", None), "metrics", None)
     for r in range(args.num_requests):
-        x = load_image(args.input_image, nid) if fam == "cifar" else make_prompt(ctx, args.prompt)
+        x = cifar_request(args, nid, rows, r) if fam == "cifar" else make_prompt(ctx, args.prompt)
+        t_req = time.perf_counter()
         log(f"[{nid}] Running model part {ctx.part_index}...")
         loop = asyncio.get_running_loop()
         out, pred = await loop.run_in_executor(None, fwd, x)
@@ -324,6 +332,8 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
                 log(f"[{nid}] Final result status received, but tensor not included in response.")
                 rc = 1
             else:
+                if met is not None:
+                    met.record(time.perf_counter() - t_req, rows)
                 p = pred.tolist()
                 log(f"[{nid}] ***** FINAL PREDICTION (Index): {p[0] if len(p) == 1 else p} *****")
         except Exception as e:  # noqa: BLE001
