@@ -30,6 +30,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", default="1,255,1024")
+    ap.add_argument("--microbatches", type=int, default=1,
+                    help="a request of B images as this many microbatches streamed down the pipeline (1 = the "
+                         "reference's one tensor per request)")
     ap.add_argument("--requests", type=int, default=60)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--port", type=int, default=50161)
@@ -53,7 +56,8 @@ def main():
         cfg = {"nodes": [{"id": "node1", "address": f"127.0.0.1:{p0}", "part_index": 0},
                          {"id": "node2", "address": f"127.0.0.1:{p1}", "part_index": 1}],
                "model_weights": wpath, "num_parts": 2, "return_to_node_id": "node1", "transport": "grpc",
-               "model": "cifar10", "micro_batch_size": B, "num_microbatches": 1}
+               "model": "cifar10", "micro_batch_size": -(-B // max(1, min(a.microbatches, B))),
+               "num_microbatches": max(1, min(a.microbatches, B))}
         cpath = os.path.join(tmp, f"cfg_{B}.json")
         with open(cpath, "w") as f:
             json.dump(cfg, f)
@@ -75,7 +79,9 @@ def main():
                 srv.wait()
             slog.close()
         met = [ln for ln in r.stdout.splitlines() if ln.startswith("METRICS ")]
-        out = {"config": "cifar10 2-stage, CPU, localhost gRPC (BASELINE config 1)", "batch": B,
+        mb = cfg["num_microbatches"]
+        B = cfg["micro_batch_size"] * mb  # images per request
+        out = {"config": "cifar10 2-stage, CPU, localhost gRPC (BASELINE config 1)", "batch": B, "microbatches": mb,
                "requests": a.requests, "intra_op_threads": a.threads, "rc": r.returncode}
         if r.returncode != 0 or not met:
             out["error"] = (r.stdout + r.stderr)[-800:]

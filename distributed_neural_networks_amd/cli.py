@@ -309,6 +309,13 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
         t_req = time.perf_counter()
         log(f"[{nid}] Running model part {ctx.part_index}...")
         loop = asyncio.get_running_loop()
+        if fam == "cifar" and client is not None and ctx.pipeline.num_microbatches > 1:
+            # microbatches streamed down the pipeline: microbatch k's hop and the
+            # downstream stages run while this stage computes k + 1 (the
+            # servicers serialise their compute, not their transfers)
+            ok = await _initiate_microbatches(ctx, args, client, fwd, x, r, t_req, met)
+            rc = rc if ok else 1
+            continue
         out, pred = await loop.run_in_executor(None, fwd, x)
         if client is None:  # single-stage pipeline
             p = pred.tolist()
@@ -341,6 +348,39 @@ async def initiate(ctx: NodeContext, args, stage, fwd, fam) -> int:
             rc = 1
     await client.close() if client is not None else None
     return rc
+
+
+async def _initiate_microbatches(ctx: NodeContext, args, client, fwd, x, r: int, t_req: float, met) -> bool:
+    """One CIFAR request as ``num_microbatches`` SendTensor calls in flight at
+    once (``initiate``): per-row predictions concatenated in microbatch order."""
+    from .control.service import decode_prediction
+    from .wire import codec, proto
+    import grpc
+    nid, mbs = ctx.node_id, ctx.pipeline.micro_batch_size
+    loop = asyncio.get_running_loop()
+    sends = []
+    for k in range((x.shape[0] + mbs - 1) // mbs):
+        out, _ = await loop.run_in_executor(None, fwd, x[k * mbs:(k + 1) * mbs])
+        out = out.detach().cpu()
+        if out.is_floating_point():
+            out = out.float()
+        req = proto.TensorRequest(request_id=f"{ctx.pipeline.model}_pipe_{ctx.num_parts}node_{r:03d}_mb{k}",
+                                  tensor=codec.encode(out))
+        sends.append(asyncio.ensure_future(client.send_tensor(req)))
+    try:
+        resps = await asyncio.gather(*sends)
+    except grpc.aio.AioRpcError as e:
+        log(f"!!! [{nid}] SendTensor RPC failed during initiation: {e}")
+        return False
+    preds = [decode_prediction(rp) for rp in resps]
+    if any(p is None for p in preds):
+        log(f"[{nid}] Final result status received, but tensor not included in response.")
+        return False
+    if met is not None:
+        met.record(time.perf_counter() - t_req, int(x.shape[0]))
+    p = np.concatenate(preds).tolist()
+    log(f"[{nid}] ***** FINAL PREDICTION (Index): {p} *****")
+    return True
 
 
 def cifar_request(args, nid: str, rows: int, tag: int) -> torch.Tensor:

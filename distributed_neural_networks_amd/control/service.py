@@ -22,7 +22,6 @@ from __future__ import annotations
 
 import asyncio
 import os
-import threading
 import time
 import traceback
 from typing import Callable, Optional
@@ -64,7 +63,11 @@ class NodeServicer:
         self.wire_dtype = wire_dtype
         self.ready = forward is not None
         self._channel = None
-        self._lock = threading.Lock()
+        # serialises the stage compute (device stages reuse their buffers) without
+        # blocking the event loop: concurrent SendTensor calls (microbatches
+        # streamed by stage 0) wait here while transfers keep flowing — a
+        # threading.Lock held across the executor await would stall the loop
+        self._lock: Optional[asyncio.Lock] = None
         self.shutdown_event = asyncio.Event()
         self.requests_served = 0
 
@@ -86,8 +89,11 @@ class NodeServicer:
             x = codec.decode(request.tensor)
             log(f"[{nid}] Deserialized input tensor shape: {x.shape}")
             loop = asyncio.get_running_loop()
-            with self._lock, trace.span("SendTensor.forward", "compute", request=request.request_id):
-                out, pred = await loop.run_in_executor(None, self.forward, x)
+            if self._lock is None:
+                self._lock = asyncio.Lock()
+            async with self._lock:
+                with trace.span("SendTensor.forward", "compute", request=request.request_id):
+                    out, pred = await loop.run_in_executor(None, self.forward, x)
             self.metrics.record(time.perf_counter() - t0, int(x.shape[0]) if x.dim() else 1)
             out = out.detach().to("cpu")
             if self.wire_dtype is not None and out.is_floating_point():
