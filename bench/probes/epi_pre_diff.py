@@ -1,0 +1,46 @@
+"""Run-to-run and prefetch on/off differences of the forced one-shot decode
+GEMM with the folded LayerNorm + GELU epilogue (test_epilogue_prefetch_bit_identical
+diagnostics): prints max |diff| and count for (off, off), (on, on), (off, on)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    from distributed_neural_networks_amd.ops._lib import lib
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear_norm,
+                                                          set_oneshot_gemm)
+    dev = torch.device("cuda", 0)
+    for (N, K) in ((2304, 768), (3072, 768), (4800, 1600)):
+        M = 64
+        g = torch.Generator(device=dev).manual_seed(N + K)
+        x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
+        w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+        bias = torch.randn(N, device=dev, generator=g)
+        ws = decode_workspace(dev)
+        f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
+                      bias, False, 1e-5, dev, False)
+        attach_shuffled(f)
+        outs = {}
+        set_oneshot_gemm(2)
+        for tag, on in (("off1", 0), ("off2", 0), ("on1", 1), ("on2", 1)):
+            lib().gemm_set_epi_prefetch(on)
+            outs[tag] = linear_norm(x, f, act="gelu", ws=ws).float().clone()
+        torch.cuda.synchronize()
+        lib().gemm_set_epi_prefetch(1)
+        set_oneshot_gemm(1)
+        res = {"N": N, "K": K}
+        for a, b in (("off1", "off2"), ("on1", "on2"), ("off1", "on1")):
+            d = (outs[a] - outs[b]).abs()
+            i = int(d.argmax())
+            res[f"{a}_{b}"] = {"max": d.max().item(), "n": int((d > 0).sum()), "at": [i // N, i % N],
+                               "vals": [outs[a].view(-1)[i].item(), outs[b].view(-1)[i].item()]}
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

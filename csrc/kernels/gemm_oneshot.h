@@ -124,22 +124,24 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   constexpr bool PRE = QPW <= 2 && !SPLIT && ACT != ACT_SILU_MUL;
   const bool pre = PRE && epi_pre && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
                    ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
+  // Unconditional, branch-free loads (absent operands read a valid dummy
+  // address, and ``pre`` / has_b / has_r decide what is used): a load under a
+  // branch made the compiler wait for it at the merge, before the image was
+  // even issued.
   f32x4 pre_sw[QPW], pre_cs[QPW], pre_b[QPW];
   bf16x4 pre_r[QPW];
+  if constexpr (PRE) {
+    const float* dummy = reinterpret_cast<const float*>(A);
 #pragma unroll
-  for (int k = 0; k < QPW; ++k) {
-    pre_sw[k] = pre_cs[k] = pre_b[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    pre_r[k] = bf16x4{0, 0, 0, 0};
-    const int q = wave + 4 * k;
-    if (pre && q < NTW * MT) {
+    for (int k = 0; k < QPW; ++k) {
+      const int q = min(wave + 4 * k, NTW * MT - 1);
       const int nn = min((tile * NTW + q / MT) * 16 + fg * 4, N - 4);
       const int mm = min(m0 + 16 * (q % MT) + fr, M - 1);
       if constexpr (W8) pre_sw[k] = *reinterpret_cast<const f32x4*>(sw + nn);
-      if constexpr (NORM == 2) {
-        if (colsum != nullptr) pre_cs[k] = *reinterpret_cast<const f32x4*>(colsum + nn);
-      }
-      if (bias != nullptr) pre_b[k] = *reinterpret_cast<const f32x4*>(bias + nn);
-      if (R != nullptr) pre_r[k] = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + nn);
+      if constexpr (NORM == 2) pre_cs[k] = *reinterpret_cast<const f32x4*>(colsum != nullptr ? colsum + nn : dummy);
+      pre_b[k] = *reinterpret_cast<const f32x4*>(bias != nullptr ? bias + nn : dummy);
+      pre_r[k] = *reinterpret_cast<const bf16x4*>(R != nullptr ? R + (size_t)mm * ldr + nn
+                                                              : reinterpret_cast<const bf16_t*>(dummy));
     }
   }
   float shift[MT], s1s[MT], s2s[MT];
@@ -154,6 +156,12 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       }
     }
   }
+  // the loads above (row-statistics partials, epilogue operands, shifts) stay
+  // ahead of the image and the weights: the counted vmcnt waits below retire
+  // the image by counting only the weights issued after it, so nothing may be
+  // scheduled in between (a prefetch load sunk past the LDS-DMA let the image
+  // be read before it landed)
+  __builtin_amdgcn_sched_barrier(0);
   // ---- issue: every A row segment of the wave's range by LDS-DMA (full
   // lines), then every weight chunk, step-major.  The activations come from
   // L2 and land first: the row statistics are taken from the image while the

@@ -176,21 +176,22 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   constexpr int NP = PRE ? NT : 1;
   const bool pre = PRE && epi_pre && wave < MT && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
                    ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
+  // unconditional loads (dummy address for absent operands; ``pre`` and
+  // has_b / has_r decide use): a load under a branch is waited for at the merge
   f32x4 pre_sw[NP], pre_cs[NP], pre_b[NP];
   bf16x4 pre_r[NP];
+  if constexpr (PRE) {
+    const float* dummy = reinterpret_cast<const float*>(A);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    pre_sw[j] = pre_cs[j] = pre_b[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    pre_r[j] = bf16x4{0, 0, 0, 0};
-    if (pre) {
+    for (int j = 0; j < NP; ++j) {
       const int nn = min(n0 + j * 16 + (lane >> 4) * 4, N - 4);
-      const int mm = min(wave * 16 + (lane & 15), M - 1);
+      const int mm = min(min(wave, MT - 1) * 16 + (lane & 15), M - 1);
       if constexpr (W8) pre_sw[j] = *reinterpret_cast<const f32x4*>(sw + nn);
-      if constexpr (NORM == NORM_LN) {
-        if (colsum != nullptr) pre_cs[j] = *reinterpret_cast<const f32x4*>(colsum + nn);
-      }
-      if (bias != nullptr) pre_b[j] = *reinterpret_cast<const f32x4*>(bias + nn);
-      if (R != nullptr) pre_r[j] = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + nn);
+      if constexpr (NORM == NORM_LN)
+        pre_cs[j] = *reinterpret_cast<const f32x4*>(colsum != nullptr ? colsum + nn : dummy);
+      pre_b[j] = *reinterpret_cast<const f32x4*>(bias != nullptr ? bias + nn : dummy);
+      pre_r[j] = *reinterpret_cast<const bf16x4*>(R != nullptr ? R + (size_t)mm * ldr + nn
+                                                              : reinterpret_cast<const bf16_t*>(dummy));
     }
   }
   f32x4 acc[NT][MT];

@@ -275,9 +275,10 @@ def test_oneshot_pinned_configs(cfg):
 def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     """Epilogue operands issued with the first loads (gemm_oneshot.h /
     gemm_skinny_kernel ``pre``, the default) change when the channel scales,
-    column sums, bias and residual arrive, not the operations: outputs match
-    the late-load epilogue (``gemm_set_epi_prefetch(0)``) up to the compiler's
-    mul-add contraction (fp32 ulps, so a rare bf16 rounding flip)."""
+    column sums, bias and residual arrive, not the arithmetic: outputs are
+    bit-identical to the late-load epilogue (``gemm_set_epi_prefetch(0)``) and
+    from run to run (a first version let the activation image be read before
+    its DMA landed, which only showed as run-to-run differences)."""
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
@@ -306,15 +307,12 @@ def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     outs = []
     try:
         set_oneshot_gemm(2 if path == "oneshot" else 0)
-        for on in (0, 1):
+        for on in (0, 1, 1, 1):
             lib().gemm_set_epi_prefetch(on)
             outs.append(run().clone())
         torch.cuda.synchronize()
     finally:
         lib().gemm_set_epi_prefetch(1)
         set_oneshot_gemm(1)
-    a, b = outs[0].float(), outs[1].float()
-    # one bf16 step of the larger value (a flip at a binade edge is a full step of it)
-    ulp = torch.maximum(torch.maximum(a.abs(), b.abs()), torch.full_like(b, 2.0 ** -126)) * 2.0 ** -7
-    assert bool(((a - b).abs() <= ulp).all()), (a - b).abs().max().item()
-    assert (a != b).float().mean().item() < 1e-2
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o), (o.float() - outs[0].float()).abs().max().item()
