@@ -10,7 +10,40 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
+def bias_res_w8(N, K):
+    """linear_w8 with bias + residual (GPT-2 XL O / c_proj) under the same arms."""
+    from distributed_neural_networks_amd.ops._lib import lib
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import decode_workspace, set_oneshot_gemm, shuffle_weight
+    dev = torch.device("cuda", 0)
+    M = 64
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
+    w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    ws = decode_workspace(dev)
+    q = quantize_weight(w, dev)
+    q.shuf = shuffle_weight(q.q[:, :K])
+    res_ = {"N": N, "K": K, "epi": "bias_res_w8"}
+    for mode in (2, 0):
+        outs = {}
+        set_oneshot_gemm(mode)
+        for tag, on in (("off1", 0), ("off2", 0), ("on1", 1), ("on2", 1)):
+            lib().gemm_set_epi_prefetch(on)
+            outs[tag] = linear_w8(x, q, bias, 0, res, ws=ws).float().clone()
+        torch.cuda.synchronize()
+        for a, b in (("off1", "off2"), ("on1", "on2"), ("off1", "on1")):
+            d = (outs[a] - outs[b]).abs()
+            res_[f"mode{mode}_{a}_{b}"] = {"max": d.max().item(), "n": int((d > 0).sum())}
+    lib().gemm_set_epi_prefetch(1)
+    set_oneshot_gemm(1)
+    print(json.dumps(res_), flush=True)
+
+
 def main():
+    bias_res_w8(1600, 6400)
+    bias_res_w8(1600, 1600)
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear_norm,
                                                           set_oneshot_gemm)

