@@ -48,16 +48,22 @@ def main():
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear_norm,
                                                           set_oneshot_gemm)
     dev = torch.device("cuda", 0)
-    for (N, K) in ((2304, 768), (3072, 768), (4800, 1600)):
+    for (N, K), test_data in (((2304, 768), True), ((2304, 768), False), ((3072, 768), True), ((4800, 1600), False)):
         M = 64
         g = torch.Generator(device=dev).manual_seed(N + K)
         x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
         w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
         bias = torch.randn(N, device=dev, generator=g)
+        if test_data:  # the draw order of test_epilogue_prefetch_bit_identical (a residual before gamma / beta)
+            torch.randn(M, N, device=dev, generator=g)
         ws = decode_workspace(dev)
-        f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
-                      bias, False, 1e-5, dev, False)
+        gam = torch.rand(K, device=dev, generator=g) + 0.5
+        bet = torch.randn(K, device=dev, generator=g) * 0.1
+        f = fold_norm(w, gam, bet, bias, False, 1e-5, dev, False)
         attach_shuffled(f)
+        xf = x.float()
+        xn = (xf - xf.mean(1, keepdim=True)) / torch.sqrt(xf.var(1, unbiased=False, keepdim=True) + 1e-5)
+        ref = torch.nn.functional.gelu((xn * gam + bet) @ w.t() + bias, approximate="tanh")
         outs = {}
         set_oneshot_gemm(2)
         for tag, on in (("off1", 0), ("off2", 0), ("on1", 1), ("on2", 1)):
@@ -67,11 +73,18 @@ def main():
         lib().gemm_set_epi_prefetch(1)
         set_oneshot_gemm(1)
         res = {"N": N, "K": K}
+        res["test_data"] = test_data
+        for a in ("off1", "on1"):
+            d = (outs[a] - ref).abs()
+            i = int(d.argmax())
+            res[f"{a}_vs_fp32"] = {"max": d.max().item(), "at": [i // N, i % N], "ref": ref.view(-1)[i].item()}
         for a, b in (("off1", "off2"), ("on1", "on2"), ("off1", "on1")):
             d = (outs[a] - outs[b]).abs()
             i = int(d.argmax())
             res[f"{a}_{b}"] = {"max": d.max().item(), "n": int((d > 0).sum()), "at": [i // N, i % N],
-                               "vals": [outs[a].view(-1)[i].item(), outs[b].view(-1)[i].item()]}
+                               "vals": [outs[a].view(-1)[i].item(), outs[b].view(-1)[i].item()],
+                                "ref": ref.view(-1)[i].item(), "n_gt_step": int((d > outs[a].abs().maximum(
+                                    outs[b].abs()) * 2.0 ** -7).sum())}
         print(json.dumps(res), flush=True)
 
 
