@@ -210,8 +210,10 @@ def linear_w8(x: torch.Tensor, w: Fp8Weight, bias: Optional[torch.Tensor] = None
     wsp, wsb = (0, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
     from .gemm import _LAST_RS, _RowStats
     rs = _RowStats(rs_out, rs_in, M)
-    check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0), ptr(bias),
-                               ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, act, norm,
-                               ptr(colsum), eps, stream_ptr(), ptr(w.shuf), wsp, wsb), "gemm_skinny_w8")
-    _LAST_RS[0] = rs.done()
+    try:
+        check(lib().gemm_skinny_w8(ptr(x), x.stride(0), ptr(w.q), kp, ptr(w.scale), ptr(out), out.stride(0),
+                                   ptr(bias), ptr(residual), 0 if residual is None else residual.stride(0), M, N, K,
+                                   act, norm, ptr(colsum), eps, stream_ptr(), ptr(w.shuf), wsp, wsb), "gemm_skinny_w8")
+    finally:  # a rejected call must not leave the request armed for the next GEMM
+        _LAST_RS[0] = rs.done()
     return out

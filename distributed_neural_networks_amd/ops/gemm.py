@@ -163,11 +163,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         raise ValueError("linear: colsum needs rowstat and N fp32 entries")
     wsp, wsb = _ws_args(ws)
     rs = _RowStats(rs_out, None, M)
-    check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
-                          ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
-                          1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf), ptr(rowstat),
-                          ptr(colsum), wsp, wsb), "gemm_bf16")
-    _LAST_RS[0] = rs.done()
+    try:
+        check(lib().gemm_bf16(ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(o2), o2.stride(0), ptr(bias),
+                              ptr(r2), 0 if r2 is None else r2.stride(0), M, N, K, a,
+                              1 if o2.dtype == torch.float32 else 0, stream_ptr(), ptr(w_shuf), ptr(rowstat),
+                              ptr(colsum), wsp, wsb), "gemm_bf16")
+    finally:  # a rejected call must not leave the request armed for the next GEMM
+        _LAST_RS[0] = rs.done()
     return out
 
 
@@ -320,10 +322,13 @@ def linear_norm(x: torch.Tensor, f: FoldedLinear, act=None, residual: Optional[t
         raise ValueError("linear_norm: ws is not shuffle_weight(w)")
     wsp, wsb = _ws_args(ws)
     rs = _RowStats(None, rs_in, M)
-    check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0), ptr(f.bias),
-                                 ptr(residual), 0 if residual is None else residual.stride(0), M, N, K, a, f.norm,
-                                 ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws), wsp, wsb), "gemm_skinny_norm")
-    rs.done()
+    try:
+        check(lib().gemm_skinny_norm(ptr(x), x.stride(0), ptr(f.w), f.w.stride(0), ptr(out), out.stride(0),
+                                     ptr(f.bias), ptr(residual), 0 if residual is None else residual.stride(0), M, N,
+                                     K, a, f.norm, ptr(f.colsum), f.eps, stream_ptr(), ptr(f.ws), wsp, wsb),
+              "gemm_skinny_norm")
+    finally:
+        rs.done()
     return out
 
 QKV_SCATTER = True  # prefill c_attn writes q / K / V head-major (A/B switch)
