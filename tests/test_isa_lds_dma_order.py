@@ -1,4 +1,4 @@
-"""Static race check of the one-shot decode GEMM's LDS-DMA image (CPU only:
+"""Static race check of the decode GEMMs' LDS-DMA images (CPU only:
 hipcc cross-compiles gfx950 device assembly, nothing runs on a GPU).
 
 gemm_oneshot.h issues each wave's activation image by LDS-DMA and then every
@@ -13,6 +13,9 @@ configurations and the forced test shapes) and asserts both, so a schedule
 change that breaks the count fails here, on the CPU, rather than as rare
 wrong tiles on the GPU.  (MI355X_MICROARCH.md item 7: nothing but the
 issuing wave's covering vmcnt orders a ds_read behind a pending LDS-DMA.)
+The fused LM head (gemm_head.h) stages its activation image the same way,
+one image per K pass: every LDS read must come after a wait that retires
+the pass's last DMA.
 """
 import os
 import re
@@ -38,7 +41,11 @@ CONFIGS = [
     (2, 4, "true", 0, "ACT_NONE", "true", 2),     # split-K slab variant
 ]
 
+# <W8, NORM, NCH, CPP, GS>: the GPT-2 and GPT-2 XL fp8 heads of the decode step
+HEADS = [("false", 2, 24, 24, 12), ("true", 2, 25, 14, 5)]
+
 SRC = """#include "kernels/gemm_oneshot.h"
+#include "kernels/gemm_head.h"
 namespace dnn {{
 void* isa_keep[] = {{ {items} }};
 }}
@@ -46,8 +53,9 @@ void* isa_keep[] = {{ {items} }};
 
 
 def _asm():
-    items = ", ".join(f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}>"
-                      for mt, ntw, w8, norm, act, split, steps in CONFIGS)
+    items = ", ".join([f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}>"
+                       for mt, ntw, w8, norm, act, split, steps in CONFIGS] +
+                      [f"(void*)&gemm_head_kernel<{w8}, {norm}, {nch}, {cpp}, {gs}>" for w8, norm, nch, cpp, gs in HEADS])
     d = tempfile.mkdtemp(prefix="dnn_isa_")
     src, out = os.path.join(d, "oneshot_isa.hip"), os.path.join(d, "oneshot_isa.s")
     with open(src, "w") as f:
@@ -62,11 +70,11 @@ def _asm():
     return text
 
 
-def _kernels(text):
+def _kernels(text, kernel="gemm_oneshot_kernel"):
     """{mangled name: [memory / wait instructions in program order]}"""
     out, name = {}, None
     for line in text.splitlines():
-        m = re.match(r"^(_Z\S*gemm_oneshot_kernel\S*):", line)
+        m = re.match(r"^(_Z\S*" + kernel + r"\S*):", line)
         if m:
             name = m.group(1)
             out[name] = []
@@ -104,3 +112,34 @@ def test_oneshot_image_dma_retired_by_counted_wait():
                 break
         assert wait is not None, f"{name}: no vmcnt wait before the first image read"
         assert wait <= issued, f"{name}: vmcnt({wait}) with only {issued} loads after the image DMA"
+
+
+def _unretired_reads(seq):
+    """Linear scan (the kernels' DMA phases are fully unrolled): LDS reads
+    issued while an LDS-DMA may still be pending, i.e. before a vmcnt wait
+    that leaves at most as many loads outstanding as were issued after the
+    most recent DMA."""
+    pending, after, bad = False, 0, []
+    for t in seq:
+        if "global_load_lds" in t or (t.startswith("buffer_load") and " lds" in t):
+            pending, after = True, 0
+        elif t.startswith(("global_load", "buffer_load")):
+            after += 1
+        elif t.startswith("s_waitcnt") and "vmcnt" in t:
+            if pending and int(re.search(r"vmcnt\((\d+)\)", t).group(1)) <= after:
+                pending = False
+        elif t.startswith("ds_read") and pending:
+            bad.append(t)
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_lds_dma_images_retired_before_reads():
+    text = _asm()
+    for kernel, n in (("gemm_oneshot_kernel", len(CONFIGS)), ("gemm_head_kernel", len(HEADS))):
+        ks = _kernels(text, kernel)
+        assert len(ks) == n, (kernel, sorted(ks))
+        for name, seq in ks.items():
+            assert any("global_load_lds" in t for t in seq), name
+            bad = _unretired_reads(seq)
+            assert not bad, f"{name}: {len(bad)} LDS reads before the image DMA is retired: {bad[:3]}"
