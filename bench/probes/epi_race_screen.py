@@ -1,11 +1,15 @@
-"""Race screen of the forced one-shot decode GEMM (folded LayerNorm + GELU,
-the data of test_epilogue_prefetch_bit_identical): a settled reference per
-epilogue arm (prefetch off / on, each the second of two back-to-back calls),
-then ``--iters`` calls, each after a launch of the same kernel on other
-activations (the LDS and the caches hold someone else's data), compared
-bit for bit with the reference of its arm.  A read of the activation image
-before its LDS-DMA landed shows as mismatches here even when back-to-back
-repeats agree.  Prints one JSON line per shape."""
+"""Race screen of the one-shot decode GEMM (csrc/kernels/gemm_oneshot.h): a
+settled reference per epilogue arm (prefetch off / on, each the second of two
+back-to-back calls), then ``--iters`` calls, each after a launch of the same
+kernel on other activations (the LDS and the caches hold someone else's
+data), compared bit for bit with the reference of its arm.  A read of the
+activation image before its LDS-DMA landed shows as mismatches here even when
+back-to-back repeats agree (the same bytes are already in LDS).
+
+Cases: the folded LayerNorm + GELU shapes of test_epilogue_prefetch_bit_identical
+(forced one-shot, bf16), the GPT-2 O projection with bias + residual, and the
+GPT-2 XL W8A16 c_fc (LN + GELU) and O (bias + residual) at their planned
+two-step configurations.  Prints one JSON line per case."""
 import argparse
 import json
 import os
@@ -16,43 +20,55 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
-def screen(N, K, iters):
+def case(name, N, K, epi, w8, iters):
     from distributed_neural_networks_amd.ops._lib import lib
-    from distributed_neural_networks_amd.ops.gemm import attach_shuffled, decode_workspace, fold_norm, linear_norm
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
+                                                          linear_norm, shuffle_weight)
     dev = torch.device("cuda", 0)
     M = 64
     g = torch.Generator(device=dev).manual_seed(N + K)
     x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
     w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
     bias = torch.randn(N, device=dev, generator=g)
-    torch.randn(M, N, device=dev, generator=g)  # the test's residual draw
-    f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
-                  bias, False, 1e-5, dev, False)
-    attach_shuffled(f)
+    res = torch.randn(M, N, device=dev, generator=g).bfloat16()
     x2 = (torch.randn(M, K, device=dev, generator=g) * 3 - 1.0).bfloat16()
     ws = decode_workspace(dev)
+    if epi == "ln_gelu":
+        f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
+                      bias, False, 1e-5, dev, w8)
+        attach_shuffled(f)
+        run = lambda a: linear_norm(a, f, act="gelu", ws=ws)  # noqa: E731
+    elif w8:
+        q = quantize_weight(w, dev)
+        q.shuf = shuffle_weight(q.q[:, :K])
+        run = lambda a: linear_w8(a, q, bias, 0, res, ws=ws)  # noqa: E731
+    else:
+        wb = w.bfloat16()
+        wsh = shuffle_weight(wb)
+        run = lambda a: linear(a, wb, bias, None, res, w_shuf=wsh, ws=ws)  # noqa: E731
     ref = {}
     for on in (0, 1):
         lib().gemm_set_epi_prefetch(on)
-        linear_norm(x, f, act="gelu", ws=ws)
-        ref[on] = linear_norm(x, f, act="gelu", ws=ws).clone()
-    res = {"N": N, "K": K, "iters": iters,
+        run(x)
+        ref[on] = run(x).clone()
+    out = {"case": name, "N": N, "K": K, "w8": w8, "iters": iters,
            "ref_on_vs_off_max": (ref[0].float() - ref[1].float()).abs().max().item()}
     for on in (0, 1):
         bad, worst, rows = 0, 0.0, set()
         for i in range(iters):
             lib().gemm_set_epi_prefetch(i % 2)  # the poisoning call alternates arms too
-            linear_norm(x2, f, act="gelu", ws=ws)
+            run(x2)
             lib().gemm_set_epi_prefetch(on)
-            o = linear_norm(x, f, act="gelu", ws=ws)
+            o = run(x)
             d = (o.float() - ref[on].float()).abs()
             if bool((d > 0).any()):
                 bad += 1
                 worst = max(worst, d.max().item())
                 rows.update((d > 0).any(1).nonzero().flatten().tolist())
-        res[f"arm{on}"] = {"mismatched_calls": bad, "max": worst, "rows": sorted(rows)[:16]}
+        out[f"arm{on}"] = {"mismatched_calls": bad, "max": worst, "rows": sorted(rows)[:16]}
     lib().gemm_set_epi_prefetch(1)
-    return res
+    return out
 
 
 def main():
@@ -60,10 +76,15 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     a = ap.parse_args()
     from distributed_neural_networks_amd.ops.gemm import set_oneshot_gemm
-    set_oneshot_gemm(2)
+    cases = [("ln_gelu_2304x768_forced", 2304, 768, "ln_gelu", False, 2),
+             ("ln_gelu_3072x768_forced", 3072, 768, "ln_gelu", False, 2),
+             ("gpt2_o_bias_res", 768, 768, "bias_res", False, 1),
+             ("xl_c_fc_w8_ln_gelu", 6400, 1600, "ln_gelu", True, 1),
+             ("xl_o_w8_bias_res", 1600, 1600, "bias_res", True, 1)]
     try:
-        for N, K in ((2304, 768), (3072, 768), (768, 3072)):
-            print(json.dumps(screen(N, K, a.iters)), flush=True)
+        for name, N, K, epi, w8, mode in cases:
+            set_oneshot_gemm(mode)
+            print(json.dumps(case(name, N, K, epi, w8, a.iters)), flush=True)
     finally:
         set_oneshot_gemm(1)
 

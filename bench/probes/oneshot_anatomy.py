@@ -12,6 +12,10 @@ decode projection at B = 64, timed whole and with parts removed —
     empty     the launch alone (every wave returns at once)
     no_red    no cross-wave reduction through LDS (each wave's partial stored)
     no_ld_no_red  neither loads nor the reduction
+    counted_wait  the round-4/5 image wait (vmcnt(weights after the image)
+                  instead of vmcnt(0)): with two steps, step 0 computes while
+                  step 1's weights land — racy (gemm_oneshot.h "Retiring the
+                  image"), measured here only for what the fix costs
 
 Each arm is a HIP-graph replay of ``--iters`` launches over weight copies
 rotated past the 256 MB MALL (as bench/oneshot_sweep.py), interleaved over
@@ -33,7 +37,7 @@ SHAPES = [  # name, N, K, cfg (gemm_skinny.hip dnn_gemm_oneshot_ablate), w8
     ("gpt2_c_attn", 2304, 768, 2, False), ("gpt2_c_fc", 3072, 768, 2, False),
 ]
 ARMS = {"full": 0, "no_w": 1, "no_a": 2, "no_ld": 3, "no_mfma": 4, "no_store": 8, "empty": 32, "no_red": 64,
-        "no_ld_no_red": 67}
+        "no_ld_no_red": 67, "counted_wait": 128}
 
 
 def main():

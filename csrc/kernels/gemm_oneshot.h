@@ -25,13 +25,12 @@
 //     (LDS-DMA writes lane-linear);
 //   * each wave loads its quarter of the NTW weight tiles straight to VGPRs,
 //     non-temporally (read once), all chunks in flight;
-//   * the A rows are issued first, then the weights step-major: the folded
-//     norm's row statistics are taken from the image while the weights are
-//     still in flight (measured neutral against taking them from the MFMA
-//     fragments: the statistics' VALU, ~200 elements per lane at 32 rows and
-//     K = 1600, outlasts the weight flight either way,
-//     profiles/r4_oneshot_norm_ab*.jsonl), and with two steps a counted vmcnt
-//     lets step 0 compute while step 1 lands;
+//   * the A rows are issued first, then the weights step-major; the folded
+//     norm's row statistics are taken from the image once every load has
+//     landed and the workgroup has synchronised ("Retiring the image"
+//     below; the round-4 version took them under the weight flight, measured
+//     neutral against taking them from the MFMA fragments,
+//     profiles/r4_oneshot_norm_ab*.jsonl);
 //   * MFMAs from LDS fragments x register weights; the 4
 //     partial sums meet in LDS (each wave reuses its own image region), and
 //     the epilogue runs in the workgroup (bias / GELU / residual / packed
@@ -59,7 +58,30 @@ constexpr int os_lds_bytes() {
 // ABL (probe only, bench/probes/oneshot_anatomy.py; 0 in every product launch):
 // bit 1 no weight loads, 2 no activation image, 4 no MFMAs, 8 no epilogue
 // stores, 32 return at once (the launch alone), 64 no cross-wave reduction
-// (each wave's own partial goes to the epilogue) — what each part costs.
+// (each wave's own partial goes to the epilogue), 128 the round-4/5 counted
+// image wait (racy, below) — what each part costs.
+//
+// Retiring the image.  A race screen that runs each call after a launch on
+// other activations (bench/probes/epi_race_screen.py,
+// profiles/r5_oneshot_race_screen.jsonl) found the row statistics of rows
+// 16-31 — the last DMAs of the image — taken from stale LDS bytes in 1-5 of
+// 200 calls, while back-to-back repeats (the same bytes already in LDS) agreed.
+// In that build the statistics' ds_reads already followed a vmcnt(0) the
+// compiler had placed: the LDS-DMA's counter retiring is not enough for the
+// issuing wave's own reads.  The image is now read only after the sequence
+// composable_kernel uses after direct-to-LDS loads (block_sync_lds_direct_load:
+// vmcnt(0), lgkmcnt(0), s_barrier), so the statistics no longer overlap the
+// weight flight and with two steps step 0 no longer computes while step 1
+// lands (cost: the ABL 128 arm of bench/probes/oneshot_anatomy.py, which keeps
+// the round-4/5 counted wait).  Plain loads issued before the image
+// (row-statistics partials, epilogue operands) are still retired by counted
+// waits: plain loads complete in order among themselves.
+// tests/test_isa_lds_dma_order.py checks the sequence in the product ISA.
+__device__ __forceinline__ void os_image_sync() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 template <int MT, int NTW, bool W8, int NORM, int ACT, bool SPLIT, int STEPS, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __restrict__ A, int lda_b,
                                                               const uint8_t* __restrict__ Wsh,
@@ -163,9 +185,8 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   // be read before it landed)
   __builtin_amdgcn_sched_barrier(0);
   // ---- issue: every A row segment of the wave's range by LDS-DMA (full
-  // lines), then every weight chunk, step-major.  The activations come from
-  // L2 and land first: the row statistics are taken from the image while the
-  // weights are still in flight, and step 0 computes while step 1 lands
+  // lines), then every weight chunk, step-major (all in flight at once; the
+  // image is read after os_image_sync)
   const int kb0 = w0 * ACH;  // first A byte of the wave's range in a row
   // last valid 16 B of the range (surplus slots clamp here; their weights are zeroed)
   const int kb_last = min(max(w1, w0 + 1), nch) * ACH - 16;
@@ -202,10 +223,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- row statistics of this wave's K range from its image (the 4 lane
-  // groups hold disjoint k), while the weight loads are outstanding
+  // groups hold disjoint k)
   if (rsi) {
-    // merge the producer's partials instead (they and the image were issued
-    // before the weights): mean / rstd of row tid / TPR into LDS
+    // merge the producer's partials instead (plain loads issued before the
+    // weights: the counted wait retires them): mean / rstd of row tid / TPR
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     const float2 mr = rowstat_merge<NORM, TPR, SPT>(rsp, rs0, tid % TPR, kelems, eps);
@@ -215,7 +236,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     }
     __builtin_amdgcn_sched_barrier(0);
   } else if constexpr (NORM != 0) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");  // the image (issued first)
+    if constexpr ((ABL & 128) != 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");  // racy (probe only)
+    else
+      os_image_sync();  // the image (see "Retiring the image")
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -242,12 +266,14 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // the image and step 0's weights retired; step 1's weights (NTW x CS loads,
-  // issued last) may still be in flight
-  if constexpr (STEPS == 2) {
+  // the image and every weight retired (ABL 128: step 1's weights, NTW x CS
+  // loads issued last, still in flight — racy for the image, probe only)
+  if constexpr (STEPS == 2 && (ABL & 128) != 0) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NTW * CS) : "memory");
-  } else {
+  } else if constexpr ((ABL & 128) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    os_image_sync();  // again after a statistics pass: the weights land here, the barrier is cheap
   }
   __builtin_amdgcn_sched_barrier(0);
 

@@ -736,6 +736,8 @@ extern "C" int dnn_gemm_oneshot_ablate(const void* A, int lda, const void* Wsh, 
                                                                        N, kbytes, nullptr, 0.f, st, nullptr, 1);      \
       case 67: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 67>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, M, \
                                                                        N, kbytes, nullptr, 0.f, st, nullptr, 1);      \
+      case 128: return launch_os_cfg<MTV, NTV, SV, ACT_NONE, 0, W8V, 128>(A, lb, Wsh, sw, C, ldc, nullptr, nullptr, 0, \
+                                                                         M, N, kbytes, nullptr, 0.f, st, nullptr, 1); \
       default: return -2;                                                                                              \
     }                                                                                                                  \
   }

@@ -2,20 +2,19 @@
 hipcc cross-compiles gfx950 device assembly, nothing runs on a GPU).
 
 gemm_oneshot.h issues each wave's activation image by LDS-DMA and then every
-weight load, and retires the image with a *counted* wait: ``vmcnt(N)`` with N
-the number of weight loads issued after it.  That wait covers the image only
-if no other vector-memory load is issued between the first and the last
-image DMA, and at least N loads follow the last one before the first LDS read
-(a load sunk past the DMA by the compiler let the image be read before it
-landed: the round-5 race fixed with ``sched_barrier``).  The check reads the
+weight load.  The round-4/5 kernel read the image after a counted wait (and,
+as compiled, after a vmcnt(0) the compiler placed); a race screen that runs
+each call after a launch on other activations (bench/probes/epi_race_screen.py,
+profiles/r5_oneshot_race_screen.jsonl) still found the last rows of the image
+read stale in a few calls out of hundreds.  The kernel now reads an image
+only after composable_kernel's direct-load sequence (vmcnt(0), lgkmcnt(0),
+s_barrier; gemm_oneshot.h "Retiring the image").  This check reads the
 assembly of the product instantiations (the planned GPT-2 / GPT-2 XL decode
-configurations and the forced test shapes) and asserts both, so a schedule
-change that breaks the count fails here, on the CPU, rather than as rare
-wrong tiles on the GPU.  (MI355X_MICROARCH.md item 7: nothing but the
-issuing wave's covering vmcnt orders a ds_read behind a pending LDS-DMA.)
-The fused LM head (gemm_head.h) stages its activation image the same way,
-one image per K pass: every LDS read must come after a wait that retires
-the pass's last DMA.
+configurations and the forced test shapes) and of the fused LM head
+(gemm_head.h, one image per K pass) and asserts, on every control-flow path,
+that no LDS read follows an LDS-DMA without a vmcnt(0) and then an s_barrier
+in between.  The racy round-4/5 variant (probe bit ABL 128) is compiled too
+and must be flagged, so the check is known to see the bug it guards.
 """
 import os
 import re
@@ -30,6 +29,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 # <MT, NTW, W8, NORM, ACT, SPLIT, STEPS>: gemm_skinny.hip os_plan (planned
 # shapes and the forced "every eligible shape" mode the GPU tests use)
+RACY = [(2, 1, "false", 2, "ACT_GELU", "false", 1, 128), (1, 2, "true", 0, "ACT_NONE", "false", 2, 128)]
 CONFIGS = [
     (2, 2, "false", 2, "ACT_NONE", "false", 1),   # GPT-2 c_attn (folded LN)
     (2, 2, "false", 2, "ACT_GELU", "false", 1),   # GPT-2 c_fc (folded LN + GELU)
@@ -55,6 +55,8 @@ void* isa_keep[] = {{ {items} }};
 def _asm():
     items = ", ".join([f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}>"
                        for mt, ntw, w8, norm, act, split, steps in CONFIGS] +
+                      [f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}, {abl}>"
+                       for mt, ntw, w8, norm, act, split, steps, abl in RACY] +
                       [f"(void*)&gemm_head_kernel<{w8}, {norm}, {nch}, {cpp}, {gs}>" for w8, norm, nch, cpp, gs in HEADS])
     d = tempfile.mkdtemp(prefix="dnn_isa_")
     src, out = os.path.join(d, "oneshot_isa.hip"), os.path.join(d, "oneshot_isa.s")
@@ -70,8 +72,9 @@ def _asm():
     return text
 
 
-def _kernels(text, kernel="gemm_oneshot_kernel"):
-    """{mangled name: [memory / wait instructions in program order]}"""
+def _kernels(text, kernel="gemm_oneshot_kernel", raw=False):
+    """{mangled name: [memory / wait instructions in program order]} (raw:
+    every label and instruction, for the control-flow scan)"""
     out, name = {}, None
     for line in text.splitlines():
         m = re.match(r"^(_Z\S*" + kernel + r"\S*):", line)
@@ -84,62 +87,101 @@ def _kernels(text, kernel="gemm_oneshot_kernel"):
         if line.startswith(".Lfunc_end"):
             name = None
             continue
-        t = line.strip()
-        if re.match(r"(global_load|buffer_load|ds_read|s_waitcnt)", t):
+        t = line.split(";")[0].strip()
+        if raw:
+            if t and not t.startswith("."):
+                out[name].append(t)
+            elif re.match(r"^\.LBB\w+:", t):
+                out[name].append(t)
+        elif re.match(r"(global_load|buffer_load|ds_read|s_waitcnt)", t):
             out[name].append(t)
     return out
 
 
+def _product(ks):
+    """Drop the probe instantiations (ABL != 0: a ninth template argument)."""
+    return {n: q for n, q in ks.items() if not re.search(r"ELi(128)EE", n)}
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_oneshot_image_dma_retired_by_counted_wait():
-    ks = _kernels(_asm())
+def test_oneshot_image_dma_issued_first():
+    """The image DMAs form one run (no load in between): every weight load is
+    issued after the whole image, as the kernel's issue order intends."""
+    ks = _product(_kernels(_asm()))
     assert len(ks) == len(CONFIGS), sorted(ks)
     for name, seq in ks.items():
         dma = [i for i, t in enumerate(seq) if "global_load_lds" in t]
         assert dma, name
-        first, last = dma[0], dma[-1]
-        between = [t for t in seq[first:last] if t.startswith(("global_load", "buffer_load")) and "lds" not in t]
+        between = [t for t in seq[dma[0]:dma[-1]] if t.startswith(("global_load", "buffer_load")) and "lds" not in t]
         assert not between, f"{name}: loads interleaved with the image DMA: {between[:4]}"
-        # the first LDS read after the image: the vmcnt in force must be <= the
-        # loads issued after the last DMA
-        issued, wait = 0, None
-        for t in seq[last + 1:]:
-            if t.startswith(("global_load", "buffer_load")):
-                issued += 1
-            elif t.startswith("s_waitcnt") and "vmcnt" in t:
-                wait = int(re.search(r"vmcnt\((\d+)\)", t).group(1))
-            elif t.startswith("ds_read"):
-                break
-        assert wait is not None, f"{name}: no vmcnt wait before the first image read"
-        assert wait <= issued, f"{name}: vmcnt({wait}) with only {issued} loads after the image DMA"
 
 
-def _unretired_reads(seq):
-    """Linear scan (the kernels' DMA phases are fully unrolled): LDS reads
-    issued while an LDS-DMA may still be pending, i.e. before a vmcnt wait
-    that leaves at most as many loads outstanding as were issued after the
-    most recent DMA."""
-    pending, after, bad = False, 0, []
-    for t in seq:
-        if "global_load_lds" in t or (t.startswith("buffer_load") and " lds" in t):
-            pending, after = True, 0
-        elif t.startswith(("global_load", "buffer_load")):
-            after += 1
-        elif t.startswith("s_waitcnt") and "vmcnt" in t:
-            if pending and int(re.search(r"vmcnt\((\d+)\)", t).group(1)) <= after:
-                pending = False
-        elif t.startswith("ds_read") and pending:
-            bad.append(t)
-    return bad
+def _unretired_reads(lines):
+    """LDS reads that some path reaches after an LDS-DMA without vmcnt(0) and
+    then s_barrier in between: a forward may-analysis over the kernel's
+    basic blocks (labels, s_branch / s_cbranch_*, s_endpgm)."""
+    blocks, labels, cur = [], {}, []
+    for t in lines:  # split into basic blocks
+        if t.endswith(":"):
+            if cur:
+                blocks.append(cur)
+            cur = []
+            labels[t[:-1]] = len(blocks)
+            continue
+        cur.append(t)
+        if t.startswith(("s_branch", "s_cbranch", "s_endpgm")):
+            blocks.append(cur)
+            cur = []
+    if cur:
+        blocks.append(cur)
+    # labels index the block that starts after them
+    succ = []
+    for i, b in enumerate(blocks):
+        last = b[-1] if b else ""
+        nxt = [i + 1] if i + 1 < len(blocks) else []
+        m = re.match(r"s_(c?)branch\w*\s+(\.LBB\w+)", last)
+        if last.startswith("s_endpgm"):
+            succ.append([])
+        elif m:
+            tgt = labels.get(m.group(2))
+            succ.append(([tgt] if tgt is not None else []) + (nxt if m.group(1) else []))
+        else:
+            succ.append(nxt)
+    # state: 0 clear, 1 DMA waited for (vmcnt(0)) but no barrier yet, 2 DMA
+    # pending; a block's entry state is the worst over its predecessors
+    entry = [0] * len(blocks)
+    bad, work = set(), list(range(len(blocks)))
+    while work:
+        i = work.pop(0)
+        st = entry[i]
+        for j, t in enumerate(blocks[i]):
+            if "global_load_lds" in t or (t.startswith("buffer_load") and " lds" in t):
+                st = 2
+            elif t.startswith("s_waitcnt") and re.search(r"vmcnt\(0\)", t):
+                st = min(st, 1)
+            elif t.startswith("s_barrier") and st == 1:
+                st = 0
+            elif t.startswith("ds_read") and st:
+                bad.add((i, j, t))
+        for k in succ[i]:
+            if st > entry[k]:
+                entry[k] = st
+                work.append(k)
+    return sorted(bad)
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 def test_lds_dma_images_retired_before_reads():
     text = _asm()
     for kernel, n in (("gemm_oneshot_kernel", len(CONFIGS)), ("gemm_head_kernel", len(HEADS))):
-        ks = _kernels(text, kernel)
+        ks = _product(_kernels(text, kernel, raw=True))
         assert len(ks) == n, (kernel, sorted(ks))
         for name, seq in ks.items():
             assert any("global_load_lds" in t for t in seq), name
             bad = _unretired_reads(seq)
             assert not bad, f"{name}: {len(bad)} LDS reads before the image DMA is retired: {bad[:3]}"
+    # the racy counted-wait variants must be flagged (the check sees the bug)
+    racy = {n: q for n, q in _kernels(text, raw=True).items() if n not in _product({n: q})}
+    assert len(racy) == len(RACY), sorted(racy)
+    for name, seq in racy.items():
+        assert _unretired_reads(seq), f"{name}: counted-wait variant not flagged"
