@@ -282,7 +282,9 @@ def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     up to the compiler's mul-add contraction of the split-K combine (a
     straight-line scale-and-bias fuses into one fma: a bf16 step in a handful
     of the 102 400 outputs of the 1600 x 6400 shape, bias_res_w8 in
-    profiles/r5_epi_prefetch_determinism.jsonl)."""
+    profiles/r5_epi_prefetch_determinism.jsonl).  Every recorded call follows
+    a launch on other activations (the LDS holds other bytes), which is what
+    exposed the image-sync race (gemm_oneshot.h "Retiring the image")."""
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
     from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear,
@@ -299,20 +301,24 @@ def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
         f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
                       bias, False, 1e-5, dev, w8)
         attach_shuffled(f)
-        run = lambda: linear_norm(x, f, act="gelu", ws=ws)  # noqa: E731
+        run = lambda a=x: linear_norm(a, f, act="gelu", ws=ws)  # noqa: E731
     elif w8:
         q = quantize_weight(w, dev)
         q.shuf = shuffle_weight(q.q[:, :K])
-        run = lambda: linear_w8(x, q, bias, 0, res, ws=ws)  # noqa: E731
+        run = lambda a=x: linear_w8(a, q, bias, 0, res, ws=ws)  # noqa: E731
     else:
         wb = w.bfloat16()
         wsh = shuffle_weight(wb)
-        run = lambda: linear(x, wb, bias, None, res, w_shuf=wsh, ws=ws)  # noqa: E731
+        run = lambda a=x: linear(a, wb, bias, None, res, w_shuf=wsh, ws=ws)  # noqa: E731
+    # each recorded call follows a launch on other activations, so an image read
+    # before its LDS-DMA landed sees different stale bytes (bench/probes/epi_race_screen.py)
+    x2 = (torch.randn(M, K, device=dev, generator=g) * 3 - 1.0).bfloat16()
     outs = []
     try:
         set_oneshot_gemm(2 if path == "oneshot" else 0)
         for on in (0, 1, 1, 1, 0):
             lib().gemm_set_epi_prefetch(on)
+            run(x2)
             outs.append(run().clone())
         torch.cuda.synchronize()
     finally:
