@@ -55,7 +55,7 @@ def case(name, N, K, epi, w8, iters):
     out = {"case": name, "N": N, "K": K, "w8": w8, "iters": iters,
            "ref_on_vs_off_max": (ref[0].float() - ref[1].float()).abs().max().item()}
     for on in (0, 1):
-        bad, worst, rows = 0, 0.0, set()
+        bad, worst, rows, detail = 0, 0.0, set(), []
         for i in range(iters):
             lib().gemm_set_epi_prefetch(i % 2)  # the poisoning call alternates arms too
             run(x2)
@@ -66,7 +66,12 @@ def case(name, N, K, epi, w8, iters):
                 bad += 1
                 worst = max(worst, d.max().item())
                 rows.update((d > 0).any(1).nonzero().flatten().tolist())
-        out[f"arm{on}"] = {"mismatched_calls": bad, "max": worst, "rows": sorted(rows)[:16]}
+                if len(detail) < 6:  # where: column tiles, element count, rows
+                    nz = (d > 0).nonzero()
+                    detail.append({"call": i, "n": int(nz.shape[0]), "rows": sorted(set(nz[:, 0].tolist()))[:32],
+                                   "col16_tiles": sorted(set((nz[:, 1] // 16).tolist()))[:32],
+                                   "max": d.max().item()})
+        out[f"arm{on}"] = {"mismatched_calls": bad, "max": worst, "rows": sorted(rows)[:16], "detail": detail}
     lib().gemm_set_epi_prefetch(1)
     return out
 
@@ -74,19 +79,39 @@ def case(name, N, K, epi, w8, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--cases", default="", help="comma-separated case names (default: all)")
     a = ap.parse_args()
     from distributed_neural_networks_amd.ops.gemm import set_oneshot_gemm
     cases = [("ln_gelu_2304x768_forced", 2304, 768, "ln_gelu", False, 2),
+             ("ln_gelu_2304x768_skinny", 2304, 768, "ln_gelu", False, 0),
+             ("ln_gelu_2304x768_planned", 2304, 768, "ln_gelu", False, 1),
+             # pinned one-shot configurations (mt, ntw, steps): grid 576 / 288 / 144 workgroups
+             ("ln_gelu_2304x768_pin111", 2304, 768, "ln_gelu", False, (2, 1, 1, 1)),
+             ("ln_gelu_2304x768_pin211", 2304, 768, "ln_gelu", False, (2, 2, 1, 1)),
+             ("ln_gelu_2304x768_pin221", 2304, 768, "ln_gelu", False, (2, 2, 2, 1)),
+             ("bias_2304x768_pin111", 2304, 768, "bias_res", False, (2, 1, 1, 1)),
+             # the same without the one-workgroup-per-CU LDS floor (gemm_set_oneshot_lds_floor(0))
+             ("nofloor_ln_gelu_2304x768_pin111", 2304, 768, "ln_gelu", False, (2, 1, 1, 1)),
+             ("nofloor_ln_gelu_2304x768_pin211", 2304, 768, "ln_gelu", False, (2, 2, 1, 1)),
              ("ln_gelu_3072x768_forced", 3072, 768, "ln_gelu", False, 2),
              ("gpt2_o_bias_res", 768, 768, "bias_res", False, 1),
              ("xl_c_fc_w8_ln_gelu", 6400, 1600, "ln_gelu", True, 1),
              ("xl_o_w8_bias_res", 1600, 1600, "bias_res", True, 1)]
     try:
         for name, N, K, epi, w8, mode in cases:
-            set_oneshot_gemm(mode)
+            if a.cases and name not in a.cases.split(","):
+                continue
+            from distributed_neural_networks_amd.ops._lib import lib
+            lib().gemm_set_oneshot_lds_floor(0 if name.startswith("nofloor") else 82 * 1024)
+            if isinstance(mode, tuple):
+                set_oneshot_gemm(mode[0], *mode[1:])
+            else:
+                set_oneshot_gemm(mode)
             print(json.dumps(case(name, N, K, epi, w8, a.iters)), flush=True)
     finally:
         set_oneshot_gemm(1)
+        from distributed_neural_networks_amd.ops._lib import lib
+        lib().gemm_set_oneshot_lds_floor(82 * 1024)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,7 @@
 // permutation for A and W, so the dot product is unchanged); the weight bytes
 // and so the step time halve.  KS is chosen on the host so that N/16 x KS waves
 // cover the CUs.
+#include <algorithm>
 #include "gemm_epilogue.h"
 #include "gemm_head.h"
 #include "gemm_oneshot.h"
@@ -538,6 +539,18 @@ static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const flo
 // LDS steps per wave, split-K); the plan below is fitted to
 // bench/oneshot_sweep.py, and dnn_gemm_set_oneshot can pin a config (A/B).
 static int g_os_on = 1;                             // 0 off, 1 planned shapes, 2 every eligible shape (tests)
+// LDS floor of a one-shot launch: above half the CU's 160 KB, so one workgroup
+// per CU.  The race screen (bench/probes/epi_race_screen.py) found one
+// workgroup's statistics off by a few ulp in ~1 of 150 calls only in grids
+// that put two workgroups with LDS-DMA images on one CU (forced 2/1/1 at
+// N = 2304 / 3072: 288 / 384 workgroups), never in the planned grids (<= 256
+// workgroups); profiles/r5_oneshot_race_screen*.jsonl.  0 = the kernel's own
+// size (A/B).
+static int g_os_lds_floor = 82 * 1024;
+extern "C" int dnn_gemm_set_oneshot_lds_floor(int bytes) {
+  g_os_lds_floor = bytes < 0 ? 0 : bytes;
+  return 0;
+}
 static int g_os_pin[4] = {0, 0, 0, 0};              // mt, ntw, steps, splitk (0 = planned)
 
 struct OsCfg {
@@ -623,7 +636,7 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
   const int ntiles = (N + BN - 1) / BN, mgroups = (M + MP - 1) / MP;
   const int kelems = W8 ? kbytes : kbytes / 2;
   const dim3 grid(ntiles * mgroups * splitk), block(256);
-  const size_t smem = os_lds_bytes<MT, STEPS>();
+  const size_t smem = std::max<size_t>(os_lds_bytes<MT, STEPS>(), (size_t)g_os_lds_floor);
   if (splitk == 1) {
     // row statistics: partials of the output (not for the half-width SwiGLU
     // output); merged partials of the input when they fit OS_RS_SPT per thread
