@@ -2,19 +2,20 @@
 hipcc cross-compiles gfx950 device assembly, nothing runs on a GPU).
 
 gemm_oneshot.h issues each wave's activation image by LDS-DMA and then every
-weight load.  The round-4/5 kernel read the image after a counted wait (and,
-as compiled, after a vmcnt(0) the compiler placed); a race screen that runs
-each call after a launch on other activations (bench/probes/epi_race_screen.py,
-profiles/r5_oneshot_race_screen.jsonl) still found the last rows of the image
-read stale in a few calls out of hundreds.  The kernel now reads an image
-only after composable_kernel's direct-load sequence (vmcnt(0), lgkmcnt(0),
-s_barrier; gemm_oneshot.h "Retiring the image").  This check reads the
-assembly of the product instantiations (the planned GPT-2 / GPT-2 XL decode
-configurations and the forced test shapes) and of the fused LM head
+weight load.  The kernel reads an image only after composable_kernel's
+direct-load sequence (vmcnt(0), lgkmcnt(0), s_barrier; gemm_oneshot.h
+"Retiring the image"), not after a count of the weights issued behind it:
+an LDS-DMA is not ordered with the plain loads that follow it.  This check
+reads the assembly of the product instantiations (the planned GPT-2 / GPT-2
+XL decode configurations and the forced test shapes) and of the fused LM head
 (gemm_head.h, one image per K pass) and asserts, on every control-flow path,
 that no LDS read follows an LDS-DMA without a vmcnt(0) and then an s_barrier
-in between.  The racy round-4/5 variant (probe bit ABL 128) is compiled too
-and must be flagged, so the check is known to see the bug it guards.
+in between.  The round-4/5 counted-wait variant (probe bit ABL 128) is
+compiled too and must be flagged, so the check is known to see what it
+guards.  (The GPU-side screen for the same kernel is
+bench/probes/epi_race_screen.py; its findings, including the one-workgroup-
+per-CU LDS floor, are in docs/ARCHITECTURE.md and
+profiles/r5_oneshot_race_screen_*.jsonl.)
 """
 import os
 import re
