@@ -61,19 +61,19 @@ constexpr int os_lds_bytes() {
 // (each wave's own partial goes to the epilogue), 128 the round-4/5 counted
 // image wait (racy, below) — what each part costs.
 //
-// Retiring the image.  A race screen that runs each call after a launch on
-// other activations (bench/probes/epi_race_screen.py,
-// profiles/r5_oneshot_race_screen.jsonl) found the row statistics of rows
-// 16-31 — the last DMAs of the image — taken from stale LDS bytes in 1-5 of
-// 200 calls, while back-to-back repeats (the same bytes already in LDS) agreed.
-// In that build the statistics' ds_reads already followed a vmcnt(0) the
-// compiler had placed: the LDS-DMA's counter retiring is not enough for the
-// issuing wave's own reads.  The image is now read only after the sequence
-// composable_kernel uses after direct-to-LDS loads (block_sync_lds_direct_load:
-// vmcnt(0), lgkmcnt(0), s_barrier), so the statistics no longer overlap the
-// weight flight and with two steps step 0 no longer computes while step 1
-// lands (cost: the ABL 128 arm of bench/probes/oneshot_anatomy.py, which keeps
-// the round-4/5 counted wait).  Plain loads issued before the image
+// Retiring the image.  The image is read only after composable_kernel's
+// direct-load sequence (block_sync_lds_direct_load: vmcnt(0), lgkmcnt(0),
+// s_barrier), not after a count of the weights issued behind it: an LDS-DMA is
+// not ordered with the plain loads that follow it.  The round-4/5 counted wait
+// stays as the probe bit ABL 128; the sync costs nothing measurable
+// (oneshot_anatomy.py counted_wait arm within +-0.13 us,
+// profiles/r5_oneshot_anatomy_imagesync.jsonl) although the statistics no
+// longer overlap the weight flight nor step 0 step 1's weights.  A race screen
+// (bench/probes/epi_race_screen.py, profiles/r5_oneshot_race_screen_*.jsonl)
+// also found a rare few-ulp error in one workgroup's second 16-row tile of
+// statistics, only where two one-shot workgroups shared a CU; the sync did not
+// change it, the host's LDS floor (one workgroup per CU, gemm_skinny.hip
+// g_os_lds_floor) removed it.  Plain loads issued before the image
 // (row-statistics partials, epilogue operands) are still retired by counted
 // waits: plain loads complete in order among themselves.
 // tests/test_isa_lds_dma_order.py checks the sequence in the product ISA.
