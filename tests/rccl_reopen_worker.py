@@ -51,7 +51,14 @@ def main() -> int:
             ch = rccl.pair_channel(rank, 1 - rank, dev, "world", store=st)
             uids.append(ch.uid.hex())
     st.set(f"done/{rank}", "1")
-    st.get(f"done/{1 - rank}")  # the store host outlives the other rank's reads
+    st.get(f"done/{1 - rank}")
+    # the store host (rank 0) outlives the other rank's last store call: rank 1
+    # says goodbye after its reads, rank 0 waits for that and a little longer
+    if rank == 1:
+        st.set("bye/1", "1")
+    else:
+        st.get("bye/1")
+        time.sleep(0.5)
     with open(out, "w") as f:
         f.write("\n".join(uids))
     return 0
