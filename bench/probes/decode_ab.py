@@ -46,6 +46,8 @@ def apply(switch: str, v: int) -> None:
         os.environ["DNN_FLASH_DB"] = str(v)
     elif switch == "epi_pre":  # decode GEMM epilogue operands issued with the first loads (gemm_oneshot.h / skinny)
         lib().gemm_set_epi_prefetch(v)
+    elif switch == "os_lds_floor":  # one-shot launch LDS floor in bytes (gemm_skinny.hip g_os_lds_floor; 0 = own size)
+        lib().gemm_set_oneshot_lds_floor(v)
     elif switch == "flash_pipe":  # hd-64 flash prefill software pipeline (attention.hip DNN_FLASH_PIPE)
         os.environ["DNN_FLASH_PIPE"] = str(v)
     elif switch == "rowstats_r":  # prefill row statistics rows per wave (norm_embed.hip dnn_row_stats)
