@@ -90,6 +90,9 @@ def parse():
                          "concurrently (-1 = auto: 0 on 1 GPU, 16 on N > 1)")
     ap.add_argument("--cut", default="auto", choices=["auto", "1", "2"],
                     help="stage boundary: 1 = after conv2/pool (reference), 2 = after fc1; auto = per placement")
+    ap.add_argument("--verify_images", type=int, default=-1,
+                    help="N>1 pp2: images each stage-0 GPU pushes through the distributed pipeline and checks "
+                         "against fp32 torch after the timed run (0 = off, -1 = 4096 on GPUs, 256 with --cpu)")
     ap.add_argument("--extra_budget_s", type=float, default=420.0,
                     help="N>1: wall-clock cap of the extra keys (a hang only drops keys)")
     ap.add_argument("--time_budget_s", type=float, default=480.0,
@@ -99,6 +102,8 @@ def parse():
                     help="N>1 without a launcher: wall-clock limit of the self-launched job "
                          "(-1 = --time_budget_s + 240 s)")
     a = ap.parse_args()
+    if a.verify_images < 0:
+        a.verify_images = 256 if a.cpu else VERIFY_IMAGES
     if a.launch_timeout < 0:
         a.launch_timeout = a.time_budget_s + 240.0
     return a
@@ -283,6 +288,7 @@ def bench_pp2(args, info):
     n = N // 2
     stage = r % 2
     s0, s1 = stages_for(dev, 1, args.precision)
+    args._stages = (s0, s1)  # for the distributed correctness check (pp2_verify)
     M = max(1, args.microbatches)
     mb = (args.batch // M) // n * n  # rows per microbatch, split evenly over the N/2 receivers
     if mb < n:
@@ -384,11 +390,14 @@ def hop_bandwidth(info, nbytes: int, reps: int = 4, timeout_s: float = 60.0) -> 
     return nbytes * reps / el / 1e9 if el > 0 else float("nan")
 
 
+DEADLINE_RC = 3  # exit status of a run a Deadline cut short (its line is printed first)
+
+
 class Deadline:
     """A wall-clock backstop for a multi-rank section: if the block is still
     running after ``seconds``, rank 0 prints the line it has (noting what was
-    cut) and every rank exits 0, so a hang only drops keys and never the
-    headline."""
+    cut) and every rank exits with ``DEADLINE_RC``: a hang drops keys, never
+    the headline, and still shows in the job's exit status."""
 
     def __init__(self, seconds: float, line, what: str):
         import threading
@@ -398,7 +407,10 @@ class Deadline:
             if line is not None:
                 line["extras_error"] = f"{self.what} exceeded its {seconds:.0f} s budget; skipped"
                 print(json.dumps(line), flush=True)
-            os._exit(0)
+            else:
+                time.sleep(3.0)  # rank 0 prints first: a launcher stops the job at the first exit
+            sys.stdout.flush()
+            os._exit(DEADLINE_RC)
         self.timer = threading.Timer(max(1.0, seconds), bail)
         self.timer.daemon = True
 
@@ -447,6 +459,98 @@ def pp2_latency(args, info, s0, s1, back) -> float:
         dsync(dev)
     sync_time(info)
     return statistics.median(ts) * 1e3 if ts else float("nan")
+
+
+VERIFY_IMAGES = 4096  # images each stage-0 GPU pushes through the distributed correctness check
+
+
+def golden_probs(dev, x: torch.Tensor) -> torch.Tensor:
+    """fp32 torch probabilities of the benchmarked weights (TF32 off): the oracle
+    of ``precision_check`` and of the distributed check."""
+    from distributed_neural_networks_amd import checkpoint as ckpt
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
+    ref = NeuralNetwork().to(dev).eval()
+    ref.load_state_dict(ckpt.random_stage_state_dict("cifar10", 0, 3, True, True, 0))
+    tf32 = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        with torch.no_grad():
+            return ref(x)
+    finally:
+        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
+
+
+def pp2_verify(info, s0, s1, n_img: int = VERIFY_IMAGES) -> dict:
+    """The answer that crossed the hops, checked (the
+    reference's one check is the prediction that comes back over the hop,
+    ``node.py:58-68``, ``node.py:184-192``).  Every stage-0 GPU pushes a fixed
+    seeded set of ``n_img`` images through the *distributed* pipeline the
+    headline measured: its stage-0 kernel, the bipartite ``SplitLink`` hop to
+    every stage-1 GPU, their stage-1 kernels; each stage-1 GPU returns the
+    probabilities and its per-row predictions of every slice to the stage-0
+    GPU the slice came from, over the back-edge communicator
+    (``return_to_node_id``).  The stage-0 GPU compares what came back with the
+    fp32 torch model on the same images.  Job-wide: argmax agreement (sum of
+    matches over every stage-0 GPU's images), max |dprob| (max over them), and
+    whether the returned predictions are the argmax of the returned
+    probabilities.  Outside every timed region."""
+    import torch.distributed as dist
+    from distributed_neural_networks_amd.parallel import comm
+    from distributed_neural_networks_amd.parallel.links import SplitLink, make_link
+    dev, N, r = info.device, info.world, info.rank
+    n = N // 2
+    back = comm.back_group()
+    vmb = max(n, (1024 if dev.type == "cuda" else 32) // n * n)  # rows per microbatch, split over n receivers
+    V = max(vmb, n_img // vmb * vmb)
+    stats = torch.zeros(4, dtype=torch.float64, device=dev)  # matches, images, max|dp|, pred==argmax(probs)
+    if r % 2 == 0:
+        g = torch.Generator(device=dev).manual_seed(7000 + r)
+        x = torch.randn((V, 3, 32, 32), device=dev, generator=g)
+        fwd = SplitLink([make_link(2 * j + 1, dev) for j in range(n)])
+        ret = SplitLink([make_link(2 * j + 1, dev, back) for j in range(n)])
+        sh, dt = s0.out_spec(vmb)
+        y = torch.empty(sh, dtype=dt, device=dev)
+        probs = torch.full((V, 10), float("nan"), device=dev)
+        pred = torch.full((V,), -1, dtype=torch.int32, device=dev)
+        for i in range(V // vmb):
+            s0.forward(x[i * vmb:(i + 1) * vmb], y)
+            w = fwd.isend(y)
+            rp = ret.irecv(probs[i * vmb:(i + 1) * vmb])
+            rq = ret.irecv(pred[i * vmb:(i + 1) * vmb])
+            for wk in (w, rp, rq):
+                wk.wait()
+        dsync(dev)
+        p = golden_probs(dev, x)
+        stats[0] = float((pred.long() == p.argmax(1)).sum().item())
+        stats[1] = float(V)
+        stats[2] = float((probs - p).abs().max().item()) if bool(torch.isfinite(probs).all()) else float("inf")
+        stats[3] = float((pred.long() == probs.argmax(1)).sum().item())
+    else:
+        prev = SplitLink([make_link(2 * a, dev) for a in range(n)])
+        ret = SplitLink([make_link(2 * a, dev, back) for a in range(n)])
+        sh, dt = s1.in_spec(vmb)
+        yin = torch.empty(sh, dtype=dt, device=dev)
+        pbuf = torch.empty((vmb, 10), device=dev)
+        corrupt = os.environ.get("DNN_TEST_CORRUPT_VERIFY") == "1"  # tests: the check must see a bad hop
+        for _ in range(V // vmb):
+            prev.recv(yin)
+            if corrupt:
+                yin[::7].mul_(-1.0)
+            out = s1.forward(yin, pbuf)
+            ret.send(out.probs.contiguous())
+            ret.send(out.pred.contiguous())
+        dsync(dev)
+    mx = torch.tensor([stats[2].item()], dtype=torch.float64, device=dev)
+    sm = stats[[0, 1, 3]].clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm)
+    matches, imgs, self_ok = (float(v) for v in sm.tolist())
+    return {"dist_argmax_agreement_vs_fp32_torch": round(matches / imgs, 6) if imgs else None,
+            "dist_max_abs_dprob": float(mx.item()),
+            "dist_pred_is_argmax_of_returned_probs": round(self_ok / imgs, 6) if imgs else None,
+            "dist_verify_images": int(imgs),
+            "dist_verify_path": f"stage 0 x{n} -> bipartite hop -> stage 1 x{n} -> probs + preds back over the "
+                                f"back-edge, vs fp32 torch"}
 
 
 def bench_fc1cut(args, info):
@@ -658,22 +762,12 @@ def precision_check(dev, precision: str, n_img: int = 4096) -> dict:
     """max|dprob| and argmax agreement of the HIP pipeline (the benchmarked
     stages and weights) against the fp32 torch model (TF32 off), on n_img
     random images.  Outside every timed region."""
-    from distributed_neural_networks_amd import checkpoint as ckpt
-    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
     from distributed_neural_networks_amd.runtime.pipeline import ColocatedPipeline
     s0, s1 = stages_for(dev, 1, precision)
-    ref = NeuralNetwork().to(dev).eval()
-    ref.load_state_dict(ckpt.random_stage_state_dict("cifar10", 0, 3, True, True, 0))
     g = torch.Generator(device=dev).manual_seed(11)
     x = torch.randn((n_img, 3, 32, 32), device=dev, generator=g)
     out = ColocatedPipeline([s0, s1], n_img)(x)
-    tf32 = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
-    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
-    try:
-        with torch.no_grad():
-            p = ref(x)
-    finally:
-        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
+    p = golden_probs(dev, x)
     dsync(dev)
     return {"max_abs_dprob_vs_fp32_torch": float((out.probs - p).abs().max().item()),
             "argmax_agreement_vs_fp32_torch": round(float((out.pred.long() == p.argmax(1)).float().mean().item()), 6),
@@ -761,6 +855,20 @@ def main():
             out.update(precision_check(info.device, args.precision, 16384))
             phases["precision_check_s"] = round(time.perf_counter() - tp, 2)
         out.update(extra)
+    if N > 1 and args.placement == "pp2" and args.verify_images > 0:
+        # the answer that crossed the hops, against fp32 torch (pp2_verify)
+        tp = time.perf_counter()
+        try:
+            with Deadline(min(120.0, max(10.0, args.time_budget_s - elapsed_s() - EXTRAS_MARGIN_S)), out,
+                          "distributed correctness check"):
+                with rccl.scope(info.device):
+                    ver = pp2_verify(info, *args._stages, n_img=args.verify_images)
+            if out is not None:
+                out.update(ver)
+        except Exception as e:  # noqa: BLE001 — reported in the line, never silently dropped
+            if out is not None:
+                out["dist_verify_error"] = f"{type(e).__name__}: {e}"[:200]
+        phases["dist_verify_s"] = round(time.perf_counter() - tp, 2)
     if N > 1 and args.placement == "pp2":
         tp = time.perf_counter()
         try:
@@ -877,6 +985,10 @@ def multi_gpu_extras(args, info, line, phases):
                 line[key + "_decode_ms_per_step"] = g["ms_per_step"]
                 line[key + "_prefill_tok_s"] = g["prefill_tokens_per_s"]
                 line[key + "_p50_token_ms"] = g["decode_p50_token_latency_ms"]
+                for k in ("dist_token_agreement_vs_colocated", "dist_first_token_agreement_vs_colocated",
+                          "dist_verify_tokens", "dist_verify_steps"):
+                    if k in g:
+                        line[key + "_" + k] = g[k]
                 line[key + "_config"] = dict(
                     c, model=label if cuda else f"{c['model']} (gloo schedule test)",
                     placement=f"{c['gpu_groups']} GPU groups x {c['replicas']} replicas, decode ring over "

@@ -57,6 +57,11 @@ def parse(argv=None):
     ap.add_argument("--gloo_gpu", action="store_true",
                     help="every rank on GPU 0 (HIP kernels + graphs), hops staged through host memory over gloo "
                          "(the 1-GPU box's multi-process schedule test; RCCL refuses two ranks on one GPU)")
+    ap.add_argument("--verify_steps", type=int, default=-1,
+                    help="after the timed run: greedy tokens of this many steps of the distributed ring on fixed "
+                         "seeded prompts, against the same stages colocated on rank 0's device "
+                         "(-1 = 8 when the ring spans several GPU groups, else 0)")
+    ap.add_argument("--verify_prompt", type=int, default=64, help="prompt length of the --verify_steps check")
     ap.add_argument("--prepost_ab", type=int, default=0,
                     help="after the timed run: this many interleaved A/B pairs of decode runs without / with "
                          "the pre-posted next-microbatch receive (DecodeRing.prepost)")
@@ -82,6 +87,54 @@ def _build_group(model, ranges, stage_ids, dev, max_batch, max_seq, fp8, kv="bf1
                                     fp8_prefill=fp8_prefill))
         del sd
     return out
+
+
+def verify_ring(args, info, ring, grp, rep, groups, M, B, V, ranges, max_seq, fp8, kv, sync) -> dict:
+    """The tokens that crossed the hops, checked: the
+    distributed ring generates ``--verify_steps`` greedy tokens for fixed
+    seeded prompts (every microbatch, ``--verify_prompt`` tokens each), then
+    rank 0 builds every stage of the model on its own device (same weights:
+    ``random_stage_state_dict`` is seeded per stage) as a one-group ring and
+    generates from the same prompts.  Returns, on rank 0, the fraction of
+    (sequence, step) tokens the two agree on and that of the first (prefill)
+    token.  Every rank runs the same collectives; idle ranks only join the
+    barriers.  Outside every timed region."""
+    from distributed_neural_networks_amd.runtime.scheduler import DecodeRing, RingLinks
+    steps = args.verify_steps if args.verify_steps > 0 else 8
+    Tv = max(1, min(args.verify_prompt, max_seq - steps - 2))
+    g = torch.Generator().manual_seed(4242)
+    prompts = [torch.randint(0, V, (B, Tv), generator=g, dtype=torch.int32) for _ in range(M)]
+    dev = info.device
+    sync()
+    toks = None
+    if ring is not None:
+        ring.record = True
+        mine = [p.to(dev) for p in prompts] if grp == 0 else None
+        if mine is not None and os.environ.get("DNN_TEST_CORRUPT_VERIFY") == "1":  # tests: a wrong ring must show
+            mine[0] = (mine[0] + 1) % V
+        toks = ring.generate(mine, Tv, steps)
+        ring.record = False
+    sync()
+    res = {}
+    if info.rank == 0:
+        S = len(ranges)
+        stages = _build_group(args.model, ranges, list(range(S)), dev, B * M, max_seq, fp8, kv,
+                              getattr(args, "kv_scale", "calibrated"), getattr(args, "fp8_prefill", "e4m3"))
+        ref = DecodeRing(stages, RingLinks(), 1, M, B, use_graphs=not args.no_graph, record=True)
+        want = ref.generate([p.to(dev) for p in prompts], Tv, steps)
+        del ref, stages
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+        got = toks
+        ok = (got == want) if got is not None and got.shape == want.shape else torch.zeros_like(want, dtype=torch.bool)
+        res = {"dist_token_agreement_vs_colocated": round(float(ok.float().mean().item()), 6),
+               "dist_first_token_agreement_vs_colocated": round(float(ok[:, 0].float().mean().item()), 6),
+               "dist_verify_tokens": int(want.numel()), "dist_verify_steps": steps, "dist_verify_prompt_len": Tv,
+               "dist_verify_path": f"{groups} GPU groups over the hops + token back-edge vs all stages colocated "
+                                   f"on rank 0"}
+    sync()
+    return res
 
 
 def main(args=None):
@@ -232,6 +285,11 @@ def run(args=None, shutdown: bool = True):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    vsteps = getattr(args, "verify_steps", -1)
+    if vsteps < 0:
+        vsteps = 8 if groups > 1 else 0
+    ver = verify_ring(args, info, ring, grp, rep, groups, M, B, V, ranges, max_seq, fp8, kv, sync) if vsteps else {}
+
     ab = {}
     if getattr(args, "prepost_ab", 0) and ring is not None:
         # interleaved A/B of the decode schedule: each input received just before
@@ -277,6 +335,7 @@ def run(args=None, shutdown: bool = True):
                        "global_batch": B * M * replicas, "parallelism": f"pp{groups}x dp{replicas}"},
         }
         out.update(ab)
+        out.update(ver)
     if N > 1 and shutdown:
         comm.shutdown()
     return out if r == 0 else None

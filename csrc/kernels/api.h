@@ -45,6 +45,7 @@ int dnn_gemm_set_stream(int on, long long min_bytes, int fold = -1);
 // (mt, ntw, steps, splitk) pins that config for every eligible call (A/B probes)
 int dnn_gemm_set_oneshot(int on, int mt, int ntw, int steps, int splitk);
 int dnn_gemm_set_oneshot_lds_floor(int bytes);
+int dnn_gemm_set_oneshot_probe(void* rec);  // race probe records (nullptr = off)
 int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
                            int K, int mt, int ntw, int steps, int splitk, int w8, void* ws, long long ws_bytes,
                            hipStream_t st);

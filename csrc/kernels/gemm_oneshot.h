@@ -77,6 +77,13 @@ constexpr int os_lds_bytes() {
 // (row-statistics partials, epilogue operands) are still retired by counted
 // waits: plain loads complete in order among themselves.
 // tests/test_isa_lds_dma_order.py checks the sequence in the product ISA.
+constexpr int OS_PROBE_WORDS = 1024;  // ABL 256 record per workgroup (int32 words)
+
+__device__ __forceinline__ char* os_probe_lds() {
+  extern __shared__ __attribute__((aligned(1024))) char os_lds[];
+  return os_lds;
+}
+
 __device__ __forceinline__ void os_image_sync() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -96,6 +103,18 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
                                                               int rs_ld_in = 0, int epi_pre = 1) {
   if constexpr ((ABL & 32) != 0) return;
   using Cfg = StrCfg<W8>;
+  // ABL 256 (race probe only, bench/probes/oneshot_race_probe.py): ``slab`` is
+  // a per-workgroup int32 record (OS_PROBE_WORDS), ``rs_ld_in`` the launch's
+  // dynamic LDS bytes; the LDS past the kernel's own os_lds_bytes is filled
+  // with a canary and checked at exit, and the row statistics are taken a
+  // second time from the image after the MFMAs (early vs late).
+  [[maybe_unused]] uint64_t prb_t0 = 0;
+  if constexpr ((ABL & 256) != 0) {
+    prb_t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(os_probe_lds());
+    for (int i = os_lds_bytes<MT, STEPS>() / 4 + (int)threadIdx.x; i < rs_ld_in / 4; i += 256) w32[i] = 0xA5A5A5A5u ^ i;
+    __syncthreads();
+  }
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
   constexpr int BN = 16 * NTW;
@@ -325,6 +344,53 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     }
   }
 
+  // ABL 256: the same statistics again from the image, after the MFMAs
+  [[maybe_unused]] float prb_l1[MT], prb_l2[MT];
+  if constexpr ((ABL & 256) != 0 && NORM != 0) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) prb_l1[t] = prb_l2[t] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int s = c / CS, cc = c % CS;
+      if (c < nvalid) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int h = 0; h < AU; ++h) {
+            const int row = 16 * t + fr;
+            const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
+            const bf16x8 a8 =
+                *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
+            str_stats<NORM>(a8, shift[t], prb_l1[t], prb_l2[t]);
+          }
+      }
+    }
+    int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      bad |= prb_l1[t] != s1s[t] || prb_l2[t] != s2s[t];
+      float e1 = s1s[t], e2 = s2s[t], l1 = prb_l1[t], l2 = prb_l2[t];
+      e1 += __shfl_xor(e1, 16, 64);
+      e1 += __shfl_xor(e1, 32, 64);
+      e2 += __shfl_xor(e2, 16, 64);
+      e2 += __shfl_xor(e2, 32, 64);
+      l1 += __shfl_xor(l1, 16, 64);
+      l1 += __shfl_xor(l1, 32, 64);
+      l2 += __shfl_xor(l2, 16, 64);
+      l2 += __shfl_xor(l2, 32, 64);
+      if (lane < 16 && t < 2) {
+        float* f = reinterpret_cast<float*>(rec) + 16 + ((wave * 2 + t) * 16 + lane) * 4;
+        f[0] = e1;
+        f[1] = e2;
+        f[2] = l1;
+        f[3] = l2;
+      }
+    }
+    const int nbad = __builtin_popcountll(__ballot(bad));
+    if (lane == 0) rec[10 + wave] = nbad;
+  }
+
   // ---- row statistics of this wave's K range: the 4 lane groups hold disjoint k
   if (NORM != 0 && !rsi) {
 #pragma unroll
@@ -437,6 +503,26 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       } else {
         epi_t4<ACT, false>(v, m, n, M, N, Cv, ldc, bias, R, ldr, vec);
       }
+    }
+  }
+  if constexpr ((ABL & 256) != 0) {
+    __syncthreads();
+    int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(os_lds);
+    int nbad = 0;
+    for (int i = os_lds_bytes<MT, STEPS>() / 4 + tid; i < rs_ld_in / 4; i += 256) nbad += w32[i] != (0xA5A5A5A5u ^ i);
+    nbad = (int)wave_sum((float)nbad);
+    if (lane == 0) rec[6 + wave] = nbad;
+    if (tid == 0) {
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      rec[0] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID: wave/simd/cu/sh/se ids
+      rec[1] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      rec[2] = (int)(uint32_t)prb_t0;
+      rec[3] = (int)(uint32_t)(prb_t0 >> 32);
+      rec[4] = (int)(uint32_t)t1;
+      rec[5] = (int)(uint32_t)(t1 >> 32);
+      rec[14] = rs_ld_in;
+      rec[15] = (int)blockIdx.x;
     }
   }
 }

@@ -552,6 +552,14 @@ extern "C" int dnn_gemm_set_oneshot_lds_floor(int bytes) {
   return 0;
 }
 static int g_os_pin[4] = {0, 0, 0, 0};              // mt, ntw, steps, splitk (0 = planned)
+// race probe (bench/probes/oneshot_race_probe.py): non-null = the instrumented
+// ABL 256 variant of the forced LN + GELU shapes (MT 2, STEPS 1, bf16) writes
+// one OS_PROBE_WORDS record per workgroup here
+static int* g_os_probe = nullptr;
+extern "C" int dnn_gemm_set_oneshot_probe(void* rec) {
+  g_os_probe = static_cast<int*>(rec);
+  return 0;
+}
 
 struct OsCfg {
   int mt = 0, ntw = 0, steps = 0, splitk = 1;
@@ -642,6 +650,15 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
     // output); merged partials of the input when they fit OS_RS_SPT per thread
     float2* rso = ACT != ACT_SILU_MUL ? g_rs_cur.out : nullptr;
     const float2* rsi = (NORM != 0 && (kelems + 15) / 16 <= OS_RS_SPT * (256 / MP)) ? g_rs_cur.in : nullptr;
+    if constexpr (ABL == 0 && MT == 2 && STEPS == 1 && !W8 && NORM == 2 && ACT == ACT_GELU && NTW <= 2) {
+      if (g_os_probe != nullptr && rsi == nullptr) {
+        hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, 256>), grid, block, smem, st,
+                           (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M,
+                           N, nch, cps, colsum, eps, kelems, (float*)g_os_probe, ntiles, mgroups, nullptr, 0, nullptr,
+                           (int)smem, g_epi_pre);
+        return (int)hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, ABL>), grid, block, smem, st,
                        (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N,
                        nch, cps, colsum, eps, kelems, (float*)nullptr, ntiles, mgroups, rso, g_rs_cur.out_ld, rsi,

@@ -286,12 +286,41 @@ def test_bench_pp2_schedule_cpu(n, launcher):
     assert "hop_GBps_error" not in d and d["hop_GBps_per_pair"] > 0
     assert d["hop_bound_images_per_s"] == pytest.approx((n // 2) * d["hop_GBps_per_pair"] * 1e9 / 16384, rel=0.02)
     assert "extras_error" not in d and d["fc1cut_images_per_s"] > 0
+    # the answer that crossed the hops: every stage-0 rank's
+    # images through the distributed pipeline and back, against fp32 torch
+    assert "dist_verify_error" not in d, d.get("dist_verify_error")
+    assert d["dist_argmax_agreement_vs_fp32_torch"] == 1.0
+    assert d["dist_pred_is_argmax_of_returned_probs"] == 1.0
+    assert d["dist_max_abs_dprob"] < 1e-5
+    assert d["dist_verify_images"] == (n // 2) * 256
     for key, groups in (("gpt2_4stage", min(n, 4)), ("llama3_8b_8stage_b32", min(n, 4)),
                         ("gpt2xl_fp8_8stage_b64", min(n, 4))):
         assert key + "_error" not in d, d.get(key + "_error")
         assert d[key + "_decode_tok_s"] > 0 and d[key + "_prefill_tok_s"] > 0
         assert d[key + "_p50_token_ms"] > 0
         assert d[key + "_config"]["gpu_groups"] == groups
+        # the ring's greedy tokens vs the same stages colocated on rank 0
+        assert d[key + "_dist_token_agreement_vs_colocated"] == 1.0, key
+        assert d[key + "_dist_verify_tokens"] == 8 * d[key + "_config"]["global_batch"] // d[key + "_config"]["replicas"]
+
+
+def test_bench_verify_sees_a_bad_hop_cpu(monkeypatch):
+    """The distributed checks are not vacuous: with the stage-1 input of the
+    check corrupted (every 7th row negated) and the ring's prompts changed for
+    one microbatch, the keys fall below 1."""
+    monkeypatch.setitem(ENV, "DNN_TEST_CORRUPT_VERIFY", "1")
+    d = _bench_cpu(2, "--no_extra")
+    assert d["dist_argmax_agreement_vs_fp32_torch"] < 1.0
+    assert d["dist_max_abs_dprob"] > 1e-3
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench", "gpt_bench.py"), "--gpus", "2",
+           "--cpu", "--model", "gpt2-tiny", "--stages", "2", "--batch", "2", "--prompt", "8", "--steps", "2",
+           "--warmup", "1", "--prefill_iters", "1"]
+    r = subprocess.run(cmd, env=dict(ENV, OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    g = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert g["dist_token_agreement_vs_colocated"] < 1.0
 
 
 def test_bench_gpus_must_match_world():
@@ -367,6 +396,7 @@ def test_gpt_decode_ring_bench_cpu(n):
     assert d["config"]["gpu_groups"] == 4 and d["config"]["replicas"] == n // 4
     assert d["config"]["microbatches"] == 4
     assert d["decode_p50_token_latency_ms"] > 0
+    assert d["dist_token_agreement_vs_colocated"] == 1.0 and d["dist_first_token_agreement_vs_colocated"] == 1.0
 
 
 # ----------------------------------------------------------------------------- failure detection
@@ -449,8 +479,18 @@ def test_cli_gloo_many_microbatches(cifar_setup):
     assert r0.returncode == 0, r0.stdout[-3000:] + r0.stderr[-3000:]
     lines = [l for l in r0.stdout.splitlines() if "***** FINAL PREDICTION (Index):" in l]
     assert len(lines) == 2
-    preds = json.loads(lines[0].split("(Index):")[1].split("*****")[0].strip())
-    assert len(preds) == 16 and preds[0] == _golden_pred(str(ck), str(img))
+    from distributed_neural_networks_amd.cli import cifar_request
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
+    m = NeuralNetwork().eval()
+    m.load_state_dict(torch.load(str(ck), weights_only=True))
+
+    class A:
+        input_image = str(img)
+    for req, line in enumerate(lines):  # every row that crossed the hop and came back
+        preds = json.loads(line.split("(Index):")[1].split("*****")[0].strip())
+        with torch.no_grad():
+            assert preds == m(cifar_request(A, "t", 16, req)).argmax(1).tolist()
+    assert json.loads(lines[0].split("(Index):")[1].split("*****")[0].strip())[0] == _golden_pred(str(ck), str(img))
 
 
 def test_cli_gloo_stage_build_failure_aborts_peers(cifar_setup):

@@ -40,16 +40,40 @@ def _bench(*args, timeout=600):
     return json.loads(lines[0])
 
 
-def test_bench_pp2_headline_two_gpus():
+def _need(n):
+    import torch
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs, {torch.cuda.device_count()} visible")
+
+
+def _check_dist_verify(d, n):
+    """The answer that crossed the hops (bench.py pp2_verify): every stage-0
+    GPU's 4096 images through the bipartite hop and back over the back-edge,
+    against fp32 torch (one GPU measures argmax agreement 1.0 and max|dprob|
+    3.3e-7 on 16384 images with the same kernels)."""
+    assert "dist_verify_error" not in d, d.get("dist_verify_error")
+    assert d["dist_verify_images"] == (n // 2) * 4096
+    assert d["dist_argmax_agreement_vs_fp32_torch"] == 1.0
+    assert d["dist_pred_is_argmax_of_returned_probs"] == 1.0
+    assert d["dist_max_abs_dprob"] < 1e-5
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_pp2_headline(n):
     """The N > 1 headline: the reference cut, one stage per GPU, the hop over
-    this package's native RCCL channels (not a ProcessGroupNCCL fallback)."""
-    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "8192", "--latency_iters", "5",
+    this package's native RCCL channels (not a ProcessGroupNCCL fallback);
+    at 4 and 8 GPUs the bipartite SplitLink hop the driver's scaling run takes.
+    The line must carry the distributed correctness keys at 1.0."""
+    _need(n)
+    d = _bench("--gpus", str(n), "--steps", "3", "--warmup", "1", "--batch", "8192", "--latency_iters", "5",
                "--no_extra")
-    assert d["n_gpus"] == 2 and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
+    assert d["n_gpus"] == n and d["value"] > 0 and d["metric"] == "images/sec CIFAR-10 2-stage"
     assert d["config"]["p2p"] == "native"
     assert d["config"]["stage_cut"] == REF_CUT
-    assert d["config"]["parallelism"] == "pp2-rccl-1x1"
+    k = n // 2
+    assert d["config"]["parallelism"] == f"pp2-rccl-{k}x{k}" + ("-bipartite" if k > 1 else "")
     assert d["p50_latency_ms"] is not None and d["p50_latency_ms"] > 0
+    _check_dist_verify(d, n)
 
 
 def test_bench_fc1cut_two_gpus():
@@ -59,17 +83,22 @@ def test_bench_fc1cut_two_gpus():
     assert d["config"]["stage_cut"].startswith("conv+fc1|fc2")
 
 
-def test_bench_full_line_two_gpus():
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_full_line(n):
     """The complete multi-GPU line the driver records: headline plus the
-    fc1-cut and the BASELINE config 3/4/5 decode rings over RCCL."""
-    d = _bench("--gpus", "2", "--steps", "5", "--warmup", "2", timeout=1100)
-    assert d["n_gpus"] == 2 and d["config"]["p2p"] == "native" and d["config"]["stage_cut"] == REF_CUT
+    fc1-cut and the BASELINE config 3/4/5 decode rings over RCCL, each ring's
+    greedy tokens equal to the same stages colocated on rank 0's GPU."""
+    _need(n)
+    d = _bench("--gpus", str(n), "--steps", "5", "--warmup", "2", timeout=1100)
+    assert d["n_gpus"] == n and d["config"]["p2p"] == "native" and d["config"]["stage_cut"] == REF_CUT
     assert "extras_error" not in d, d.get("extras_error")
     assert d["fc1cut_images_per_s"] > 0
-    for key in ("gpt2_4stage", "llama3_8b_8stage_b32", "gpt2xl_fp8_8stage_b64"):
+    _check_dist_verify(d, n)
+    for key, stages in (("gpt2_4stage", 4), ("llama3_8b_8stage_b32", 8), ("gpt2xl_fp8_8stage_b64", 8)):
         assert key + "_error" not in d, d.get(key + "_error")
         assert d[key + "_decode_tok_s"] > 0 and d[key + "_prefill_tok_s"] > 0 and d[key + "_p50_token_ms"] > 0
-        assert d[key + "_config"]["gpu_groups"] == 2
+        assert d[key + "_config"]["gpu_groups"] == min(n, stages)
+        assert d[key + "_dist_token_agreement_vs_colocated"] == 1.0, key
 
 
 def test_bench_gpt2_pipeline_two_gpus():
@@ -79,18 +108,42 @@ def test_bench_gpt2_pipeline_two_gpus():
 
 
 def test_cli_rccl_two_stage(tmp_path):
-    """node.py CLI on configs/cifar_2gpu_rccl.json: one stage per GPU, RCCL P2P."""
+    """node.py CLI on configs/cifar_2gpu_rccl.json: one stage per GPU, RCCL P2P.
+    Each request (the input image plus 7 seeded images, 2 microbatches of 4)
+    crosses the hop and its predictions come back over the back-edge; every
+    printed prediction must equal the fp32 torch model's (the reference's one
+    check, ``node.py:184-192``)."""
+    import numpy as np
+    import torch
+    from PIL import Image
+    from distributed_neural_networks_amd.cli import cifar_request
+    from distributed_neural_networks_amd.models.cifar import NeuralNetwork
     from distributed_neural_networks_amd.tools import make_checkpoint
     ck = tmp_path / "cifar10_model.pth"
     make_checkpoint.main(["--out", str(ck)])
+    img = tmp_path / "img.png"
+    Image.fromarray(np.random.default_rng(0).integers(0, 255, (40, 48, 3), dtype=np.uint8)).save(img)
     cfg = json.load(open(os.path.join(ROOT, "configs", "cifar_2gpu_rccl.json")))
     cfg["model_weights"] = str(ck)
+    cfg["micro_batch_size"], cfg["num_microbatches"] = 4, 2
     for i, n in enumerate(cfg["nodes"]):
         n["address"] = f"127.0.0.1:{_port()}"
     p = tmp_path / "cfg.json"
     p.write_text(json.dumps(cfg))
     r = subprocess.run([sys.executable, "-m", "distributed_neural_networks_amd.tools.launch", "--config", str(p),
-                        "--num_requests", "3", "--timeout", "240"], env=ENV, capture_output=True, text=True,
-                       timeout=300, cwd=ROOT)
+                        "--num_requests", "3", "--input_image", str(img), "--timeout", "240"], env=ENV,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    out = r.stdout + r.stderr
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    assert "FINAL PREDICTION" in r.stdout + r.stderr
+    lines = [l for l in out.splitlines() if "***** FINAL PREDICTION (Index):" in l]
+    assert len(lines) == 3, out[-3000:]
+    m = NeuralNetwork().eval()
+    m.load_state_dict(torch.load(str(ck), weights_only=True))
+
+    class A:
+        input_image = str(img)
+    for req, line in enumerate(lines):
+        got = json.loads(line.split("(Index):")[1].split("*****")[0].strip())
+        with torch.no_grad():
+            want = m(cifar_request(A, "t", 8, req)).argmax(1).tolist()
+        assert got == want, (req, got, want)
