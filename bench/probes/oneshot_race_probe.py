@@ -1,28 +1,19 @@
 """Root-cause probe of the one-shot decode GEMM race (VERDICT r5 item 2;
 csrc/kernels/gemm_oneshot.h "Retiring the image").
 
-Symptom (profiles/r5_oneshot_race_screen_*.jsonl): in ~1 of 150 forced
+Symptom (profiles/r5_oneshot_race_screen_*.jsonl): in ~2 % of forced
 LN + GELU calls at 2/1/1 (288 or 384 workgroups, two per CU) one workgroup's
 second 16-row tile (rows 16-31 of its m-group) comes out a few bf16 ulp off,
-in one 16-column tile; an 82 KB LDS floor (one workgroup per CU) hides it.
+in one 16-column tile: its row statistics, read from its own LDS-DMA image
+right after the wait + one barrier, saw a few pre-DMA bytes.
 
-Experiments, each a bit-for-bit comparison with a settled reference of the
-same launch over ``--iters`` calls, every call preceded by a call on other
-activations (the LDS holds someone else's data):
-
-  (a) floors: 0 (the kernel's own 66.5 KB: two workgroups per CU), 72 KB (two
-      per CU with an unused tail: an out-of-range LDS write would land in the
-      workgroup's own padding) and 82 KB (one per CU);
-  (b) the instrumented kernel (ABL 256): the LDS past the kernel's own size is
-      filled with a canary at entry and checked at exit (an out-of-range write
-      by the workgroup itself), and the row statistics are taken twice from
-      the image, right after the image sync (as the product does) and again
-      after the MFMAs: early != late means the image changed after it was
-      read; per-workgroup records also carry the hardware ids and
-      s_memrealtime stamps, so a failing workgroup's co-residents are named;
-  (c) the failing records' early / late statistics against the reference
-      call's: which of the two is the correct one.
-One JSON line per experiment."""
+Each experiment compares ``--iters`` calls bit for bit with a settled
+reference of the same launch; every call follows a call on other activations
+(the LDS holds someone else's bytes).  Probe bits (gemm_oneshot.h) select
+instrumented or alternative image syncs; profiles/r6_oneshot_race_root_cause.md
+tells the story of the round-6 runs (LDS floors 0 / 72 / 82 KB, an entry
+barrier, a detector, CK's split waits, ck_tile's vmcnt-only wait, a short
+s_sleep, a second barrier).  One JSON line per experiment."""
 import argparse
 import json
 import os
@@ -60,115 +51,114 @@ def setup(N, K, dev):
     return (lambda a: linear_norm(a, f, act="gelu", ws=ws, out=out)), x, x2
 
 
-def experiment(name, N, K, pin, floor, probe, iters, dev):
+def experiment(name, N, K, pin, floor, abl, iters, dev):
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.gemm import set_oneshot_gemm
     set_oneshot_gemm(2, *pin)
     lib().gemm_set_oneshot_lds_floor(floor)
     run, x, x2 = setup(N, K, dev)
-    rec = torch.zeros((4096, WORDS), dtype=torch.int32, device=dev) if probe else None
-    lib().gemm_set_oneshot_probe(rec.data_ptr() if probe else 0)
+    det = bool(abl & 256)
+    rec = torch.zeros((4096, WORDS), dtype=torch.int32, device=dev)
+    check(lib().gemm_set_oneshot_probe(rec.data_ptr() if abl else 0, abl))
     try:
         run(x)
         ref = run(x).clone()
-        ref_rec = rec.clone() if probe else None
-        nwg = int((ref_rec[:, 15] != 0).sum().item()) + 1 if probe else None  # blockIdx 0 writes 0
-        bad_calls, early_late_calls, canary_calls, worst, fails = 0, 0, 0, 0.0, []
+        torch.cuda.synchronize()
+        nwg = int((rec[:, 15] != 0).sum().item()) + 1 if det else None  # blockIdx 0 writes 0
+        bad_calls, det_calls, both, worst, fails = 0, 0, 0, 0.0, []
         for i in range(iters):
             run(x2)
+            if det:
+                rec[:, 16:16 + 256].zero_()
             o = run(x)
             d = (o.float() - ref.float()).abs()
             mism = bool((d > 0).any())
-            el = can = 0
-            if probe:
-                r = rec[:nwg]
-                el = int(r[:, 10:14].sum().item())
-                can = int(r[:, 6:10].sum().item())
-                early_late_calls += el > 0
-                canary_calls += can > 0
+            ev = 0
+            if det:
+                ev = int((rec[:nwg, 16:16 + 256] != 0).sum().item())
+                det_calls += ev > 0
+                both += ev > 0 and mism
             if mism:
                 bad_calls += 1
                 worst = max(worst, d.max().item())
-            if (mism or el or can) and len(fails) < 8:
+            if (mism or ev) and len(fails) < 8:
                 nz = (d > 0).nonzero()
                 f = {"call": i, "out_mismatch": mism, "n": int(nz.shape[0]),
                      "rows": sorted(set(nz[:, 0].tolist()))[:32], "col16_tiles": sorted(set((nz[:, 1] // 16).tolist())),
                      "max": d.max().item()}
-                if probe:
-                    f.update(analyse(rec[:nwg].cpu(), ref_rec[:nwg].cpu()))
+                if det:
+                    f.update(analyse(rec[:nwg].cpu(), pin[1], f["col16_tiles"]))
                 fails.append(f)
-        return {"exp": name, "N": N, "K": K, "pin": list(pin), "lds_floor": floor, "probe": probe, "iters": iters,
-                "workgroups": nwg, "mismatched_calls": bad_calls, "max": worst,
-                "early_late_calls": early_late_calls, "canary_calls": canary_calls, "fails": fails}
+        return {"exp": name, "N": N, "K": K, "pin": list(pin), "lds_floor": floor, "abl": abl, "iters": iters,
+                "workgroups": nwg, "mismatched_calls": bad_calls, "max": worst, "detector_calls": det_calls,
+                "detector_and_output_calls": both, "fails": fails}
     finally:
-        lib().gemm_set_oneshot_probe(0)
+        lib().gemm_set_oneshot_probe(0, 0)
 
 
-def analyse(r, ref):
-    """Which workgroups / waves / tiles saw early != late, how each compares
-    with the reference call's statistics, and who shared their CU."""
-    out = {"wg_early_late": [], "wg_canary": []}
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f"probe call failed: {rc}")
+
+
+def analyse(r, ntw, tiles):
+    """Per workgroup whose detector fired: which statistics-pass reads changed
+    after they were made, decoded into (row of the m-group, 16-B K slot, the
+    LDS slot it sits in, and the DMA instruction / lane that wrote it); plus
+    the output tiles of the same call and who shared the CU."""
+    out = []
     keys = [cu_key(r[i]) for i in range(r.shape[0])]
-    span = [(stamp(r[i], 2), stamp(r[i], 4)) for i in range(r.shape[0])]
     for lg in range(r.shape[0]):
-        el = r[lg, 10:14].tolist()
-        if any(el):
-            f = r[lg, 16:16 + 4 * 2 * 16 * 4].view(torch.float32).view(4, 2, 16, 4)
-            fr = ref[lg, 16:16 + 4 * 2 * 16 * 4].view(torch.float32).view(4, 2, 16, 4)
-            waves = []
-            for w in range(4):
-                for t in range(2):
-                    e, late, refv = f[w, t, :, :2], f[w, t, :, 2:], fr[w, t, :, :2]
-                    de = (e - refv).abs().max().item()
-                    dl = (late - refv).abs().max().item()
-                    if de > 0 or dl > 0:
-                        rows = ((e - refv).abs().sum(1) > 0).nonzero().flatten().tolist()
-                        waves.append({"wave": w, "t": t, "early_vs_ref": de, "late_vs_ref": dl,
-                                      "rows_early_off": rows, "ref_s1_mean_abs": refv[:, 0].abs().mean().item()})
-            co = [j for j in range(r.shape[0]) if j != lg and keys[j] == keys[lg]
-                  and span[j][0] < span[lg][1] and span[lg][0] < span[j][1]]
-            out["wg_early_late"].append({"lg": lg, "lanes_per_wave": el, "cu": list(keys[lg]),
-                                         "co_resident_lg": co, "waves": waves[:8]})
-        if any(r[lg, 6:10].tolist()):
-            out["wg_canary"].append({"lg": lg, "bad_words_per_wave": r[lg, 6:10].tolist()})
-    out["wg_early_late"] = out["wg_early_late"][:6]
-    out["wg_canary"] = out["wg_canary"][:6]
-    # co-residency census of the whole call
-    from collections import Counter
-    c = Counter(keys)
-    out["cus_used"] = len(c)
-    out["max_wg_per_cu"] = max(c.values())
-    return out
+        m = r[lg, 16:16 + 256]
+        if not bool((m != 0).any()):
+            continue
+        reads = []
+        for w in range(4):
+            for lane in range(64):
+                mask = int(m[w * 64 + lane]) & 0xFFFFFFFF
+                for bit in range(32):
+                    if mask >> bit & 1:
+                        c, t = bit // 2, bit % 2
+                        fr, fg = lane & 15, lane >> 4
+                        row = 16 * t + fr
+                        slot = c * 4 + fg                      # 16-B K slot within the wave's 512-B step row
+                        phys = slot ^ (row & 15)               # LDS slot it sits in
+                        reads.append({"wave": w, "row": row, "k_slot": slot, "lds_slot": phys,
+                                      "dma_instr": row // 2, "dma_lane": (row & 1) * 32 + phys})
+        mg, rest = lg % 2, lg // 2
+        out.append({"lg": lg, "mgroup": mg, "col_tile": rest, "cu": list(keys[lg]),
+                    "same_cu_lg": [j for j in range(r.shape[0]) if j != lg and keys[j] == keys[lg]][:8],
+                    "n_reads": len(reads), "reads": reads[:12]})
+    return {"detector_wgs": out[:4], "n_detector_wgs": len(out)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--exps", default="")
+    ap.add_argument("--control_iters", type=int, default=3000)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     from distributed_neural_networks_amd.ops._lib import lib
     from distributed_neural_networks_amd.ops.gemm import set_oneshot_gemm
     KB = 1024
     exps = [
-        # (a) plain product kernel, three floors, two grids
-        ("a_2304_floor0", 2304, 768, (2, 1, 1, 1), 0, False),
-        ("a_2304_floor72", 2304, 768, (2, 1, 1, 1), 72 * KB, False),
-        ("a_2304_floor82", 2304, 768, (2, 1, 1, 1), 82 * KB, False),
-        ("a_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, False),
-        ("a_3072_floor72", 3072, 768, (2, 1, 1, 1), 72 * KB, False),
-        ("a_3072_ntw2_floor0", 3072, 768, (2, 2, 1, 1), 0, False),
-        # (b)/(c) instrumented kernel
-        ("b_2304_floor72", 2304, 768, (2, 1, 1, 1), 72 * KB, True),
-        ("b_3072_floor72", 3072, 768, (2, 1, 1, 1), 72 * KB, True),
-        ("b_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, True),
-        ("b_3072_ntw2_floor72", 3072, 768, (2, 2, 1, 1), 72 * KB, True),
+        # the product kernel (probe bits 0: the wait + TWO barriers before the
+        # first image read) at two workgroups per CU: floors 0 and 72 KB
+        ("p_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 0),
+        ("p_2304_floor0", 2304, 768, (2, 1, 1, 1), 0, 0),
+        ("p_3072_floor72", 3072, 768, (2, 1, 1, 1), 72 * KB, 0),
+        ("p_3072_ntw2_floor0", 3072, 768, (2, 2, 1, 1), 0, 0),
+        # positive control: the round-4/5 sequence (wait + ONE barrier)
+        ("c16384_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 16384),
+        ("c16384_3072_floor82", 3072, 768, (2, 1, 1, 1), 82 * KB, 16384),
     ]
     try:
-        for name, N, K, pin, floor, probe in exps:
+        for name, N, K, pin, floor, abl in exps:
             if a.exps and name not in a.exps.split(","):
                 continue
-            print(json.dumps(experiment(name, N, K, pin, floor, probe, a.iters, dev)), flush=True)
+            it = a.control_iters if name.startswith("c") else a.iters
+            print(json.dumps(experiment(name, N, K, pin, floor, abl, it, dev)), flush=True)
     finally:
         set_oneshot_gemm(1)
         lib().gemm_set_oneshot_lds_floor(82 * KB)

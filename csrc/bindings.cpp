@@ -66,7 +66,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
     return dnn_gemm_set_oneshot(on, mt, ntw, steps, splitk);
   }, py::arg("on"), py::arg("mt") = 0, py::arg("ntw") = 0, py::arg("steps") = 0, py::arg("splitk") = 0);
   m.def("gemm_set_oneshot_lds_floor", [](int bytes) { return dnn_gemm_set_oneshot_lds_floor(bytes); });
-  m.def("gemm_set_oneshot_probe", [](u64 rec) { return dnn_gemm_set_oneshot_probe(P(rec)); });
+  m.def("gemm_set_oneshot_probe", [](u64 rec, int abl) { return dnn_gemm_set_oneshot_probe(P(rec), abl); });
   m.def("gemm_set_head", [](int on) { return dnn_gemm_set_head(on); });
   m.def("gemm_set_split_tail", [](int on) { return dnn_gemm_set_split_tail(on); });
   m.def("gemm_head", [](u64 A, int lda, u64 Wsh, u64 sw, u64 colsum, u64 bias, float eps, int norm, u64 C, int ldc,

@@ -45,7 +45,8 @@ int dnn_gemm_set_stream(int on, long long min_bytes, int fold = -1);
 // (mt, ntw, steps, splitk) pins that config for every eligible call (A/B probes)
 int dnn_gemm_set_oneshot(int on, int mt, int ntw, int steps, int splitk);
 int dnn_gemm_set_oneshot_lds_floor(int bytes);
-int dnn_gemm_set_oneshot_probe(void* rec);  // race probe records (nullptr = off)
+// race probe (gemm_oneshot.h probe bits; abl 0 = off): records per workgroup in rec
+int dnn_gemm_set_oneshot_probe(void* rec, int abl);
 int dnn_gemm_oneshot_sweep(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
                            int K, int mt, int ntw, int steps, int splitk, int w8, void* ws, long long ws_bytes,
                            hipStream_t st);
@@ -57,6 +58,7 @@ int dnn_gemm_head(const void* A, int lda, const void* Wsh, const float* sw, cons
 // hist (optional, with pos_inc): hist[row * hist_ld + pos_inc[row]] = id before the advance (token history)
 int dnn_argmax_final(const void* part, int S, int M, int* out, int* out2, int* pos_inc, hipStream_t st,
                      int* hist = nullptr, int hist_ld = 0);
+// prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
 int dnn_gemm_set_split_tail(int on);
 // MX-scaled W8A8 prefill (e8m0 per (row, 128 columns), common.h mx_index)
 int dnn_quant_fp8_mx(const void* x, int ldx, void* q, int ldq, void* sx, int M, int K, int kpad, hipStream_t st);
@@ -71,10 +73,11 @@ int dnn_gemm_fp8_qkv_scatter_mx(const void* A8, const void* sx, const void* W8, 
 // producer-side row statistics for the next decode GEMM call of this thread (gemm_skinny.hip)
 int dnn_gemm_rowstats(void* out, int out_ld, const void* in, int in_ld);
 int dnn_gemm_rowstats_written();
+// decode GEMM epilogue operands with the first loads (1, default) / after (0)
 int dnn_gemm_set_epi_prefetch(int on);
+// probe: one-shot launch with parts removed
 int dnn_gemm_oneshot_ablate(const void* A, int lda, const void* Wsh, const float* sw, void* C, int ldc, int M, int N,
-                            int K, int cfg, int abl, hipStream_t st);  // probe: one-shot launch with parts removed  // decode GEMM epilogue operands with the first loads (1, default) / after (0)
-// prefill: 256^2 + 256x128 tail split (gemm_bf16.hip launch_gemm)
+                            int K, int cfg, int abl, hipStream_t st);
 int dnn_silu_mul_packed(const void* gu, int ld_in, void* out, int ld_out, int M, int F, hipStream_t st);
 int dnn_cifar_stage0_v4(const float* x, void* out, const void* w1p, const float* b1, const void* w2p, const float* b2,
                         int B, int grid, hipStream_t st);

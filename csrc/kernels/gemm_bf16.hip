@@ -206,6 +206,30 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, int l
   }
 }
 
+// Epilogue operands of a 256^2 tile by LDS-DMA, into EPI_LDS bytes past the
+// operand buffers, issued before the first staging DMA (so the prologue's
+// counted wait retires them and no register carries them through the main
+// loop): wave 0 the bias of the tile's 256 columns, wave 1 the per-column
+// scale (fp8 channel scales / folded-norm column sums), waves 2-3 the row
+// statistics (float2) of its 256 rows, wave 4 the per-row fp8 activation
+// scales.  After the main loop every output group then reads them from LDS:
+// loaded there per group they cost one dependent memory round trip each (16
+// per tile), a load under a branch being waited for at the merge.  Addresses
+// past the matrix clamp to its last 16 B (host/kernel: N % 4 == 0, M even,
+// 16-B aligned vectors; those columns / rows are never stored).
+constexpr int EPI_LDS = 5 * 1024;
+constexpr int EPI_B = 0, EPI_C = 1024, EPI_RS = 2048, EPI_SA = 4096;  // byte offsets
+
+__device__ __forceinline__ void epi_operands_dma(const float* bias, const float* col, const float2* rowstat,
+                                                 const float* sa, int n0, int N, int m0, int M, char* dst, int wave,
+                                                 int lane) {
+  if (wave == 0 && bias != nullptr) glds16(bias + min(n0 + 4 * lane, N - 4), dst + EPI_B);
+  if (wave == 1 && col != nullptr) glds16(col + min(n0 + 4 * lane, N - 4), dst + EPI_C);
+  if ((wave == 2 || wave == 3) && rowstat != nullptr)
+    glds16(rowstat + min(m0 + (wave - 2) * 128 + 2 * lane, M - 2), dst + EPI_RS + (wave - 2) * 1024);
+  if (wave == 4 && sa != nullptr) glds16(sa + min(m0 + 4 * lane, M - 4), dst + EPI_SA);
+}
+
 __device__ __forceinline__ void bg_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -303,7 +327,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     int res_pre, const float2* __restrict__ rowstat, const float* __restrict__ colsum, QkvScatter scat = {}) {
   static_assert(NQ == 1 || NQ == 2, "256x256 or 256x128 tiles");
   constexpr int TN = 128 * NQ;
-  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF + EPI_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + TN - 1) / TN, ntm = (M + BG_M - 1) / BG_M;
   int tm, tn;
@@ -311,6 +335,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / BG_K;
+  // epilogue operands in LDS (epi_operands_dma); uniform.  SCATTER: the bias
+  // is indexed by the global column (the tail launch's c_off).
+  char* epi = smem + 8 * BG_HALF;
+  const int boff = SCATTER ? scat.c_off : 0;
+  const bool epv = (N & 3) == 0 && (M & 1) == 0 && M >= 2 && N >= 4 &&
+                   ((reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(colsum) |
+                     reinterpret_cast<uintptr_t>(rowstat)) & 15) == 0;
+  if (epv)
+    epi_operands_dma(bias != nullptr ? bias + boff : nullptr, colsum, rowstat, nullptr, n0, N, m0, M, epi, wave, lane);
 
   f32x4 acc[2][NQ][4][2];
 #pragma unroll
@@ -427,13 +460,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
   //   n = n0 + nq*128 + wc*32 + j*16 + (lane>>4)*4.
   if (rowstat != nullptr) {  // folded pre-norm (prefill QKV / up projections)
-    // 8 row statistics and 4 column-sum vectors per lane, loaded once
+    // 8 row statistics and 4 column-sum vectors per lane (from the LDS copy)
     float2 rs[2][4];
     f32x4 cs[NQ][2];
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rs[mq][i] = rowstat[min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1)];
+      for (int i = 0; i < 4; ++i) {
+        const int rl = mq * 128 + arow + i * 16 + (lane & 15);
+        rs[mq][i] = epv ? reinterpret_cast<const float2*>(epi + EPI_RS)[rl] : rowstat[min(m0 + rl, M - 1)];
+      }
 #pragma unroll
     for (int nq = 0; nq < NQ; ++nq)
 #pragma unroll
@@ -441,7 +477,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
         const int n = n0 + nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4;
         cs[nq][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (colsum != nullptr) {
-          if (n + 3 < N) {
+          if (epv) {
+            cs[nq][j] = *reinterpret_cast<const f32x4*>(epi + EPI_C + 4 * (n - n0));
+          } else if (n + 3 < N) {
             cs[nq][j] = *reinterpret_cast<const f32x4*>(colsum + n);
           } else {
 #pragma unroll
@@ -459,6 +497,21 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
           for (int j = 0; j < 2; ++j)
             acc[mq][nq][i][j] = acc[mq][nq][i][j] * rs[mq][i].x + rs[mq][i].y * cs[nq][j];
   }
+  // the bias from the LDS copy, added here: the output calls get none to load
+  const bool badd = epv && bias != nullptr && ACT != ACT_SILU_MUL;  // uniform
+  if (badd) {
+#pragma unroll
+    for (int nq = 0; nq < NQ; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(epi + EPI_B + 4 * (nq * 128 + wc * 32 + j * 16 + (lane >> 4) * 4));
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[mq][nq][i][j] += b4;
+      }
+  }
+  const float* bias_e = badd ? nullptr : bias;
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
   // Residual epilogue: every residual load of the tile (32 x 8 B per lane, into
@@ -483,7 +536,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], m0 + mq * 128 + arow + i * 16 + (lane & 15),
-                                   n0 + nq * 128 + wc * 32, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, lane,
+                                   n0 + nq * 128 + wc * 32, M, reinterpret_cast<bf16_t*>(Cv), ldc, bias_e, R, ldr, lane,
                                    rr[mq][nq][i][0], rr[mq][nq][i][1]);
     return;
   }
@@ -502,15 +555,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
           // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
           // residual, N % 32 == 0, hd % 8 == 0 -> a 32-column pair is whole or
           // past N, wave-uniformly)
-          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias, lane, scat);
+          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias_e, lane, scat);
         } else if (!OUT_F32 && pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
-                             bias, R, ldr, lane);
+                             bias_e, R, ldr, lane);
         } else {
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            epi_t4<ACT, OUT_F32>(acc[mq][nq][i][j], m, nb + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias, R, ldr,
-                                 vec);
+            epi_t4<ACT, OUT_F32>(acc[mq][nq][i][j], m, nb + j * 16 + (lane >> 4) * 4, M, N, Cv, ldc, bias_e, R,
+                                 ldr, vec);
         }
       }
 }
@@ -592,7 +645,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   static_assert(!MXA || NQ == 2, "MX activations: 256^2 tiles");
   static_assert(!QOUT || (MXA && ACT == ACT_GELU && !SCATTER), "quantised output: the MX c_fc");
   constexpr int TN = 128 * NQ;  // NQ = 1: the 256x128 variant (tail-split launches), as the bf16 kernel's
-  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * BG_HALF + EPI_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + TN - 1) / TN, ntm = (M + BG_M - 1) / BG_M;
   int tm, tn;
@@ -600,6 +653,16 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = Kb / 128;
+  // epilogue operands in LDS (epi_operands_dma): channel scales, bias (SCATTER:
+  // by the global column), per-row activation scales (not MXA); uniform
+  char* epi = smem + 8 * BG_HALF;
+  const int boff = SCATTER ? scat.c_off : 0;
+  const bool epv = (N & 3) == 0 && (MXA || (M & 3) == 0) && M >= 4 && N >= 4 &&
+                   ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(bias) |
+                     reinterpret_cast<uintptr_t>(sa)) & 15) == 0;
+  if (epv)
+    epi_operands_dma(bias != nullptr ? bias + boff : nullptr, sw, nullptr, MXA ? nullptr : sa, n0, N, m0, M, epi,
+                     wave, lane);
   // byte-identical staging: view the e4m3 rows as bf16 rows of half the length
   const bf16_t* A = reinterpret_cast<const bf16_t*>(A8);
   const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
@@ -742,7 +805,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
             // 16-B channel-scale / bias loads (per-element ones were 8 scalar
             // loads per quad)
             f32x4 cs, bs = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (n + 3 < N) {
+            if (epv) {  // the LDS copy (columns past N are zeroed below)
+              cs = *reinterpret_cast<const f32x4*>(epi + EPI_C + 4 * (n - n0));
+              if (bias != nullptr) bs = *reinterpret_cast<const f32x4*>(epi + EPI_B + 4 * (n - n0));
+            } else if (n + 3 < N) {
               cs = *reinterpret_cast<const f32x4*>(sw + n);
               if (bias != nullptr) bs = *reinterpret_cast<const f32x4*>(bias + n);
             } else {
@@ -795,6 +861,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
         }
     return;
   }
+  const bool badd = epv && bias != nullptr && ACT != ACT_SILU_MUL;  // uniform: bias added from the LDS copy
+  const float* bias_e = badd ? nullptr : bias;
   const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
   // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
@@ -818,33 +886,38 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + mq * 128 + arow + i * 16 + (lane & 15);
         const int nb = n0 + nq * 128 + wc * 32;
-        const float rs = MXA ? 1.f : (m < M ? sa[m] : 0.f);  // MXA: the activation scales are in acc
+        // MXA: the activation scales are in acc
+        const float rs = MXA ? 1.f
+                             : (epv ? reinterpret_cast<const float*>(epi + EPI_SA)[m - m0] : (m < M ? sa[m] : 0.f));
         f32x4 v[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int n = nb + j * 16 + (lane >> 4) * 4;
           f32x4 cs;
-          if (n + 3 < N) {
+          if (epv) {
+            cs = *reinterpret_cast<const f32x4*>(epi + EPI_C + 4 * (n - n0));
+          } else if (n + 3 < N) {
             cs = *reinterpret_cast<const f32x4*>(sw + n);
           } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) cs[r] = n + r < N ? sw[n + r] : 0.f;
           }
           v[j] = acc[mq][nq][i][j] * (cs * rs);
+          if (badd) v[j] += *reinterpret_cast<const f32x4*>(epi + EPI_B + 4 * (n - n0));
         }
         if (SCATTER) {
-          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias, lane, scat);
+          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias_e, lane, scat);
         } else if (ACT == ACT_SILU_MUL) {
           epi_silu_pair<false>(v[0], v[1], m, nb / 2, M, N / 2, C, ldc, vec, lane);
         } else if (rpre) {
-          epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane, rr[mq][nq][i][0],
+          epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane, rr[mq][nq][i][0],
                                    rr[mq][nq][i][1]);
         } else if (pair && nb + 31 < N) {
-          epi_pair_bf16<ACT>(v[0], v[1], m, nb, M, C, ldc, bias, R, ldr, lane);
+          epi_pair_bf16<ACT>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane);
         } else {
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            epi_t4<ACT, false>(v[j], m, nb + j * 16 + (lane >> 4) * 4, M, N, C, ldc, bias, R, ldr, vec);
+            epi_t4<ACT, false>(v[j], m, nb + j * 16 + (lane >> 4) * 4, M, N, C, ldc, bias_e, R, ldr, vec);
         }
       }
 }

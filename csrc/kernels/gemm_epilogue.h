@@ -135,6 +135,7 @@ __device__ __forceinline__ void epi_t4_pre(f32x4 v, int m, int n, void* __restri
 // to rs[m * ld + n0 / 16] from lane group 0.  Every lane must call it.
 __device__ __forceinline__ void epi_rowstat16(const f32x4& x, int m, int n0, int M, int N, float2* __restrict__ rs,
                                               int ld, int lane) {
+  if (n0 >= N) return;  // a surplus tile past the row (uniform: n0 is the tile's): no partial, no write
   const int nt = min(16, N - n0);  // >= 1: the tile starts inside the row
   const int nv = min(4, max(0, N - n0 - 4 * (lane >> 4)));
   float s = 0.f;

@@ -77,16 +77,47 @@ constexpr int os_lds_bytes() {
 // (row-statistics partials, epilogue operands) are still retired by counted
 // waits: plain loads complete in order among themselves.
 // tests/test_isa_lds_dma_order.py checks the sequence in the product ISA.
-constexpr int OS_PROBE_WORDS = 1024;  // ABL 256 record per workgroup (int32 words)
+constexpr int OS_PROBE_WORDS = 1024;  // race-probe record per workgroup (int32 words)
 
-__device__ __forceinline__ char* os_probe_lds() {
-  extern __shared__ __attribute__((aligned(1024))) char os_lds[];
-  return os_lds;
+__device__ __forceinline__ uint32_t os_hash16(const bf16x8& v) {  // race probe: a 16-B read's fingerprint
+  uint32_t w[4];
+  __builtin_memcpy(w, &v, 16);
+  return (w[0] * 0x9E3779B1u) ^ (w[1] * 0x85EBCA77u) ^ (w[2] * 0xC2B2AE3Du) ^ (w[3] * 0x27D4EB2Fu) ^ 0x5bd1e995u;
 }
 
 __device__ __forceinline__ void os_image_sync() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  // one barrier more before the first read (see "Retiring the image"): with a
+  // second workgroup on the CU, a ds_read right after the wait + ONE barrier
+  // saw pre-DMA bytes in ~2 % of calls
+  __builtin_amdgcn_s_barrier();
+}
+// the round-4/5 sequence: the wait and one barrier (race probe ABL 16384 only)
+__device__ __forceinline__ void os_image_sync_1() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+// race-probe variants of the image sync, each with ONE barrier (ABL 2048 / 4096 /
+// 8192 / 16384): composable_kernel's separate vmcnt(0) then lgkmcnt(0); vmcnt(0)
+// alone (ck_tile); the merged wait plus a short s_sleep (a pure delay); the
+// round-4/5 merged wait (profiles/r6_oneshot_race_root_cause.jsonl)
+template <int ABL>
+__device__ __forceinline__ void os_image_sync_v() {
+  if constexpr ((ABL & 2048) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr ((ABL & 4096) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr ((ABL & 8192) != 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_sleep 1" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr ((ABL & 16384) != 0) {
+    os_image_sync_1();
+  } else {
+    os_image_sync();
+  }
 }
 
 template <int MT, int NTW, bool W8, int NORM, int ACT, bool SPLIT, int STEPS, int ABL = 0>
@@ -103,18 +134,15 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
                                                               int rs_ld_in = 0, int epi_pre = 1) {
   if constexpr ((ABL & 32) != 0) return;
   using Cfg = StrCfg<W8>;
-  // ABL 256 (race probe only, bench/probes/oneshot_race_probe.py): ``slab`` is
-  // a per-workgroup int32 record (OS_PROBE_WORDS), ``rs_ld_in`` the launch's
-  // dynamic LDS bytes; the LDS past the kernel's own os_lds_bytes is filled
-  // with a canary and checked at exit, and the row statistics are taken a
-  // second time from the image after the MFMAs (early vs late).
-  [[maybe_unused]] uint64_t prb_t0 = 0;
-  if constexpr ((ABL & 256) != 0) {
-    prb_t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t* w32 = reinterpret_cast<uint32_t*>(os_probe_lds());
-    for (int i = os_lds_bytes<MT, STEPS>() / 4 + (int)threadIdx.x; i < rs_ld_in / 4; i += 256) w32[i] = 0xA5A5A5A5u ^ i;
-    __syncthreads();
-  }
+  // Race-probe bits (bench/probes/oneshot_race_probe.py; never in a product
+  // launch).  ``slab`` is then a per-workgroup int32 record (OS_PROBE_WORDS):
+  //   256  detector: every 16-B image read of the row-statistics pass is
+  //        hashed and read again after the MFMAs; lane l's record word is the
+  //        mask of its (chunk, row tile) reads whose bytes changed in between;
+  //   512  one workgroup barrier at entry (and nothing else);
+  //   1024 the image sync twice before the statistics pass.
+  static_assert((ABL & 256) == 0 || (!W8 && STEPS == 1 && !SPLIT), "race detector: bf16 one-step images only");
+  if constexpr ((ABL & 512) != 0) __syncthreads();
   constexpr int ACH = Cfg::ACH, CS = Cfg::CS, AU = Cfg::AU;
   constexpr int MP = MT * 16;
   constexpr int BN = 16 * NTW;
@@ -186,6 +214,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     }
   }
   float shift[MT], s1s[MT], s2s[MT];
+  [[maybe_unused]] uint32_t prb_h[CPW][MT];  // ABL 256: hashes of the statistics pass's image reads
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     shift[t] = 0.f;
@@ -258,7 +287,8 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     if constexpr ((ABL & 128) != 0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEPS * NTW * CS) : "memory");  // racy (probe only)
     else
-      os_image_sync();  // the image (see "Retiring the image")
+      os_image_sync_v<ABL>();  // the image (see "Retiring the image")
+    if constexpr ((ABL & 1024) != 0) os_image_sync();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -272,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
             const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
             const bf16x8 a8 =
                 *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
+            if constexpr ((ABL & 256) != 0) prb_h[c][t] = os_hash16(a8);
             str_stats<NORM>(a8, shift[t], s1s[t], s2s[t]);
           }
       }
@@ -292,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
   } else if constexpr ((ABL & 128) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    os_image_sync();  // again after a statistics pass: the weights land here, the barrier is cheap
+    os_image_sync_v<ABL>();  // again after a statistics pass: the weights land here, the barrier is cheap
   }
   __builtin_amdgcn_sched_barrier(0);
 
@@ -344,51 +375,25 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     }
   }
 
-  // ABL 256: the same statistics again from the image, after the MFMAs
-  [[maybe_unused]] float prb_l1[MT], prb_l2[MT];
+  // ABL 256: the statistics pass's reads again, after the MFMAs
   if constexpr ((ABL & 256) != 0 && NORM != 0) {
-#pragma unroll
-    for (int t = 0; t < MT; ++t) prb_l1[t] = prb_l2[t] = 0.f;
+    uint32_t mask = 0;
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
       const int s = c / CS, cc = c % CS;
-      if (c < nvalid) {
+      if (c < nvalid && !rsi) {
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-          for (int h = 0; h < AU; ++h) {
-            const int row = 16 * t + fr;
-            const int slot = (cc * ACH + fg * (ACH / 4) + 16 * h) >> 4;
-            const bf16x8 a8 =
-                *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
-            str_stats<NORM>(a8, shift[t], prb_l1[t], prb_l2[t]);
-          }
+        for (int t = 0; t < MT; ++t) {
+          const int row = 16 * t + fr;
+          const int slot = (cc * ACH + fg * (ACH / 4)) >> 4;
+          const bf16x8 a8 =
+              *reinterpret_cast<const bf16x8*>(img + s * MP * OS_SB + row * OS_SB + ((slot ^ (row & 15)) << 4));
+          if (os_hash16(a8) != prb_h[c][t]) mask |= 1u << (c * MT + t);
+        }
       }
     }
     int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;
-    bool bad = false;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      bad |= prb_l1[t] != s1s[t] || prb_l2[t] != s2s[t];
-      float e1 = s1s[t], e2 = s2s[t], l1 = prb_l1[t], l2 = prb_l2[t];
-      e1 += __shfl_xor(e1, 16, 64);
-      e1 += __shfl_xor(e1, 32, 64);
-      e2 += __shfl_xor(e2, 16, 64);
-      e2 += __shfl_xor(e2, 32, 64);
-      l1 += __shfl_xor(l1, 16, 64);
-      l1 += __shfl_xor(l1, 32, 64);
-      l2 += __shfl_xor(l2, 16, 64);
-      l2 += __shfl_xor(l2, 32, 64);
-      if (lane < 16 && t < 2) {
-        float* f = reinterpret_cast<float*>(rec) + 16 + ((wave * 2 + t) * 16 + lane) * 4;
-        f[0] = e1;
-        f[1] = e2;
-        f[2] = l1;
-        f[3] = l2;
-      }
-    }
-    const int nbad = __builtin_popcountll(__ballot(bad));
-    if (lane == 0) rec[10 + wave] = nbad;
+    rec[16 + wave * 64 + lane] = (int)mask;
   }
 
   // ---- row statistics of this wave's K range: the 4 lane groups hold disjoint k
@@ -506,22 +511,10 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
     }
   }
   if constexpr ((ABL & 256) != 0) {
-    __syncthreads();
-    int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;
-    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(os_lds);
-    int nbad = 0;
-    for (int i = os_lds_bytes<MT, STEPS>() / 4 + tid; i < rs_ld_in / 4; i += 256) nbad += w32[i] != (0xA5A5A5A5u ^ i);
-    nbad = (int)wave_sum((float)nbad);
-    if (lane == 0) rec[6 + wave] = nbad;
     if (tid == 0) {
-      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;
       rec[0] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID: wave/simd/cu/sh/se ids
       rec[1] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-      rec[2] = (int)(uint32_t)prb_t0;
-      rec[3] = (int)(uint32_t)(prb_t0 >> 32);
-      rec[4] = (int)(uint32_t)t1;
-      rec[5] = (int)(uint32_t)(t1 >> 32);
-      rec[14] = rs_ld_in;
       rec[15] = (int)blockIdx.x;
     }
   }

@@ -340,6 +340,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
     }
     const int m = t * 16 + (lane & 15);
     const float rs = (FP8 && m < M) ? sa[m] : 1.f;
+    // the prefetched residual rows are tile min(wave, MT - 1)'s: only tile t == wave
+    // uses them (the column operands pre_sw / pre_cs / pre_b fit every tile)
+    const bool pre_t = pre && t == wave;
     if constexpr (W8) {  // per-output-channel weight scale, before the norm terms (colsum is of the dequantised W)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -389,12 +392,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
         }
         epi_silu_t4<OUT_F32>(s[j], m, (n0 + j * 16) / 2, M, N / 2, Cv, ldc, vec, lane);
       }
-    } else if (!OUT_F32 && !FP8 && (pre || rs_out != nullptr)) {  // uniform
+    } else if (!OUT_F32 && !FP8 && (pre_t || rs_out != nullptr)) {  // uniform
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = n0 + j * 16 + (lane >> 4) * 4;
         f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pre && n0 + j * 16 + 15 < N) {  // wave-uniform: the whole 16-column tile
+        if (pre_t && n0 + j * 16 + 15 < N) {  // wave-uniform: the whole 16-column tile
           if (m < M)
             epi_t4_pre<ACT>(s[j], m, n, Cv, ldc, bias != nullptr, pre_b[j % NP], R != nullptr, pre_r[j % NP], &x);
         } else {
@@ -556,8 +559,10 @@ static int g_os_pin[4] = {0, 0, 0, 0};              // mt, ntw, steps, splitk (0
 // ABL 256 variant of the forced LN + GELU shapes (MT 2, STEPS 1, bf16) writes
 // one OS_PROBE_WORDS record per workgroup here
 static int* g_os_probe = nullptr;
-extern "C" int dnn_gemm_set_oneshot_probe(void* rec) {
+static int g_os_probe_abl = 0;  // 256 detector, 512 entry barrier, 1024 double image sync (gemm_oneshot.h)
+extern "C" int dnn_gemm_set_oneshot_probe(void* rec, int abl) {
   g_os_probe = static_cast<int*>(rec);
+  g_os_probe_abl = abl;
   return 0;
 }
 
@@ -651,12 +656,18 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
     float2* rso = ACT != ACT_SILU_MUL ? g_rs_cur.out : nullptr;
     const float2* rsi = (NORM != 0 && (kelems + 15) / 16 <= OS_RS_SPT * (256 / MP)) ? g_rs_cur.in : nullptr;
     if constexpr (ABL == 0 && MT == 2 && STEPS == 1 && !W8 && NORM == 2 && ACT == ACT_GELU && NTW <= 2) {
-      if (g_os_probe != nullptr && rsi == nullptr) {
-        hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, 256>), grid, block, smem, st,
-                           (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M,
-                           N, nch, cps, colsum, eps, kelems, (float*)g_os_probe, ntiles, mgroups, nullptr, 0, nullptr,
-                           (int)smem, g_epi_pre);
-        return (int)hipGetLastError();
+      if (g_os_probe_abl != 0 && rsi == nullptr) {
+#define OSP(B)                                                                                                    \
+  if (g_os_probe_abl == B) {                                                                                      \
+    hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, B>), grid, block, smem, st,      \
+                       (const uint8_t*)A, lda_b, (const uint8_t*)Wsh, sw, C, ldc, bias, (const bf16_t*)R, ldr, M, N, \
+                       nch, cps, colsum, eps, kelems, (float*)g_os_probe, ntiles, mgroups, nullptr, 0, nullptr, 0,   \
+                       g_epi_pre);                                                                                \
+    return (int)hipGetLastError();                                                                                \
+  }
+        OSP(256) OSP(1024) OSP(2048) OSP(4096) OSP(8192) OSP(16384)
+#undef OSP
+        return -2;
       }
     }
     hipLaunchKernelGGL((gemm_oneshot_kernel<MT, NTW, W8, NORM, ACT, false, STEPS, ABL>), grid, block, smem, st,

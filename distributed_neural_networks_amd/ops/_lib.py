@@ -41,8 +41,23 @@ def verify_stamp(path: str) -> dict:
     return stamp
 
 
+def _load_override(path: str):
+    """``DNN_HIP_LIB=/path/_dnn_hip*.so``: load that build instead of the
+    in-tree one (A/B of two builds in one session, bench/probes/lib_ab.py;
+    no stamp check: the file is named explicitly)."""
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("distributed_neural_networks_amd._dnn_hip", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["distributed_neural_networks_amd._dnn_hip"] = mod
+    return mod
+
+
 def lib():
     global _lib
+    if _lib is None and os.environ.get("DNN_HIP_LIB"):
+        _lib = _load_override(os.environ["DNN_HIP_LIB"])
     if _lib is None:
         try:
             mod = importlib.import_module("distributed_neural_networks_amd._dnn_hip")

@@ -162,3 +162,24 @@ def test_rccl_device_mapping_validated(tmp_path):
     pinned = [dict(two[0], device=1), dict(two[1], device=1)]
     with pytest.raises(ConfigError, match="both map to GPU 1"):
         rccl_device_index(load_node(cfg(pinned), "a"), 8)
+
+
+def test_fp8_prefill_default_is_mx_e4m3(tmp_path):
+    """ADVICE r5: the fp8 prefill default is the one-byte MX path ("e4m3");
+    its end-to-end error budget against the unquantised model is pinned on
+    the GPU by tests/test_transformer_gpu.py::test_fp8_fidelity_vs_unquantised
+    (prefill logits < 0.13 rel, greedy agreement >= 0.6 on GPT-2 XL blocks)
+    and reported by the bench line's gpt2xl_fp8_vs_unquantised_fp32 key."""
+    import json as _json
+    c = {"nodes": [{"id": "node1", "address": "127.0.0.1:50051", "part_index": 0}],
+         "model_weights": "synthetic:0", "num_parts": 1, "model": "gpt2-tiny", "dtype": "fp8"}
+    p = tmp_path / "c.json"
+    p.write_text(_json.dumps(c))
+    ctx = load_node(str(p), "node1")
+    assert ctx.pipeline.fp8_prefill == "e4m3"
+    c["fp8_prefill"] = "split"
+    p.write_text(_json.dumps(c))
+    assert load_node(str(p), "node1").pipeline.fp8_prefill == "split"
+    import inspect
+    import tests.test_transformer_gpu as tg  # noqa: F401 — the GPU pin exists
+    assert "fp8-e4m3" in inspect.getsource(tg.test_fp8_fidelity_vs_unquantised)

@@ -30,7 +30,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 # <MT, NTW, W8, NORM, ACT, SPLIT, STEPS>: gemm_skinny.hip os_plan (planned
 # shapes and the forced "every eligible shape" mode the GPU tests use)
-RACY = [(2, 1, "false", 2, "ACT_GELU", "false", 1, 128), (1, 2, "true", 0, "ACT_NONE", "false", 2, 128)]
+RACY = [(2, 1, "false", 2, "ACT_GELU", "false", 1, 128), (1, 2, "true", 0, "ACT_NONE", "false", 2, 128),
+        (2, 1, "false", 2, "ACT_GELU", "false", 1, 16384)]
 CONFIGS = [
     (2, 2, "false", 2, "ACT_NONE", "false", 1),   # GPT-2 c_attn (folded LN)
     (2, 2, "false", 2, "ACT_GELU", "false", 1),   # GPT-2 c_fc (folded LN + GELU)
@@ -101,7 +102,7 @@ def _kernels(text, kernel="gemm_oneshot_kernel", raw=False):
 
 def _product(ks):
     """Drop the probe instantiations (ABL != 0: a ninth template argument)."""
-    return {n: q for n, q in ks.items() if not re.search(r"ELi(128)EE", n)}
+    return {n: q for n, q in ks.items() if not re.search(r"ELi(128|16384)EE", n)}
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
@@ -117,7 +118,7 @@ def test_oneshot_image_dma_issued_first():
         assert not between, f"{name}: loads interleaved with the image DMA: {between[:4]}"
 
 
-def _unretired_reads(lines):
+def _unretired_reads(lines, barriers: int = 1):
     """LDS reads that some path reaches after an LDS-DMA without vmcnt(0) and
     then s_barrier in between: a forward may-analysis over the kernel's
     basic blocks (labels, s_branch / s_cbranch_*, s_endpgm)."""
@@ -148,8 +149,13 @@ def _unretired_reads(lines):
             succ.append(([tgt] if tgt is not None else []) + (nxt if m.group(1) else []))
         else:
             succ.append(nxt)
-    # state: 0 clear, 1 DMA waited for (vmcnt(0)) but no barrier yet, 2 DMA
-    # pending; a block's entry state is the worst over its predecessors
+    # state: 0 clear, 1 DMA waited for (vmcnt(0)) but fewer than ``barriers``
+    # barriers since, 2 DMA pending; a block's entry state is the worst over
+    # its predecessors (``barriers`` = 2 for the one-shot image: one barrier
+    # more than the wait + barrier, gemm_oneshot.h "Retiring the image")
+    # encoded state: 0 clear, 2 + barriers pending, or 1 .. barriers (barriers still needed
+    # after the wait); a higher value is worse
+    top = barriers + 1
     entry = [0] * len(blocks)
     bad, work = set(), list(range(len(blocks)))
     while work:
@@ -157,11 +163,11 @@ def _unretired_reads(lines):
         st = entry[i]
         for j, t in enumerate(blocks[i]):
             if "global_load_lds" in t or (t.startswith("buffer_load") and " lds" in t):
-                st = 2
+                st = top
             elif t.startswith("s_waitcnt") and re.search(r"vmcnt\(0\)", t):
-                st = min(st, 1)
-            elif t.startswith("s_barrier") and st == 1:
-                st = 0
+                st = min(st, barriers)
+            elif t.startswith("s_barrier") and 0 < st < top:
+                st -= 1
             elif t.startswith("ds_read") and st:
                 bad.add((i, j, t))
         for k in succ[i]:
@@ -179,10 +185,15 @@ def test_lds_dma_images_retired_before_reads():
         assert len(ks) == n, (kernel, sorted(ks))
         for name, seq in ks.items():
             assert any("global_load_lds" in t for t in seq), name
-            bad = _unretired_reads(seq)
+            # the one-shot image: the wait and TWO barriers before the first read
+            bad = _unretired_reads(seq, 2 if kernel == "gemm_oneshot_kernel" else 1)
             assert not bad, f"{name}: {len(bad)} LDS reads before the image DMA is retired: {bad[:3]}"
-    # the racy counted-wait variants must be flagged (the check sees the bug)
+    # the racy variants must be flagged (the check sees the bug): the counted
+    # wait (ABL 128) at any barrier count, the round-4/5 wait + one barrier
+    # (ABL 16384) at two
     racy = {n: q for n, q in _kernels(text, raw=True).items() if n not in _product({n: q})}
     assert len(racy) == len(RACY), sorted(racy)
     for name, seq in racy.items():
-        assert _unretired_reads(seq), f"{name}: counted-wait variant not flagged"
+        assert _unretired_reads(seq, 2), f"{name}: racy variant not flagged"
+        if "ELi128EE" in name:
+            assert _unretired_reads(seq, 1), f"{name}: counted-wait variant not flagged"

@@ -337,3 +337,52 @@ def test_epilogue_prefetch_bit_identical(path, N, K, w8, epi):
     step = torch.maximum(torch.maximum(a.abs(), b.abs()), torch.full_like(b, 2.0 ** -126)) * 2.0 ** -7
     assert bool(((a - b).abs() <= step).all()), "on vs off: " + where(a, b)
     assert (a != b).float().mean().item() < 1e-3
+
+
+@pytest.mark.parametrize("N,floor_kb", [(3072, 0), (2304, 0), (3072, 72)])
+def test_oneshot_coresident_race_screen(N, floor_kb):
+    """VERDICT r5 item 2 regression: the forced one-shot LN + GELU grid with
+    TWO workgroups per CU (LDS floor 0, or a 72 KB floor: padded but still two
+    per CU), every call after a poisoning call on other activations, bit-
+    identical to the settled reference in all 1500 calls.  Before the fix (the
+    wait + one barrier before the image's first read) this configuration
+    differed in ~2 % of calls (few-ulp row statistics, rows 16-31 of an
+    m-group); the same screen of that sequence (probe bit 16384) runs
+    alongside as the positive control and its count is printed: with two
+    workgroups per CU it is expected to be non-zero
+    (profiles/r6_oneshot_race_root_cause.md)."""
+    from distributed_neural_networks_amd.ops._lib import lib
+    from distributed_neural_networks_amd.ops.gemm import (attach_shuffled, decode_workspace, fold_norm, linear_norm,
+                                                          set_oneshot_gemm)
+    dev = torch.device("cuda", 0)
+    M, K = 64, 768
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    x = (torch.randn(M, K, device=dev, generator=g) * 2 + 0.5).bfloat16()
+    w = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    x2 = (torch.randn(M, K, device=dev, generator=g) * 3 - 1.0).bfloat16()
+    ws = decode_workspace(dev)
+    f = fold_norm(w, torch.rand(K, device=dev, generator=g) + 0.5, torch.randn(K, device=dev, generator=g) * 0.1,
+                  bias, False, 1e-5, dev, False)
+    attach_shuffled(f)
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    counts = {}
+    try:
+        set_oneshot_gemm(2, 2, 1, 1, 1)  # forced 2/1/1: N / 16 x 2 workgroups (> 256 CUs)
+        lib().gemm_set_oneshot_lds_floor(floor_kb * 1024)
+        for arm, abl in (("product", 0), ("control", 16384)):
+            assert lib().gemm_set_oneshot_probe(0, abl) == 0
+            linear_norm(x, f, act="gelu", ws=ws, out=out)
+            ref = linear_norm(x, f, act="gelu", ws=ws, out=out).clone()
+            bad = 0
+            for _ in range(1500):
+                linear_norm(x2, f, act="gelu", ws=ws, out=out)
+                o = linear_norm(x, f, act="gelu", ws=ws, out=out)
+                bad += int(not torch.equal(o, ref))
+            counts[arm] = bad
+    finally:
+        lib().gemm_set_oneshot_probe(0, 0)
+        lib().gemm_set_oneshot_lds_floor(82 * 1024)
+        set_oneshot_gemm(1)
+    print(f"N={N} floor={floor_kb} KB: mismatched calls of 1500: {counts}")
+    assert counts["product"] == 0, counts

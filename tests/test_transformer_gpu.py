@@ -1325,6 +1325,46 @@ def test_fp8_split_activation_planes(M, K):
     assert e2 < 4e-3 and e2 < e1 / 4
 
 
+@pytest.mark.parametrize("N", [400, 1040, 272])
+@pytest.mark.parametrize("w8", [False, True])
+def test_rowstats_partial_width(N, w8):
+    """widths that are not a multiple of the kernels' column tiles
+    (16 NT / 16 NTW): a surplus tile past the row must write no partial (it
+    used to write NaN into the next row's partial 0).  Every partial of the
+    row's ceil(N/16) tiles matches torch; a guard row past M stays untouched."""
+    from distributed_neural_networks_amd.ops.fp8 import linear_w8, quantize_weight
+    from distributed_neural_networks_amd.ops.gemm import attach_shuffled, linear, rowstats_buffer, rowstats_written
+    M, K = 64, 768
+    torch.manual_seed(N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    h0 = torch.randn(M, N, device=DEV).bfloat16()
+    W = torch.randn(N, K, device=DEV) / math.sqrt(K)
+    bias = torch.randn(N, device=DEV) * 0.1
+    rs = rowstats_buffer(M + 1, N, DEV)
+    rs[M].fill_(7.0)  # guard row
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    if w8:
+        linear_w8(x, attach_shuffled(quantize_weight(W, DEV)), bias, 0, h0, out, rs_out=rs)
+    else:
+        linear(x, W.bfloat16(), bias, None, h0, out, w_shuf=attach_shuffled(W.bfloat16()), rs_out=rs)
+    if not rowstats_written():
+        pytest.skip("no producer-side statistics kernel for this shape")
+    torch.cuda.synchronize()
+    nt = -(-N // 16)
+    of = torch.nn.functional.pad(out.float(), (0, nt * 16 - N))
+    tiles = of.view(M, nt, 16)
+    cnt = torch.full((nt,), 16.0, device=DEV)
+    cnt[-1] = N - 16 * (nt - 1)
+    mean = tiles.sum(-1) / cnt
+    valid = (torch.arange(nt * 16, device=DEV) < N).view(nt, 16)
+    m2 = (((tiles - mean[..., None]) ** 2) * valid).sum(-1)
+    got = rs[:M].view(M, nt, 2)
+    assert torch.isfinite(got).all()
+    assert torch.allclose(got[..., 0], mean, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(got[..., 1], m2, rtol=1e-3, atol=1e-3)
+    assert bool((rs[M] == 7.0).all()), "a surplus tile wrote past the last row"
+
+
 @pytest.mark.parametrize("M,N,K,N2", [(64, 768, 768, 2304), (64, 768, 3072, 3072), (64, 1600, 1600, 4800),
                                       (64, 1600, 6400, 6400), (48, 768, 768, 2304)])
 @pytest.mark.parametrize("w8", [False, True])

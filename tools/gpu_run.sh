@@ -12,7 +12,8 @@
 #                    (gpt2 | gpt2xl | llama), summarised by tools/rocprof_summary.py
 #   gaps:CFG         the same trace's inter-kernel gaps (tools/rocprof_gaps.py)
 #   pmc:CFG          two rocprofv3 --pmc passes (tools/gpu_pmc.sh), tools/pmc_summary.py
-#   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with ',' for spaces), stdout to gpurun_out/TAG_<name>.jsonl
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with ',' for spaces), stdout to gpurun_out/TAG_<name>_<k>.jsonl
+#                    (k counts the py steps of the call)
 # Every GPU step runs under its own timeout and the script stops at the first
 # failure (no retries).  Outputs: gpurun_out/TAG_*.
 set -o pipefail
@@ -22,6 +23,7 @@ TAG=$1
 shift
 mkdir -p gpurun_out
 O=gpurun_out/$TAG
+pyk=0
 
 cfg_args() {
   case $1 in
@@ -70,7 +72,8 @@ for step in "$@"; do
       script=${spec%%:*}
       args=""
       [ "$spec" != "$script" ] && args=$(echo "${spec#*:}" | tr ',' ' ')
-      name=$(basename $script .py)
+      pyk=$((pyk + 1))
+      name=$(basename $script .py)_$pyk
       timeout -k 10 900 python -u $script $args > ${O}_$name.jsonl 2> ${O}_$name.err \
         || { echo PY_FAILED $script; tail -20 ${O}_$name.err; exit 1; }
       tail -c 1500 ${O}_$name.jsonl ;;
