@@ -111,7 +111,7 @@ def main():
     finally:
         set_oneshot_gemm(1)
         from distributed_neural_networks_amd.ops._lib import lib
-        lib().gemm_set_oneshot_lds_floor(82 * 1024)
+        lib().gemm_set_oneshot_lds_floor(0)  # the library default
 
 
 if __name__ == "__main__":

@@ -4,8 +4,12 @@ csrc/kernels/gemm_oneshot.h "Retiring the image").
 Symptom (profiles/r5_oneshot_race_screen_*.jsonl): in ~2 % of forced
 LN + GELU calls at 2/1/1 (288 or 384 workgroups, two per CU) one workgroup's
 second 16-row tile (rows 16-31 of its m-group) comes out a few bf16 ulp off,
-in one 16-column tile: its row statistics, read from its own LDS-DMA image
-right after the wait + one barrier, saw a few pre-DMA bytes.
+in one 16-column tile.  Cause (found with the 32768 dump, see
+profiles/r6_oneshot_race_root_cause.md): one element of that tile's row
+statistics summed without its shift in lanes 48-63 of one wave -- the SLP
+vectoriser's cross-half packed subtract, not the LDS image; the library builds
+the kernel with -fno-slp-vectorize (ops/build.py).  Run with
+``DNN_HIP_LIB=<an SLP build>`` to see the failure again.
 
 Each experiment compares ``--iters`` calls bit for bit with a settled
 reference of the same launch; every call follows a call on other activations
@@ -13,7 +17,8 @@ reference of the same launch; every call follows a call on other activations
 instrumented or alternative image syncs; profiles/r6_oneshot_race_root_cause.md
 tells the story of the round-6 runs (LDS floors 0 / 72 / 82 KB, an entry
 barrier, a detector, CK's split waits, ck_tile's vmcnt-only wait, a short
-s_sleep, a second barrier).  One JSON line per experiment."""
+s_sleep, a second barrier, register-staged images, the dump, the SLP A/B).
+One JSON line per experiment."""
 import argparse
 import json
 import os
@@ -24,6 +29,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 WORDS = 1024  # OS_PROBE_WORDS
+SAVE_DIR = os.environ.get("RACE_SAVE_DIR", "")
 
 
 def cu_key(rec):
@@ -58,12 +64,14 @@ def experiment(name, N, K, pin, floor, abl, iters, dev):
     lib().gemm_set_oneshot_lds_floor(floor)
     run, x, x2 = setup(N, K, dev)
     det = bool(abl & 256)
-    rec = torch.zeros((4096, WORDS), dtype=torch.int32, device=dev)
+    dump = bool(abl & 32768)
+    rec = torch.zeros((4096, WORDS if not dump else 2 * 64 * 24), dtype=torch.int32, device=dev)
     check(lib().gemm_set_oneshot_probe(rec.data_ptr() if abl else 0, abl))
     try:
         run(x)
         ref = run(x).clone()
         torch.cuda.synchronize()
+        ref_dump = rec.clone() if dump else None
         nwg = int((rec[:, 15] != 0).sum().item()) + 1 if det else None  # blockIdx 0 writes 0
         bad_calls, det_calls, both, worst, fails = 0, 0, 0, 0.0, []
         for i in range(iters):
@@ -88,6 +96,17 @@ def experiment(name, N, K, pin, floor, abl, iters, dev):
                      "max": d.max().item()}
                 if det:
                     f.update(analyse(rec[:nwg].cpu(), pin[1], f["col16_tiles"]))
+                if dump and mism:
+                    f.update(analyse_dump(rec, ref_dump))
+                    if SAVE_DIR:  # the raw records and the activations, for offline forensics
+                        import numpy as np
+                        tag = f"{SAVE_DIR}/{name}_call{i}"
+                        wgs = (rec.view(rec.shape[0], 2, 64, 24)[..., :15] !=
+                               ref_dump.view(rec.shape[0], 2, 64, 24)[..., :15]).flatten(1).any(1).nonzero().flatten()
+                        np.save(tag + "_wgs.npy", wgs.cpu().numpy())
+                        np.save(tag + "_got.npy", rec[wgs].cpu().numpy())
+                        np.save(tag + "_ref.npy", ref_dump[wgs].cpu().numpy())
+                        np.save(f"{SAVE_DIR}/{name}_x.npy", x.float().cpu().numpy())
                 fails.append(f)
         return {"exp": name, "N": N, "K": K, "pin": list(pin), "lds_floor": floor, "abl": abl, "iters": iters,
                 "workgroups": nwg, "mismatched_calls": bad_calls, "max": worst, "detector_calls": det_calls,
@@ -99,6 +118,38 @@ def experiment(name, N, K, pin, floor, abl, iters, dev):
 def check(rc):
     if rc != 0:
         raise RuntimeError(f"probe call failed: {rc}")
+
+
+FIELDS = ["v0", "v1", "v2", "v3", "a_w0", "a_w1", "a_w2", "a_w3", "q_w0", "q_w1", "q_w2", "q_w3", "shift", "mean",
+          "rstd"]
+
+
+def analyse_dump(rec, ref):
+    """Probe bit 32768: which epilogue inputs of which workgroup / lane differ
+    from the reference call's (v = the cross-wave GEMM sum, a_w / q_w = the row
+    statistics partial of wave w, shift, mean, rstd), with the hardware ids of
+    the workgroup and of the wave that wrote the record."""
+    a = rec.view(-1, 2, 64, 24).cpu()
+    b = ref.view(-1, 2, 64, 24).cpu()
+    af, bf = a[..., :15].view(torch.float32), b[..., :15].view(torch.float32)
+    diff = (af != bf)
+    wgs = diff.any(-1).any(-1).any(-1).nonzero().flatten().tolist()
+    out = []
+    for lg in wgs[:3]:
+        for k in range(2):
+            d = diff[lg, k]
+            if not bool(d.any()):
+                continue
+            lanes = d.any(-1).nonzero().flatten().tolist()
+            fields = sorted({FIELDS[i] for i in d.any(0).nonzero().flatten().tolist()})
+            l0 = lanes[0]
+            rel = {FIELDS[i]: (float(af[lg, k, l0, i]), float(bf[lg, k, l0, i])) for i in range(15) if d[l0, i]}
+            hw, xcc = int(a[lg, k, l0, 16]), int(a[lg, k, l0, 17])
+            wv = int(a[lg, k, l0, 18:19].view(torch.float32))
+            out.append({"lg": lg, "slot": k, "q": float(a[lg, k, l0, 15:16].view(torch.float32)), "wave": wv, "lanes": lanes[:16],
+                        "n_lanes": len(lanes), "fields": fields, "first_lane_got_vs_ref": rel,
+                        "cu": [xcc & 0xF, (hw >> 13) & 7, (hw >> 12) & 1, (hw >> 8) & 0xF, (hw >> 4) & 3]})
+    return {"dump_diff_wgs": len(wgs), "dump": out}
 
 
 def analyse(r, ntw, tiles):
@@ -143,25 +194,27 @@ def main():
     from distributed_neural_networks_amd.ops.gemm import set_oneshot_gemm
     KB = 1024
     exps = [
-        # the product kernel (probe bits 0: the wait + TWO barriers before the
-        # first image read) at two workgroups per CU: floors 0 and 72 KB
-        ("p_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 0),
-        ("p_2304_floor0", 2304, 768, (2, 1, 1, 1), 0, 0),
-        ("p_3072_floor72", 3072, 768, (2, 1, 1, 1), 72 * KB, 0),
-        ("p_3072_ntw2_floor0", 3072, 768, (2, 2, 1, 1), 0, 0),
-        # positive control: the round-4/5 sequence (wait + ONE barrier)
+        # the product launch (ABL 0), two WG/CU (floors 0 and 72 KB) and one (82 KB)
+        ("p0_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 0),
+        ("p0_2304_floor0", 2304, 768, (2, 1, 1, 1), 0, 0),
+        ("p0_3072_floor72", 3072, 768, (2, 1, 1, 1), 72 * KB, 0),
+        ("p0_2304_floor82", 2304, 768, (2, 1, 1, 1), 82 * KB, 0),
+        # epilogue-input dump (32768): the forensics of profiles/r6_oneshot_race_root_cause.md
+        ("d32768_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 32768),
+        ("d32768_2304_floor0", 2304, 768, (2, 1, 1, 1), 0, 32768),
+        # image-sync variants: the wait and two barriers (16384), CK's split waits (2048)
         ("c16384_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 16384),
-        ("c16384_3072_floor82", 3072, 768, (2, 1, 1, 1), 82 * KB, 16384),
+        ("c2048_3072_floor0", 3072, 768, (2, 1, 1, 1), 0, 2048),
     ]
     try:
         for name, N, K, pin, floor, abl in exps:
-            if a.exps and name not in a.exps.split(","):
+            if a.exps and name not in a.exps.replace("+", ",").split(","):
                 continue
-            it = a.control_iters if name.startswith("c") else a.iters
+            it = a.control_iters if name.startswith(("c", "d")) else a.iters
             print(json.dumps(experiment(name, N, K, pin, floor, abl, it, dev)), flush=True)
     finally:
         set_oneshot_gemm(1)
-        lib().gemm_set_oneshot_lds_floor(82 * KB)
+        lib().gemm_set_oneshot_lds_floor(0)  # the library default
 
 
 if __name__ == "__main__":

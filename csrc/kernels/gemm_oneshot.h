@@ -67,16 +67,29 @@ constexpr int os_lds_bytes() {
 // not ordered with the plain loads that follow it.  The round-4/5 counted wait
 // stays as the probe bit ABL 128; the sync costs nothing measurable
 // (oneshot_anatomy.py counted_wait arm within +-0.13 us,
-// profiles/r5_oneshot_anatomy_imagesync.jsonl) although the statistics no
-// longer overlap the weight flight nor step 0 step 1's weights.  A race screen
-// (bench/probes/epi_race_screen.py, profiles/r5_oneshot_race_screen_*.jsonl)
-// also found a rare few-ulp error in one workgroup's second 16-row tile of
-// statistics, only where two one-shot workgroups shared a CU; the sync did not
-// change it, the host's LDS floor (one workgroup per CU, gemm_skinny.hip
-// g_os_lds_floor) removed it.  Plain loads issued before the image
-// (row-statistics partials, epilogue operands) are still retired by counted
-// waits: plain loads complete in order among themselves.
+// profiles/r5_oneshot_anatomy_imagesync.jsonl).  Plain loads issued before
+// the image (row-statistics partials, epilogue operands) are retired by
+// counted waits: plain loads complete in order among themselves.
 // tests/test_isa_lds_dma_order.py checks the sequence in the product ISA.
+//
+// The "race" of rounds 5-6 was not in the image.  A rare few-ulp error in one
+// workgroup's second 16-row tile, only with two workgroups on a CU
+// (profiles/r5_oneshot_race_screen_*.jsonl), survived every image-side change
+// (a second barrier, CK / ck_tile wait forms, an s_sleep, register-staged
+// images, LDS floors 0 / 72 KB; profiles/r6_oneshot_race_root_cause.md).  The
+// epilogue-input dump (probe bit 32768) pinned it: in the failing wave exactly
+// ONE element of the t = 1 row statistics was summed as x instead of x - shift,
+// in lanes 48-63 only, for all 16 rows (delta s1 == shift exactly, delta s2 ==
+// 2 x shift - shift^2 for an element of the wave's own range).  Those elements
+// are the low halves of the SLP vectoriser's packed subtracts
+// (v_pk_add_f32 dst, src, shift op_sel:[0,1] neg_lo:[0,1] neg_hi:[0,1]) whose
+// low result a later 32-bit VALU op reads: under co-residency that read
+// returned the register's pre-subtract value.  Built with -fno-slp-vectorize
+// (ops/build.py PER_FILE_FLAGS; no cross-half packed FP32 in the kernel) the
+// same launches ran 10000 calls at two workgroups per CU with 0 mismatches,
+// against 100 mismatches of the SLP build in the same session
+// (profiles/r6_oneshot_race_root_cause.jsonl, r6h).  The LDS floor
+// (g_os_lds_floor) is a measured performance choice again.
 constexpr int OS_PROBE_WORDS = 1024;  // race-probe record per workgroup (int32 words)
 
 __device__ __forceinline__ uint32_t os_hash16(const bf16x8& v) {  // race probe: a 16-B read's fingerprint
@@ -88,20 +101,11 @@ __device__ __forceinline__ uint32_t os_hash16(const bf16x8& v) {  // race probe:
 __device__ __forceinline__ void os_image_sync() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  // one barrier more before the first read (see "Retiring the image"): with a
-  // second workgroup on the CU, a ds_read right after the wait + ONE barrier
-  // saw pre-DMA bytes in ~2 % of calls
-  __builtin_amdgcn_s_barrier();
 }
-// the round-4/5 sequence: the wait and one barrier (race probe ABL 16384 only)
-__device__ __forceinline__ void os_image_sync_1() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-// race-probe variants of the image sync, each with ONE barrier (ABL 2048 / 4096 /
-// 8192 / 16384): composable_kernel's separate vmcnt(0) then lgkmcnt(0); vmcnt(0)
-// alone (ck_tile); the merged wait plus a short s_sleep (a pure delay); the
-// round-4/5 merged wait (profiles/r6_oneshot_race_root_cause.jsonl)
+// race-probe variants of the image sync (ABL 2048 / 4096 / 8192 / 16384):
+// composable_kernel's separate vmcnt(0) then lgkmcnt(0); vmcnt(0) alone
+// (ck_tile); the wait plus a short s_sleep (a pure delay); the wait and two
+// barriers (profiles/r6_oneshot_race_root_cause.jsonl)
 template <int ABL>
 __device__ __forceinline__ void os_image_sync_v() {
   if constexpr ((ABL & 2048) != 0) {
@@ -114,7 +118,8 @@ __device__ __forceinline__ void os_image_sync_v() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_sleep 1" ::: "memory");
     __builtin_amdgcn_s_barrier();
   } else if constexpr ((ABL & 16384) != 0) {
-    os_image_sync_1();
+    os_image_sync();
+    __builtin_amdgcn_s_barrier();
   } else {
     os_image_sync();
   }
@@ -481,6 +486,25 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
           mean = st_lds[ml * 2 + 0];
           rstd = st_lds[ml * 2 + 1];
         }
+        if constexpr ((ABL & 32768) != 0) {  // race probe: the epilogue's inputs of this (tile, lane)
+          float* d32 = slab + ((size_t)lg * 2 + (q & 1)) * 64 * 24 + lane * 24;
+          d32[0] = v[0];
+          d32[1] = v[1];
+          d32[2] = v[2];
+          d32[3] = v[3];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            d32[4 + w] = st_lds[((w * MT + t) * 2 + 0) * 16 + fr];
+            d32[8 + w] = st_lds[((w * MT + t) * 2 + 1) * 16 + fr];
+          }
+          d32[12] = shift[t];
+          d32[13] = mean;
+          d32[14] = rstd;
+          d32[15] = (float)q;
+          d32[16] = __int_as_float((int)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+          d32[17] = __int_as_float((int)__builtin_amdgcn_s_getreg((31 << 11) | 20));
+          d32[18] = __int_as_float(wave);
+        }
         if constexpr (NORM == 2) {
           if (pre) {
             v = rstd * (v - mean * (n < N ? pre_cs[k] : f32x4{0.f, 0.f, 0.f, 0.f}));
@@ -510,6 +534,7 @@ __global__ __launch_bounds__(256, 2) void gemm_oneshot_kernel(const uint8_t* __r
       }
     }
   }
+  if constexpr ((ABL & 65536) != 0) __syncthreads();  // race probe: no wave leaves before the epilogue is done
   if constexpr ((ABL & 256) != 0) {
     if (tid == 0) {
       int* rec = reinterpret_cast<int*>(slab) + (size_t)lg * OS_PROBE_WORDS;

@@ -542,14 +542,15 @@ static int launch_stream_mt(const void* A, int lda_b, const void* Wsh, const flo
 // LDS steps per wave, split-K); the plan below is fitted to
 // bench/oneshot_sweep.py, and dnn_gemm_set_oneshot can pin a config (A/B).
 static int g_os_on = 1;                             // 0 off, 1 planned shapes, 2 every eligible shape (tests)
-// LDS floor of a one-shot launch: above half the CU's 160 KB, so one workgroup
-// per CU.  The race screen (bench/probes/epi_race_screen.py) found one
-// workgroup's statistics off by a few ulp in ~1 of 150 calls only in grids
-// that put two workgroups with LDS-DMA images on one CU (forced 2/1/1 at
-// N = 2304 / 3072: 288 / 384 workgroups), never in the planned grids (<= 256
-// workgroups); profiles/r5_oneshot_race_screen*.jsonl.  0 = the kernel's own
-// size (A/B).
-static int g_os_lds_floor = 82 * 1024;
+// LDS floor of a one-shot launch (bytes; 0 = the kernel's own size, so two
+// workgroups may share a CU).  Rounds 5-6 kept it above half the CU's 160 KB
+// (one workgroup per CU) against a rare few-ulp error seen only with two
+// workgroups per CU; that error was the SLP vectoriser's packed subtract
+// (gemm_oneshot.h "The race of rounds 5-6", the library now builds this file
+// with -fno-slp-vectorize), and the floor measured neutral both ways
+// (GPT-2 decode 0.5662 vs 0.5674 ms, XL fp8 3.8187 vs 3.8196 ms,
+// profiles/r6_oneshot_race_root_cause.md), so it is off.
+static int g_os_lds_floor = 0;
 extern "C" int dnn_gemm_set_oneshot_lds_floor(int bytes) {
   g_os_lds_floor = bytes < 0 ? 0 : bytes;
   return 0;
@@ -665,7 +666,7 @@ static int launch_os_cfg(const void* A, int lda_b, const void* Wsh, const float*
                        g_epi_pre);                                                                                \
     return (int)hipGetLastError();                                                                                \
   }
-        OSP(256) OSP(1024) OSP(2048) OSP(4096) OSP(8192) OSP(16384)
+        OSP(256) OSP(2048) OSP(16384) OSP(32768) OSP(65536)
 #undef OSP
         return -2;
       }

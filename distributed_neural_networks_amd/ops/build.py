@@ -26,12 +26,21 @@ LIB_PATH = os.path.join(PKG, "_dnn_hip" + EXT_SUFFIX)
 
 TRANSFORMER_SRCS = ("norm_embed.hip", "attention.hip", "sampler.hip", "gemm_fp8.hip")
 # ReLU/max-pool epilogues: no NaN-canonicalising v_max before every fmaxf of an MFMA result
+# No SLP vectoriser where it packs scalar FP32 into cross-half v_pk_*_f32 (op_sel
+# reads of a pair's other half) whose low result a 32-bit VALU op reads: under two
+# workgroups per CU that read returned the pre-op value in lanes 48-63 (the
+# one-shot GEMM's row statistics, csrc/kernels/gemm_oneshot.h "The race of rounds
+# 5-6"; 100 -> 0 mismatches in 10000 calls, profiles/r6_oneshot_race_root_cause.md).
+# Explicit vector code keeps its packed ops.
+NO_SLP = ["-fno-slp-vectorize"]
 PER_FILE_FLAGS = {"cifar_fused.hip": ["-ffast-math"],
                   # fp32-accurate split path: keep IEEE rounding, only drop NaN canonicalisation in fmaxf
                   "cifar_x3.hip": ["-fno-honor-nans"],
                   # flash / decode softmax maxima over MFMA results: no v_max canonicalise
                   # per score (52 -> 17 v_max per GPT-2 flash block); -inf masking is kept
-                  "attention.hip": ["-fno-honor-nans"]}
+                  "attention.hip": ["-fno-honor-nans"] + NO_SLP,
+                  "gemm_skinny.hip": NO_SLP,
+                  "gemm_bf16.hip": NO_SLP}
 
 
 def _hipcc() -> str:

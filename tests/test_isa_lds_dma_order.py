@@ -12,10 +12,15 @@ XL decode configurations and the forced test shapes) and of the fused LM head
 that no LDS read follows an LDS-DMA without a vmcnt(0) and then an s_barrier
 in between.  The round-4/5 counted-wait variant (probe bit ABL 128) is
 compiled too and must be flagged, so the check is known to see what it
-guards.  (The GPU-side screen for the same kernel is
-bench/probes/epi_race_screen.py; its findings, including the one-workgroup-
-per-CU LDS floor, are in docs/ARCHITECTURE.md and
-profiles/r5_oneshot_race_screen_*.jsonl.)
+guards.
+
+The same assembly (built with the library's own flags, ops/build.py) must hold
+no cross-half packed FP32 op (v_pk_*_f32 ... op_sel:[...]): the SLP
+vectoriser's packed subtracts in the row statistics were the rounds-5/6 "race"
+(gemm_oneshot.h "The race of rounds 5-6", profiles/r6_oneshot_race_root_cause.md);
+an SLP build of the same kernels must show them, so that check also sees what
+it guards.  (The GPU-side screens: bench/probes/oneshot_race_probe.py and
+tests/test_stream_gemm_gpu.py::test_oneshot_coresident_race_screen.)
 """
 import os
 import re
@@ -30,8 +35,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 # <MT, NTW, W8, NORM, ACT, SPLIT, STEPS>: gemm_skinny.hip os_plan (planned
 # shapes and the forced "every eligible shape" mode the GPU tests use)
-RACY = [(2, 1, "false", 2, "ACT_GELU", "false", 1, 128), (1, 2, "true", 0, "ACT_NONE", "false", 2, 128),
-        (2, 1, "false", 2, "ACT_GELU", "false", 1, 16384)]
+RACY = [(2, 1, "false", 2, "ACT_GELU", "false", 1, 128), (1, 2, "true", 0, "ACT_NONE", "false", 2, 128)]
 CONFIGS = [
     (2, 2, "false", 2, "ACT_NONE", "false", 1),   # GPT-2 c_attn (folded LN)
     (2, 2, "false", 2, "ACT_GELU", "false", 1),   # GPT-2 c_fc (folded LN + GELU)
@@ -54,7 +58,25 @@ void* isa_keep[] = {{ {items} }};
 """
 
 
-def _asm():
+def _lib_flags():
+    import sys
+    sys.path.insert(0, ROOT)
+    from distributed_neural_networks_amd.ops.build import PER_FILE_FLAGS
+    return PER_FILE_FLAGS["gemm_skinny.hip"]
+
+
+_ASM = {}
+
+
+def _asm(extra=None):
+    extra = _lib_flags() if extra is None else extra
+    key = " ".join(extra)
+    if key not in _ASM:
+        _ASM[key] = _asm_build(extra)
+    return _ASM[key]
+
+
+def _asm_build(extra):
     items = ", ".join([f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}>"
                        for mt, ntw, w8, norm, act, split, steps in CONFIGS] +
                       [f"(void*)&gemm_oneshot_kernel<{mt}, {ntw}, {w8}, {norm}, {act}, {split}, {steps}, {abl}>"
@@ -65,7 +87,8 @@ def _asm():
     with open(src, "w") as f:
         f.write(SRC.format(items=items))
     r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                        "-I" + os.path.join(ROOT, "csrc"), "-Wno-unused-result", "-Wno-pass-failed", "-o", out, src],
+                        "-I" + os.path.join(ROOT, "csrc"), "-Wno-unused-result", "-Wno-pass-failed"] + list(extra) +
+                       ["-o", out, src],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     with open(out) as f:
@@ -102,7 +125,7 @@ def _kernels(text, kernel="gemm_oneshot_kernel", raw=False):
 
 def _product(ks):
     """Drop the probe instantiations (ABL != 0: a ninth template argument)."""
-    return {n: q for n, q in ks.items() if not re.search(r"ELi(128|16384)EE", n)}
+    return {n: q for n, q in ks.items() if not re.search(r"ELi128EE", n)}
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
@@ -149,10 +172,7 @@ def _unretired_reads(lines, barriers: int = 1):
             succ.append(([tgt] if tgt is not None else []) + (nxt if m.group(1) else []))
         else:
             succ.append(nxt)
-    # state: 0 clear, 1 DMA waited for (vmcnt(0)) but fewer than ``barriers``
-    # barriers since, 2 DMA pending; a block's entry state is the worst over
-    # its predecessors (``barriers`` = 2 for the one-shot image: one barrier
-    # more than the wait + barrier, gemm_oneshot.h "Retiring the image")
+    # a block's entry state is the worst over its predecessors;
     # encoded state: 0 clear, 2 + barriers pending, or 1 .. barriers (barriers still needed
     # after the wait); a higher value is worse
     top = barriers + 1
@@ -185,15 +205,31 @@ def test_lds_dma_images_retired_before_reads():
         assert len(ks) == n, (kernel, sorted(ks))
         for name, seq in ks.items():
             assert any("global_load_lds" in t for t in seq), name
-            # the one-shot image: the wait and TWO barriers before the first read
-            bad = _unretired_reads(seq, 2 if kernel == "gemm_oneshot_kernel" else 1)
+            bad = _unretired_reads(seq, 1)
             assert not bad, f"{name}: {len(bad)} LDS reads before the image DMA is retired: {bad[:3]}"
     # the racy variants must be flagged (the check sees the bug): the counted
-    # wait (ABL 128) at any barrier count, the round-4/5 wait + one barrier
-    # (ABL 16384) at two
+    # wait (ABL 128)
     racy = {n: q for n, q in _kernels(text, raw=True).items() if n not in _product({n: q})}
     assert len(racy) == len(RACY), sorted(racy)
     for name, seq in racy.items():
-        assert _unretired_reads(seq, 2), f"{name}: racy variant not flagged"
-        if "ELi128EE" in name:
-            assert _unretired_reads(seq, 1), f"{name}: counted-wait variant not flagged"
+        assert _unretired_reads(seq, 1), f"{name}: counted-wait variant not flagged"
+
+PK_CROSS = re.compile(r"^v_pk_\w+_f32\b.*\bop_sel:\[")
+
+
+def _cross_half(text):
+    return {n: [t for t in seq if PK_CROSS.match(t)] for n, seq in _product(_kernels(text, raw=True)).items()}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_oneshot_no_cross_half_packed_fp32():
+    """The one-shot kernels as the library builds them hold no cross-half
+    packed FP32 op; the same source with the SLP vectoriser on does (the
+    row-statistics subtracts), so the check sees what it guards."""
+    assert "-fno-slp-vectorize" in _lib_flags()
+    got = _cross_half(_asm())
+    assert len(got) == len(CONFIGS), sorted(got)
+    bad = {n: v[:2] for n, v in got.items() if v}
+    assert not bad, bad
+    slp = _cross_half(_asm(["-fslp-vectorize"]))
+    assert sum(bool(v) for v in slp.values()) >= 1, "the SLP control build shows no cross-half packed op"
