@@ -61,6 +61,9 @@ def parse(argv=None):
                     help="after the timed run: greedy tokens of this many steps of the distributed ring on fixed "
                          "seeded prompts, against the same stages colocated on rank 0's device "
                          "(-1 = 8 when the ring spans several GPU groups, else 0)")
+    ap.add_argument("--lat_rounds", type=int, default=LAT_ROUNDS,
+                    help="synced single-round latency samples after the timed rounds (0: none, so a kernel trace "
+                         "of the decode region holds only the timed multi-step graphs)")
     ap.add_argument("--verify_prompt", type=int, default=64, help="prompt length of the --verify_steps check")
     ap.add_argument("--prepost_ab", type=int, default=0,
                     help="after the timed run: this many interleaved A/B pairs of decode runs without / with "
@@ -192,7 +195,8 @@ def run(args=None, shutdown: bool = True):
     M = args.microbatches or groups
     B = args.batch
     T0 = args.prompt
-    total_steps = args.warmup + args.steps + LAT_ROUNDS + 2  # + the latency rounds + graph-capture slack
+    lat_rounds = getattr(args, "lat_rounds", LAT_ROUNDS)
+    total_steps = args.warmup + args.steps + lat_rounds + 2  # + the latency rounds + graph-capture slack
     max_seq = T0 + total_steps + 1
     fp8 = args.dtype == "fp8"
     kv = getattr(args, "kv", "bf16")
@@ -259,14 +263,14 @@ def run(args=None, shutdown: bool = True):
     # time between group 0's consecutive post-round syncs is one token.
     lat = []
     if groups == 1 and ring is not None:
-        for _ in range(LAT_ROUNDS):
+        for _ in range(lat_rounds):
             ta = sync()
             ring.decode_round()
             lat.append(sync() - ta)
     elif ring is not None:
         comm.barrier(info)
         stamps = []
-        for _ in range(LAT_ROUNDS):
+        for _ in range(lat_rounds):
             ring.decode_round([0])
             if grp == 0:
                 if dev.type == "cuda":

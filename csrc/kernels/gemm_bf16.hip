@@ -217,6 +217,15 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, int l
 // per tile), a load under a branch being waited for at the merge.  Addresses
 // past the matrix clamp to its last 16 B (host/kernel: N % 4 == 0, M even,
 // 16-B aligned vectors; those columns / rows are never stored).
+// Anatomy probe of the 256^2 kernels (bench/probes/gemm_anatomy.py; 0 in every
+// product launch): bit 1 skips the epilogue's stores (the accumulators stay
+// live through one sentinel compare), bit 2 skips the main loop (prologue DMAs,
+// their wait and the epilogue only) -- what a tile's fixed cost is made of
+// (profiles/r6_gemm_anatomy.jsonl: ~8-10 us of stores per tile at M = 32768;
+// row-staged, non-temporal or start-staggered stores were measured and
+// reverted, docs/ARCHITECTURE.md "Tried and reverted").
+__device__ int g_gemm_anatomy = 0;
+
 constexpr int EPI_LDS = 5 * 1024;
 constexpr int EPI_B = 0, EPI_C = 1024, EPI_RS = 2048, EPI_SA = 4096;  // byte offsets
 
@@ -335,6 +344,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / BG_K;
+  const int gan = g_gemm_anatomy;
   // epilogue operands in LDS (epi_operands_dma); uniform.  SCATTER: the bias
   // is indexed by the global column (the tail launch's c_off).
   char* epi = smem + 8 * BG_HALF;
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
     bg_mfma<4, 2>(acc[1][0], af, b0);
     bg_barrier();
   };
-  int t = 0;
+  int t = (gan & 2) ? nk : 0;
   for (; t + 1 < nk; t += 2) {
     ktile(t, std::integral_constant<int, 0>{});
     ktile(t + 1, std::integral_constant<int, 1>{});
@@ -455,6 +465,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
+  if (gan & 1) {  // anatomy probe: no stores
+    if (acc[0][0][0][0][0] == 1.2345e-30f) reinterpret_cast<bf16_t*>(Cv)[0] = 0;
+    return;
+  }
 
   // Epilogue (transposed accumulators):
   //   row m = m0 + mq*128 + wr*64 + i*16 + (lane&15), cols n..n+3 with
@@ -653,6 +667,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   const int m0 = tm * BG_M, n0 = tn * TN;
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = Kb / 128;
+  const int gan = g_gemm_anatomy;
   // epilogue operands in LDS (epi_operands_dma): channel scales, bias (SCATTER:
   // by the global column), per-row activation scales (not MXA); uniform
   char* epi = smem + 8 * BG_HALF;
@@ -776,7 +791,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
     mm(acc[1][0], b0, scl[u][1]);
     bg_barrier();
   };
-  int t = 0;
+  int t = (gan & 2) ? nk : 0;
   for (; t + 1 < nk; t += 2) {
     ktile(t, std::integral_constant<int, 0>{});
     ktile(t + 1, std::integral_constant<int, 1>{});
@@ -785,6 +800,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bg_barrier();
+  if (gan & 1) {  // anatomy probe: no stores
+    if (acc[0][0][0][0][0] == 1.2345e-30f) C[0] = 0;
+    return;
+  }
 
   if constexpr (QOUT) {
     // bias + GELU in place, then per (row, 128-column half nq) amax: the lane's
@@ -964,6 +983,10 @@ static int g_res_prefetch = 1;
 extern "C" int dnn_gemm_set_res_prefetch(int on) {
   g_res_prefetch = on ? 1 : 0;
   return 0;
+}
+
+extern "C" int dnn_gemm_set_anatomy(int bits) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_anatomy), &bits, sizeof(int));
 }
 
 extern "C" int dnn_gemm_set_tile(int tile) {

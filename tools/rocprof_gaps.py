@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel-boundary cost of a decode run from a rocprofv3 ``--kernel-trace``
-database: over the kernels after the last prefill attention launch (the decode
+database or csv: over the kernels after the last prefill attention launch (the decode
 graphs), the span, the summed kernel time, the idle gaps between consecutive
 kernels (the per-launch boundary the HIP graph does not hide), and the mean
 duration and gap per kernel name.
@@ -19,6 +19,23 @@ def short(name: str) -> str:
     return re.sub(r"\(.*", "", name).replace("void ", "")[:80]
 
 
+def load(d):
+    """(name, start_ns, end_ns) sorted by start, from the sqlite database or
+    the csv kernel trace (``--output-format csv``) under ``d``."""
+    dbs = glob.glob(os.path.join(d, "**", "*results.db"), recursive=True)
+    if dbs:
+        con = sqlite3.connect(dbs[0])
+        cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
+        cs = next(c for c in cols if c.lower() in ("start", "start_ns", "begin", "begin_ns"))
+        ce = next(c for c in cols if c.lower() in ("end", "end_ns"))
+        return con.execute(f"select name, {cs}, {ce} from kernels order by {cs}").fetchall()
+    import csv
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    with open(f, newline="") as fh:
+        rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(fh)]
+    return sorted(rows, key=lambda r: r[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -26,12 +43,7 @@ def main():
     ap.add_argument("--detail", default="argmax_final",
                     help="also list every gap after the kernels matching this (sorted, us)")
     args = ap.parse_args()
-    db = glob.glob(os.path.join(args.dir, "**", "*results.db"), recursive=True)[0]
-    con = sqlite3.connect(db)
-    cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
-    cs = next(c for c in cols if c.lower() in ("start", "start_ns", "begin", "begin_ns"))
-    ce = next(c for c in cols if c.lower() in ("end", "end_ns"))
-    rows = con.execute(f"select name, {cs}, {ce} from kernels order by {cs}").fetchall()
+    rows = load(args.dir)
     last = max((i for i, r in enumerate(rows) if args.after in r[0]), default=-1)
     dec = rows[last + 1:]
     if len(dec) < 2:
