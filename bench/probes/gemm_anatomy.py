@@ -8,7 +8,7 @@ microseconds per launch and per round of 256 tiles, so a tile's fixed cost
 per-K-tile cost.  bf16 (``linear``) and fp8 (per-token scales, ``gemm_fp8``)
 arms; one JSON line per (dtype, shape).
 
-    python bench/probes/gemm_anatomy.py [--shapes MxNxK,...] [--dtypes bf16,fp8] [--act none|gelu]
+    python bench/probes/gemm_anatomy.py [--shapes MxNxK,...] [--dtypes bf16,fp8,fp8mx] [--act none|gelu]
 """
 from __future__ import annotations
 
@@ -42,13 +42,16 @@ def main():
     ap.add_argument("--shapes", default=DEFAULT)
     ap.add_argument("--dtypes", default="bf16,fp8")
     ap.add_argument("--act", default="none")
+    ap.add_argument("--residual", action="store_true", help="fp8mx: residual epilogue")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--arms", default="0,1,2,3",
-                    help="anatomy bits per arm: 0 product, 1 no stores, 2 no main loop")
+                    help="anatomy bits per arm: 0 product, 1 no epilogue (no stores), 2 no main loop, "
+                         "8 the epilogue with its plain-path stores predicated off")
     a = ap.parse_args()
     from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
-    from distributed_neural_networks_amd.ops.fp8 import kpad_of, quant_rows, quantize_weight, set_fp8_tile
+    from distributed_neural_networks_amd.ops.fp8 import (kpad_of, mx_scale_bytes, quant_rows, quant_rows_mx,
+                                                         quantize_weight, set_fp8_tile)
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
     L = lib()
     dev = torch.device("cuda", 0)
@@ -64,6 +67,23 @@ def main():
                     set_gemm_tile(256)
                     w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
                     fn = lambda: linear(x, w, None, act=a.act, out=out)  # noqa: E731
+                elif dt == "fp8mx":  # the MX W8A8 product path (GPT-2 XL prefill); GELU: quantised output (QOUT)
+                    wq = quantize_weight(torch.randn(N, K, device=dev) * 0.05, dev)
+                    kp = kpad_of(K)
+                    qb = torch.empty(M, kp, dtype=torch.uint8, device=dev)
+                    sx = torch.empty(mx_scale_bytes(M, kp), dtype=torch.uint8, device=dev)
+                    quant_rows_mx(x, qb, sx)
+                    bias = torch.randn(N, device=dev)
+                    kpo = kpad_of(N)
+                    qo = torch.empty(M, kpo, dtype=torch.uint8, device=dev) if a.act == "gelu" else None
+                    sxo = torch.empty(mx_scale_bytes(M, kpo), dtype=torch.uint8, device=dev) if qo is not None else None
+                    res_t = torch.randn(M, N, device=dev).bfloat16() if a.residual else None
+                    fn = lambda: L.gemm_fp8_mx(ptr(qb), ptr(sx), ptr(wq.q), ptr(wq.scale),  # noqa: E731
+                                               0 if qo is not None else ptr(out), N, ptr(bias),
+                                               ptr(res_t) if res_t is not None else 0, N, M, N, kp, act_code,
+                                               ptr(qo) if qo is not None else 0, kpo if qo is not None else 0,
+                                               ptr(sxo) if sxo is not None else 0, kpo if qo is not None else 0,
+                                               stream_ptr())
                 else:
                     set_fp8_tile(256)
                     wq = quantize_weight(torch.randn(N, K, device=dev) * 0.05, dev)
@@ -82,7 +102,7 @@ def main():
                         res[bits] = min(res.get(bits, 1e30), us)
                 L.gemm_set_anatomy(0)
                 rounds = -(-tiles // 256)
-                names = {0: "product", 1: "no_stores", 2: "no_main_loop", 3: "neither"}
+                names = {0: "product", 1: "no_stores", 2: "no_main_loop", 3: "neither", 8: "epilogue_no_store_instr"}
                 row = {"dtype": dt, "M": M, "N": N, "K": K, "act": a.act, "tiles": tiles, "tile_rounds": rounds,
                        "us": {names.get(b, str(b)): round(v, 2) for b, v in res.items()},
                        "us_per_round": {names.get(b, str(b)): round(v / rounds, 2) for b, v in res.items()},

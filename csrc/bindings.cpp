@@ -115,6 +115,7 @@ PYBIND11_MODULE(_dnn_hip, m) {
   });
   m.def("gemm_set_tile", [](int tile) { return dnn_gemm_set_tile(tile); });
   m.def("gemm_set_anatomy", [](int bits) { return dnn_gemm_set_anatomy(bits); });
+  m.def("gemm_set_skinny_pin", [](int id, int ks, int n, int k) { return dnn_gemm_set_skinny_pin(id, ks, n, k); });
   m.def("gemm_set_half_cost", [](float c) { return dnn_gemm_set_half_cost(c); });
   m.def("gemm_bf16_qkv_scatter", [](u64 A, int lda, u64 W, int ldw, u64 bias, u64 rowstat, u64 colsum, u64 q, u64 kc,
                                     u64 vc, u64 pos, int B, int T, int H, int Hkv, int hd, int S, int K, u64 st) {

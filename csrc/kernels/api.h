@@ -15,6 +15,7 @@ int dnn_gemm_bf16(const void* A, int lda, const void* W, int ldw, void* C, int l
 int dnn_row_stats(const void* x, int ldx, float* stats, int M, int N, float eps, int rms, hipStream_t st);
 int dnn_gemm_set_tile(int tile);
 int dnn_gemm_set_anatomy(int bits);
+int dnn_gemm_set_skinny_pin(int id, int ks, int n, int k);
 int dnn_gemm_bf16_qkv_scatter(const void* A, int lda, const void* W, int ldw, const float* bias, const float* rowstat,
                               const float* colsum, void* q, void* kc, void* vc, const int* pos, int B, int T, int H,
                               int Hkv, int hd, int S, int K, hipStream_t st);

@@ -220,7 +220,8 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, int l
 // Anatomy probe of the 256^2 kernels (bench/probes/gemm_anatomy.py; 0 in every
 // product launch): bit 1 skips the epilogue's stores (the accumulators stay
 // live through one sentinel compare), bit 2 skips the main loop (prologue DMAs,
-// their wait and the epilogue only) -- what a tile's fixed cost is made of
+// their wait and the epilogue only), bit 8 runs the whole epilogue but
+// predicates its plain-path stores off -- what a tile's fixed cost is made of
 // (profiles/r6_gemm_anatomy.jsonl: ~8-10 us of stores per tile at M = 32768;
 // row-staged, non-temporal or start-staggered stores were measured and
 // reverted, docs/ARCHITECTURE.md "Tried and reverted").
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
           // past N, wave-uniformly)
           if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias_e, lane, scat);
         } else if (!OUT_F32 && pair && nb + 31 < N) {
-          epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, M, reinterpret_cast<bf16_t*>(Cv), ldc,
+          epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, (gan & 8) ? 0 : M, reinterpret_cast<bf16_t*>(Cv), ldc,
                              bias_e, R, ldr, lane);
         } else {
 #pragma unroll
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
           epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane, rr[mq][nq][i][0],
                                    rr[mq][nq][i][1]);
         } else if (pair && nb + 31 < N) {
-          epi_pair_bf16<ACT>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane);
+          epi_pair_bf16<ACT>(v[0], v[1], m, nb, (gan & 8) ? 0 : M, C, ldc, bias_e, R, ldr, lane);
         } else {
 #pragma unroll
           for (int j = 0; j < 2; ++j)

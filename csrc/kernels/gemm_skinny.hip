@@ -175,7 +175,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint8_t* __restr
   // and the wide ones spilled with it)
   constexpr bool PRE = NT <= 2 && MT * NT * U <= 8 && !PIPE && !OUT_F32 && !FP8 && ACT != ACT_SILU_MUL;
   constexpr int NP = PRE ? NT : 1;
-  const bool pre = PRE && epi_pre && wave < MT && (N & 3) == 0 && epi_vec_ok(Cv, ldc, bias, R, ldr) &&
+  // (MT <= waves: wave t owns M tile t alone in the epilogue loop below, so its
+  // prefetched operands are that tile's)
+  const bool pre = PRE && epi_pre && wave < MT && MT * 64 <= (int)blockDim.x && (N & 3) == 0 &&
+                   epi_vec_ok(Cv, ldc, bias, R, ldr) &&
                    ((reinterpret_cast<uintptr_t>(sw) | reinterpret_cast<uintptr_t>(colsum)) & 15) == 0;
   // unconditional loads (dummy address for absent operands; ``pre`` and
   // has_b / has_r decide use): a load under a branch is waited for at the merge
@@ -814,6 +817,21 @@ extern "C" int dnn_gemm_set_stream(int on, long long min_bytes, int fold) {
 //   M <= 64    : by N class (wide >= 16K / mid / narrow <= 4K): 4 / 2 / 1 column
 //                tiles x 2 chunks, 4 waves (activation re-reads dominate as M
 //                grows, so narrow N keeps one column tile for more workgroups)
+// A/B pin of the M 17..64 bf16 fragment-order configuration (bench/probes/decode_ab.py
+// --switch skinny_pin): one of the table's template configurations with any wave
+// count, for the calls of width N (0: every width); id 0 = the table below.
+// A pinned shape also bypasses the one-shot and stream plans (k: its K in
+// elements, 0 = any).
+struct SkinnyPin {
+  int id = 0, ks = 4, n = 0, k = 0;
+};
+static SkinnyPin g_skinny_pin;
+extern "C" int dnn_gemm_set_skinny_pin(int id, int ks, int n, int k) {
+  if (id < 0 || id > 6 || ks < 1 || ks > 8) return -1;
+  g_skinny_pin = SkinnyPin{id, ks, n, k};
+  return 0;
+}
+
 template <int ACT, bool F32, bool FP8, int MT, int NT, int U, bool PIPE, int NORM, bool W8, bool MS = false>
 static int launch_skinny_cfg(const void* A, int lda_b, const float* sa, const void* W, int ldw_b, const float* sw,
                              void* C, int ldc, const float* bias, const void* R, int ldr, int M, int N, int kbytes,
@@ -843,7 +861,9 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   g_rs_cur = g_rs_req;
   g_rs_req = RowStatReq{};
   g_rs_written = 0;
-  if constexpr (!F32 && !FP8 && ACT != ACT_RELU) {
+  const bool pin_any = g_skinny_pin.id != 0 && (g_skinny_pin.n == 0 || g_skinny_pin.n == N) &&
+                       (g_skinny_pin.k == 0 || g_skinny_pin.k * 2 == kbytes);
+  if constexpr (!F32 && !FP8 && ACT != ACT_RELU) if (!pin_any) {
     OsCfg oc;
     if (os_eligible<ACT, NORM, W8>(A, lda_b, Wsh, M, kbytes) && os_plan<W8>(M, N, kbytes, ws != nullptr, ws_bytes, oc))
       return launch_os<ACT, NORM, W8>(oc, A, lda_b, Wsh, sw, C, ldc, bias, R, ldr, M, N, kbytes, colsum, eps, st, ws);
@@ -865,6 +885,21 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
   return launch_skinny_cfg<ACT, F32, FP8, 1, NTV, UV, PV, NORM, W8, true>(A, lda_b, sa, W, ldw_b, sw, C, ldc, bias, \
                                                                            R, ldr, M, N, kbytes, KSV, colsum, eps, st, \
                                                                            Wsh)
+  const bool pinned = g_skinny_pin.id != 0 && !FP8 && !W8 && Wsh != nullptr && M > 16 && M <= 64 &&
+                      (g_skinny_pin.n == 0 || g_skinny_pin.n == N) &&
+                      (g_skinny_pin.k == 0 || g_skinny_pin.k * 2 == kbytes);
+  if (pinned) {
+    const int pk = g_skinny_pin.ks;
+    switch (g_skinny_pin.id) {  // (MT, NT, U, PIPE) / M-split (NT, U, PIPE) of the table
+      case 1: CFG(2, 1, 2, false, pk);
+      case 2: CFG(2, 1, 8, false, pk);
+      case 3: CFG(2, 2, 2, true, pk);
+      case 4: CFG(2, 4, 2, false, pk);
+      case 5: CFG_MS(2, 4, false, pk);
+      case 6: CFG_MS(1, 4, false, pk);
+      default: break;
+    }
+  }
   // medium M (64, 256], decode of larger batches: always the M split, one
   // 16-row tile per workgroup; the weight slice of a column tile is re-read
   // from its XCD's L2 by the M tiles (the 128^2 GEMM would launch only a
@@ -907,6 +942,8 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
       CFG(4, 4, 2, false, 2);
     }
     if (N <= 1024) CFG_MS(1, 4, false, 4);
+    // (8-wave variants of the Llama-3 8B B=32 QKV / O rules below measured within
+    // noise in one process, decode_ab.py --switch skinny_pin, profiles/r6_llama_skinny_pin.jsonl)
     if (!W8 && N > 4096 && M <= 32) CFG(2, 2, 2, true, 4);  // Llama QKV (6144)
     if (W8 && N > 4096) CFG_MS(4, 2, false, 4);
     if (kbytes >= 8192) CFG_MS(2, 4, false, 4);
