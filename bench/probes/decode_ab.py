@@ -72,8 +72,9 @@ def apply(switch: str, v: int) -> None:
     elif switch == "multistep":  # K decode rounds per HIP graph (runtime/scheduler.py DecodeRing multi_step)
         os.environ["DNN_DECODE_MULTISTEP"] = str(v)
     elif switch == "skinny_pin":  # M 17..64 skinny config: v = id*1000 + ks*100 + shape (gemm_skinny.hip SkinnyPin)
-        # shapes (N, K): 1 Llama-3 8B QKV, 2 its O projection, 3 its down projection (bypasses the stream plan)
-        n, k = {0: (0, 0), 1: (6144, 4096), 2: (4096, 4096), 3: (4096, 14336)}[v % 100]
+        # shapes (N, K): 1 Llama-3 8B QKV, 2 its O projection, 3 its down projection (bypasses the stream plan),
+        # 4 GPT-2 c_proj
+        n, k = {0: (0, 0), 1: (6144, 4096), 2: (4096, 4096), 3: (4096, 14336), 4: (768, 3072)}[v % 100]
         assert lib().gemm_set_skinny_pin(v // 1000, (v // 100) % 10 or 4, n, k) == 0
     elif switch == "argmax_split":
         from distributed_neural_networks_amd.ops import transformer_ops
