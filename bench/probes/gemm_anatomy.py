@@ -42,11 +42,12 @@ def main():
     ap.add_argument("--shapes", default=DEFAULT)
     ap.add_argument("--dtypes", default="bf16,fp8")
     ap.add_argument("--act", default="none")
-    ap.add_argument("--residual", action="store_true", help="fp8mx: residual epilogue")
+    ap.add_argument("--residual", action="store_true", help="bf16 / fp8mx: residual epilogue")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--arms", default="0,1,2,3",
                     help="anatomy bits per arm: 0 product, 1 no epilogue (no stores), 2 no main loop, "
+                         "4 the residual by per-lane gathers (no LDS-DMA tile), "
                          "8 the epilogue with its plain-path stores predicated off")
     a = ap.parse_args()
     from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
@@ -66,7 +67,8 @@ def main():
                 if dt == "bf16":
                     set_gemm_tile(256)
                     w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
-                    fn = lambda: linear(x, w, None, act=a.act, out=out)  # noqa: E731
+                    rb = torch.randn(M, N, device=dev).bfloat16() if a.residual else None
+                    fn = lambda: linear(x, w, None, act=a.act, residual=rb, out=out)  # noqa: E731
                 elif dt == "fp8mx":  # the MX W8A8 product path (GPT-2 XL prefill); GELU: quantised output (QOUT)
                     wq = quantize_weight(torch.randn(N, K, device=dev) * 0.05, dev)
                     kp = kpad_of(K)
@@ -102,7 +104,8 @@ def main():
                         res[bits] = min(res.get(bits, 1e30), us)
                 L.gemm_set_anatomy(0)
                 rounds = -(-tiles // 256)
-                names = {0: "product", 1: "no_stores", 2: "no_main_loop", 3: "neither", 8: "epilogue_no_store_instr"}
+                names = {0: "product", 1: "no_stores", 2: "no_main_loop", 3: "neither", 4: "residual_gathers",
+                         8: "epilogue_no_store_instr"}
                 row = {"dtype": dt, "M": M, "N": N, "K": K, "act": a.act, "tiles": tiles, "tile_rounds": rounds,
                        "us": {names.get(b, str(b)): round(v, 2) for b, v in res.items()},
                        "us_per_round": {names.get(b, str(b)): round(v / rounds, 2) for b, v in res.items()},

@@ -221,7 +221,8 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, int l
 // product launch): bit 1 skips the epilogue's stores (the accumulators stay
 // live through one sentinel compare), bit 2 skips the main loop (prologue DMAs,
 // their wait and the epilogue only), bit 8 runs the whole epilogue but
-// predicates its plain-path stores off -- what a tile's fixed cost is made of
+// predicates its plain-path stores off, bit 4 reads the residual by per-lane
+// gathers instead of the LDS-DMA tile -- what a tile's fixed cost is made of
 // (profiles/r6_gemm_anatomy.jsonl: ~8-10 us of stores per tile at M = 32768;
 // row-staged, non-temporal or start-staggered stores were measured and
 // reverted, docs/ARCHITECTURE.md "Tried and reverted").
@@ -534,6 +535,27 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
   // first output is computed, so the tile pays one memory round trip for R
   // instead of one per output row group (-20..-25 % GEMM throughput otherwise,
   // profiles/archive/r2_gemm_epilogue_cost.jsonl).
+  if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + TN - 1 < N && (gan & 4) == 0 &&
+      (ldr & 7) == 0 && (reinterpret_cast<uintptr_t>(R) & 15) == 0) {
+    // the residual tile by LDS-DMA into the dead operand buffers (res_tile_dma;
+    // anatomy bit 4 = the per-lane gathers below)
+    __syncthreads();  // every wave past its last operand read and DMA (vmcnt(0) above)
+    res_tile_dma<TN>(R, ldr, m0, n0, M, smem, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < NQ; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rl = mq * 128 + arow + i * 16 + (lane & 15), cl = nq * 128 + wc * 32 + (lane >> 4) * 4;
+          epi_pair_bf16<ACT, true>(acc[mq][nq][i][0], acc[mq][nq][i][1], m0 + rl, n0 + nq * 128 + wc * 32, M,
+                                   reinterpret_cast<bf16_t*>(Cv), ldc, bias_e, R, ldr, lane,
+                                   res_tile_read<TN>(smem, rl, cl), res_tile_read<TN>(smem, rl, cl + 16));
+        }
+    return;
+  }
   if (res_pre && !OUT_F32 && ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + TN - 1 < N) {
     bf16x4 rr[2][NQ][4][2];
 #pragma unroll
@@ -887,8 +909,16 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
   // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
   const bool rpre = ACT != ACT_SILU_MUL && pair && R != nullptr && n0 + TN - 1 < N;
+  // the residual tile by LDS-DMA into the dead operand buffers (res_tile_dma;
+  // anatomy bit 4 = the per-lane gathers below)
+  const bool rdma = rpre && (gan & 4) == 0 && (ldr & 7) == 0 && (reinterpret_cast<uintptr_t>(R) & 15) == 0;
   bf16x4 rr[2][NQ][4][2];
-  if (rpre) {
+  if (rdma) {
+    __syncthreads();  // every wave past its last operand read and DMA (vmcnt(0) above)
+    res_tile_dma<TN>(R, ldr, m0, n0, M, smem, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if (rpre) {
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -929,6 +959,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
           if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias_e, lane, scat);
         } else if (ACT == ACT_SILU_MUL) {
           epi_silu_pair<false>(v[0], v[1], m, nb / 2, M, N / 2, C, ldc, vec, lane);
+        } else if (rdma) {
+          const int rl = m - m0, cl = nb - n0 + (lane >> 4) * 4;
+          epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane, res_tile_read<TN>(smem, rl, cl),
+                                   res_tile_read<TN>(smem, rl, cl + 16));
         } else if (rpre) {
           epi_pair_bf16<ACT, true>(v[0], v[1], m, nb, M, C, ldc, bias_e, R, ldr, lane, rr[mq][nq][i][0],
                                    rr[mq][nq][i][1]);

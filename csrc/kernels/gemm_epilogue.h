@@ -208,6 +208,32 @@ __device__ __forceinline__ void epi_pair_res_load(int m, int nb, int M, const bf
   r1 = *reinterpret_cast<const bf16x4*>(R + (size_t)mm * ldr + n0 + 16);
 }
 
+// Residual tile of a 256-row GEMM tile by LDS-DMA into the dead operand LDS
+// (TN columns, whole rows: one wave-instruction = 1 KB = 1024 / (2 TN) rows),
+// 16-B chunk p of row r holding logical chunk p ^ (r & (TN/8 - 1)) (the global
+// address is permuted, the LDS write stays lane-linear), so the epilogue's
+// 8-B reads of 16 rows x one chunk hit distinct banks.  Rows past M read row
+// M - 1 (never stored).  Replaces 32 per-lane 8-B gathers at row stride per
+// lane (bench/probes/gemm_anatomy.py --residual: the residual read was ~11 us
+// of a 40 us fp8 tile round).
+template <int TN>
+__device__ __forceinline__ void res_tile_dma(const bf16_t* __restrict__ R, int ldr, int m0, int n0, int M,
+                                             char* lds, int wave, int lane) {
+  constexpr int CPR = TN / 8, RPI = 1024 / (TN * 2), IPW = 256 / 8 / RPI;
+#pragma unroll
+  for (int k = 0; k < IPW; ++k) {
+    const int rl = (wave * IPW + k) * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ (rl & (CPR - 1));
+    glds16(R + (size_t)min(m0 + rl, M - 1) * ldr + n0 + c * 8, lds + (wave * IPW + k) * 1024);
+  }
+}
+// the 4 residual values of row rl, tile columns cl..cl+3 (cl % 4 == 0)
+template <int TN>
+__device__ __forceinline__ bf16x4 res_tile_read(const char* lds, int rl, int cl) {
+  constexpr int CPR = TN / 8;
+  return *reinterpret_cast<const bf16x4*>(lds + rl * (TN * 2) + (((cl >> 3) ^ (rl & (CPR - 1))) << 4) + (cl & 4) * 2);
+}
+
 template <int ACT, bool RES_PRE = false>
 __device__ __forceinline__ void epi_pair_bf16(f32x4 a0, f32x4 a1, int m, int nb, int M, bf16_t* __restrict__ C,
                                               int ldc, const float* __restrict__ bias,

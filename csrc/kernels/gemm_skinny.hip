@@ -943,7 +943,7 @@ static int launch_skinny(const void* A, int lda_b, const float* sa, const void* 
     }
     if (N <= 1024) CFG_MS(1, 4, false, 4);
     // (8-wave variants of the Llama-3 8B B=32 QKV / O rules below measured within
-    // noise in one process, decode_ab.py --switch skinny_pin, profiles/r6_llama_skinny_pin.jsonl)
+    // noise in one process, decode_ab.py --switch skinny_pin, profiles/r6_skinny_pin_ab.jsonl)
     if (!W8 && N > 4096 && M <= 32) CFG(2, 2, 2, true, 4);  // Llama QKV (6144)
     if (W8 && N > 4096) CFG_MS(4, 2, false, 4);
     if (kbytes >= 8192) CFG_MS(2, 4, false, 4);
