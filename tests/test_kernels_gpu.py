@@ -111,6 +111,54 @@ def test_gemm_bf16_256_many_tiles(M, N, K, epi, tile):
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(4400, 1536, 192), (300, 768, 768), (513, 2304, 3072)])
+@pytest.mark.parametrize("dtype", ["bf16", "fp8mx"])
+@pytest.mark.parametrize("tile", [256, 255])
+def test_gemm_256_residual_tile_dma_bit_identical(M, N, K, dtype, tile):
+    """The 256^2 / 256x128 residual epilogue with its residual tile moved by
+    LDS-DMA (gemm_epilogue.h res_tile_dma, the default) writes exactly what the
+    per-lane residual gathers wrote (anatomy bit 4), incl. partial M tiles."""
+    from distributed_neural_networks_amd.ops._lib import lib, ptr, stream_ptr
+    from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
+    from distributed_neural_networks_amd.ops.fp8 import kpad_of, mx_scale_bytes, quant_rows_mx, quantize_weight
+    torch.manual_seed(9)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    L = lib()
+    if dtype == "fp8mx":
+        if M < 256 or tile != 256:
+            pytest.skip("the MX path: 256^2 tiles, M >= 256")
+        wq = quantize_weight(w.float(), torch.device(DEV))
+        kp = kpad_of(K)
+        qb = torch.empty(M, kp, dtype=torch.uint8, device=DEV)
+        sx = torch.empty(mx_scale_bytes(M, kp), dtype=torch.uint8, device=DEV)
+        quant_rows_mx(x, qb, sx)
+
+        def run():
+            o = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            assert L.gemm_fp8_mx(ptr(qb), ptr(sx), ptr(wq.q), ptr(wq.scale), ptr(o), N, ptr(b), ptr(r), N, M, N, kp,
+                                 0, 0, 0, 0, 0, stream_ptr()) == 0
+            return o
+    else:
+        def run():
+            return linear(x, w, b, residual=r)
+    set_gemm_tile(tile)
+    try:
+        outs = []
+        for bits in (4, 0):
+            assert L.gemm_set_anatomy(bits) == 0
+            outs.append(run())
+            torch.cuda.synchronize()
+    finally:
+        L.gemm_set_anatomy(0)
+        set_gemm_tile(0)
+    assert torch.equal(outs[0], outs[1])
+    ref = x.float() @ w.float().t() + b + r.float()
+    assert _rel(outs[1], ref) < (5e-2 if dtype == "fp8mx" else 1e-2)
+
+
 @pytest.mark.parametrize("tile", [256, 255])
 def test_gemm_256_asymmetric_layout(tile):
     from distributed_neural_networks_amd.ops.gemm import linear, set_gemm_tile
