@@ -287,15 +287,25 @@ struct QkvScatter {
 // store count is 32 per lane and tile, so the index math avoids integer
 // division: b = m / T from the fp32 reciprocal with a one-step correction
 // (exact for m < 2^24), head / dim by shifts (hd a power of two).
-__device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c) {
+__device__ __forceinline__ int qkv_batch(const QkvScatter& sc, int m) {
   int b = (int)(((float)m + 0.5f) * sc.invT);
   b -= b * sc.T > m ? 1 : 0;
   b += (b + 1) * sc.T <= m ? 1 : 0;
+  return b;
+}
+// the cache position of row m (pos[b] + t), loaded for a lane's 8 rows before
+// the epilogue's first store: loaded per 32-column pair it waited, through the
+// in-order vmcnt, for every store issued before it
+__device__ __forceinline__ int qkv_row_pos(const QkvScatter& sc, int m) {
+  const int b = qkv_batch(sc, m);
+  return sc.pos[b] + (m - b * sc.T);
+}
+__device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c, int p) {
+  const int b = qkv_batch(sc, m);
   const int t = m - b * sc.T;
   const int hs = sc.hd_shift, hmask = (1 << hs) - 1;
   const int qw = sc.H << hs, kw = sc.Hkv << hs;
   if (c < qw) return sc.q + ((((size_t)b * sc.H + (c >> hs)) * sc.T + t) << hs) + (c & hmask);
-  const int p = sc.pos[b] + t;
   if (p >= sc.S) return nullptr;  // past the cache capacity: dropped, as in qkv_split
   const bool isk = c < qw + kw;
   const int cc = isk ? c - qw : c - qw - kw;
@@ -305,7 +315,8 @@ __device__ __forceinline__ bf16_t* qkv_dest(const QkvScatter& sc, int m, int c) 
 // One widened 16-B store per lane (as epi_pair_bf16) of a whole 32-column pair
 // to its head-major / cache destination (bias added first, no activation).
 __device__ __forceinline__ void epi_pair_scatter(f32x4 a0, f32x4 a1, int m, int nb, int M,
-                                                 const float* __restrict__ bias, int lane, const QkvScatter& sc) {
+                                                 const float* __restrict__ bias, int lane, const QkvScatter& sc,
+                                                 int p) {
   const int q = lane >> 4;
   if (bias != nullptr) {
     a0 += *reinterpret_cast<const f32x4*>(bias + nb + q * 4);
@@ -316,7 +327,7 @@ __device__ __forceinline__ void epi_pair_scatter(f32x4 a0, f32x4 a1, int m, int 
   const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
   if (m < M) {
-    bf16_t* d = qkv_dest(sc, m, nb + ((q & 1) << 4) + ((q >> 1) << 3));
+    bf16_t* d = qkv_dest(sc, m, nb + ((q & 1) << 4) + ((q >> 1) << 3), p);
     if (d != nullptr) *reinterpret_cast<uint4*>(d) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
   }
 }
@@ -528,6 +539,14 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
       }
   }
   const float* bias_e = badd ? nullptr : bias;
+  // SCATTER: the cache positions of the lane's 8 rows, loaded before any store (qkv_row_pos)
+  int spos[2][4] = {};
+  if constexpr (SCATTER) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) spos[mq][i] = qkv_row_pos(scat, min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1));
+  }
   const bool vec = epi_vec_ok(Cv, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(Cv, ldc, bias, R, ldr);
   // Residual epilogue: every residual load of the tile (32 x 8 B per lane, into
@@ -592,7 +611,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(
           // destination of the lane's 8 columns (host: ACT_NONE, bf16 out, no
           // residual, N % 32 == 0, hd % 8 == 0 -> a 32-column pair is whole or
           // past N, wave-uniformly)
-          if (nb < N) epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias_e, lane, scat);
+          if (nb < N)
+            epi_pair_scatter(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb + scat.c_off, M, bias_e, lane, scat,
+                             spos[mq][i]);
         } else if (!OUT_F32 && pair && nb + 31 < N) {
           epi_pair_bf16<ACT>(acc[mq][nq][i][0], acc[mq][nq][i][1], m, nb, (gan & 8) ? 0 : M, reinterpret_cast<bf16_t*>(Cv), ldc,
                              bias_e, R, ldr, lane);
@@ -905,6 +926,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
   }
   const bool badd = epv && bias != nullptr && ACT != ACT_SILU_MUL;  // uniform: bias added from the LDS copy
   const float* bias_e = badd ? nullptr : bias;
+  // SCATTER: the cache positions of the lane's 8 rows, loaded before any store (qkv_row_pos)
+  int spos[2][4] = {};
+  if constexpr (SCATTER) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) spos[mq][i] = qkv_row_pos(scat, min(m0 + mq * 128 + arow + i * 16 + (lane & 15), M - 1));
+  }
   const bool vec = epi_vec_ok(C, ldc, bias, R, ldr);
   const bool pair = vec && epi_pair_ok(C, ldc, bias, R, ldr);
   // residual rows of the whole tile in flight before the first output (as in the bf16 kernel)
@@ -956,7 +985,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(
           if (badd) v[j] += *reinterpret_cast<const f32x4*>(epi + EPI_B + 4 * (n - n0));
         }
         if (SCATTER) {
-          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias_e, lane, scat);
+          if (nb < N) epi_pair_scatter(v[0], v[1], m, nb + scat.c_off, M, bias_e, lane, scat, spos[mq][i]);
         } else if (ACT == ACT_SILU_MUL) {
           epi_silu_pair<false>(v[0], v[1], m, nb / 2, M, N / 2, C, ldc, vec, lane);
         } else if (rdma) {
