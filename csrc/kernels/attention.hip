@@ -950,7 +950,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
   static_assert(VE <= VU && VU % 2 == 0 && G <= 16, "bad shape");
   __shared__ __attribute__((aligned(16))) float sc[CAP * G];  // scaled scores, [key][head] (one LDS read per key)
   __shared__ float wmax[NW][G];        // per-wave score max per head
-  extern __shared__ __attribute__((aligned(16))) float red1p[];  // [GPB][G][HD] + [GPB][G]
+  extern __shared__ __attribute__((aligned(16))) float red1p[];  // [NW][G][HD] + [NW][G]
 
   const int bk = blockIdx.x, split = blockIdx.y, NS = gridDim.y;
   const int b = bk / Hkv, kvh = bk % Hkv;
@@ -1221,22 +1221,36 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_1p_kernel(const bf16_t* _
       }
     }
   }
-  // ---- 6. reduce over the row groups
-  float* red = red1p;                       // [GPB][G][HD]
-  float* lred = red1p + GPB * G * HD;       // [GPB][G]
+  // ---- 6. reduce over the row groups: first across the wave's 64 / LPK row
+  // groups by lane shuffles (xor LPK, 2 LPK, ...), then the NW wave sums
+  // through LDS -- [NW][G][HD] instead of [GPB][G][HD] (Llama-3 8B: 16 KB
+  // instead of 64 KB of LDS, so two GQA workgroups fit on a CU)
+  float* red = red1p;                  // [NW][G][HD]
+  float* lred = red1p + NW * G * HD;   // [NW][G]
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    f32x4* dst = reinterpret_cast<f32x4*>(red + ((size_t)grp * G + g) * HD + sub * 8);
-    dst[0] = f32x4{acc[g][0], acc[g][1], acc[g][2], acc[g][3]};
-    dst[1] = f32x4{acc[g][4], acc[g][5], acc[g][6], acc[g][7]};
-    if (sub == 0) lred[grp * G + g] = ls[g];
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] += __shfl_xor(acc[g][j], off, 64);
+      ls[g] += __shfl_xor(ls[g], off, 64);
+    }
+  }
+  if (lane < LPK) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4* dst = reinterpret_cast<f32x4*>(red + ((size_t)wave * G + g) * HD + sub * 8);
+      dst[0] = f32x4{acc[g][0], acc[g][1], acc[g][2], acc[g][3]};
+      dst[1] = f32x4{acc[g][4], acc[g][5], acc[g][6], acc[g][7]};
+      if (sub == 0) lred[wave * G + g] = ls[g];
+    }
   }
   __syncthreads();
   for (int i = tid; i < G * HD; i += NTH) {
     const int g = i / HD, d = i % HD;
     float s = 0.f, l = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < GPB; ++r) {
+#pragma unroll
+    for (int r = 0; r < NW; ++r) {
       s += red[((size_t)r * G + g) * HD + d];
       l += lred[r * G + g];
     }
@@ -1444,8 +1458,7 @@ struct Dec1pArgs {
 };
 template <int HD, int G, int NW, int KT, int VE, int VU, bool RS, int FM, bool NT, bool KNT>
 static void launch_1p_k(const Dec1pArgs& a, dim3 grid, hipStream_t st) {
-  constexpr int GPB = NW * 64 / (HD / 8);
-  const size_t smem = sizeof(float) * (size_t)GPB * G * (HD + 1);
+  const size_t smem = sizeof(float) * (size_t)NW * G * (HD + 1);  // [NW][G][HD] + [NW][G] (step 6)
   if (a.kf)
     hipLaunchKernelGGL((attn_decode_1p_kernel<HD, G, FM, NT, NW, KT, VE, VU, RS, KNT, true>), grid, dim3(NW * 64),
                        smem, st, a.q, a.ldq, a.kc, a.vc, a.ws, a.H, a.Hkv, a.S, a.lens, a.cosT, a.sinT, a.sl2, a.o);
